@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Headline benchmark: samples/s (whole node) of the toy 3-layer MLP, bf16, DDP.
+
+BASELINE.json metric: "samples/sec (whole node) + DDP scaling efficiency, toy MLP
+at 1/2/4/8 MI355X".  Config: MLP 3072→4096→4096→10 on CIFAR-shaped
+synthetic data (uint8 images resident on the GPU, RandomCrop+Flip augmentation
+each step as in the reference), batch 512 per GPU (the reference's default
+``--batch_size``), SGD lr 0.4 / momentum 0.9 / wd 5e-4 with the reference's
+one-cycle schedule, fp32 master weights and gradients, bf16 MFMA compute.
+Weak scaling: per-GPU batch fixed as N grows.
+
+    python bench.py --gpus 1 --steps 200 --warmup 30
+    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+
+Every timed step does the whole job: batch gather+augment, forward, loss,
+backward, bucketed gradient all-reduce (N>1), optimizer step and LR update.
+``--impl torch`` runs the stock PyTorch-ROCm recipe (nn.Linear + autocast,
+torch DDP over RCCL, foreach SGD) on the same data for the baseline number.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch_size", type=int, default=512, help="per-GPU batch")
+    p.add_argument("--hidden", type=int, default=4096)
+    p.add_argument("--layers", type=int, default=3)
+    p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg"])
+    p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
+    p.add_argument("--no_graph", action="store_true")
+    p.add_argument("--overlap_optimizer", action="store_true")
+    p.add_argument("--bucket_cap_mb", type=float, default=25.0)
+    p.add_argument("--first_bucket_mb", type=float, default=1.0)
+    p.add_argument("--train_size", type=int, default=50000)
+    p.add_argument("--json_out", default=None)
+    return p.parse_args()
+
+
+def baseline_value(metric_key: str):
+    try:
+        with open(BASELINE_FILE) as f:
+            b = json.load(f)
+        v = b.get("published", {}).get(metric_key) or b.get("measured_stock_pytorch", {}).get(metric_key)
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def setup_dist(n):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        if n > 1 and world == 1:
+            print(f"bench.py: --gpus {n} needs a launcher (torchrun --nproc-per-node {n})", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="cpu:gloo,cuda:nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def make_data(args, device, rank, world):
+    from ddpx.data.datasets import synthetic_cifar
+    from ddpx.data.loader import DeviceLoader
+    from ddpx.data.sampler import DistributedIndexSampler
+    ds = synthetic_cifar(args.train_size, seed=0)
+    sampler = DistributedIndexSampler(len(ds), world, rank, shuffle=True, seed=0)
+    layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
+    return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
+
+
+def build_ddpx(args, device, world):
+    from ddpx.models import build_model
+    from ddpx.optim.schedule import one_cycle, resolve_steps_per_epoch
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import RcclComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from ddpx.runtime.setup import prepare_model
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16" if args.model != "vgg"
+                        else "fp32", device=device)
+    prepare_model(model, device)
+    opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph)
+    net = model
+    if world > 1:
+        net = DistributedDataParallel(model, comm=RcclComm(device), bucket_cap_mb=args.bucket_cap_mb,
+                                      first_bucket_mb=args.first_bucket_mb,
+                                      overlap_optimizer=args.overlap_optimizer)
+        if args.overlap_optimizer:
+            net.attach_optimizer(opt)
+    sched = one_cycle(opt, resolve_steps_per_epoch("compat", 0, world > 1))
+    return model, net, opt, sched
+
+
+def build_torch(args, device, world):
+    """Stock PyTorch-ROCm recipe (the baseline to beat)."""
+    import torch.nn as nn
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+    from ddpx.optim.schedule import OneCycleLambda, resolve_steps_per_epoch
+    if args.model == "vgg":
+        from ddpx.models import VGG
+        model = VGG().to(device)
+    else:
+        dims = [3072] + [args.hidden] * (args.layers - 1) + [10]
+        layers = []
+        for i in range(args.layers):
+            layers.append(nn.Linear(dims[i], dims[i + 1]))
+            if i < args.layers - 1:
+                layers.append(nn.ReLU())
+        model = nn.Sequential(nn.Flatten(), *layers).to(device)
+    net = TDDP(model, device_ids=[device.index]) if world > 1 else model
+    opt = torch.optim.SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, OneCycleLambda(resolve_steps_per_epoch("compat", 0, world > 1)))
+    return model, net, opt, sched
+
+
+def main():
+    args = parse()
+    rank, world, local = setup_dist(args.gpus)
+    device = torch.device("cuda", local)
+    loader = make_data(args, device, rank, world)
+    idx_all = loader._epoch_indices()
+    nb = len(loader)
+    full = [i for i in range(nb) if (i + 1) * args.batch_size <= idx_all.numel()]
+    bs = args.batch_size
+
+    if args.impl == "ddpx":
+        from ddpx.runtime.graphs import CapturedStep
+        model, net, opt, sched = build_ddpx(args, device, world)
+        static_x, static_y = loader.make_batch(idx_all[:bs], 0)
+
+        def step_body(x, y):
+            opt.zero_grad()
+            loss, _ = net.forward_loss(x, y) if hasattr(model, "forward_loss") else (
+                torch.nn.functional.cross_entropy(net(x), y), None)
+            loss.backward()
+            opt.step()
+            return loss
+
+        graph = None
+        use_graph = not args.no_graph
+
+        def one_step(k):
+            nonlocal graph
+            b = full[k % len(full)]
+            loader.make_batch(idx_all[b * bs:(b + 1) * bs], k, out=static_x, tgt=static_y)
+            opt.sync_lr()
+            if use_graph and graph is None and k >= 2:
+                graph = CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True)
+            if graph is not None:
+                loss = graph()
+            else:
+                loss = step_body(static_x, static_y)
+            sched.step()
+            return loss
+    else:
+        model, net, opt, sched = build_torch(args, device, world)
+
+        def one_step(k):
+            b = full[k % len(full)]
+            x, y = loader.make_batch(idx_all[b * bs:(b + 1) * bs], k)
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model != "vgg"):
+                out = net(x)
+            loss = torch.nn.functional.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            sched.step()
+            return loss
+
+    # warmup (includes graph capture for ddpx)
+    loss = None
+    for k in range(args.warmup):
+        loss = one_step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        loss = one_step(k)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # gloo (CPU tensor)
+        elapsed = float(t.item())
+    final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    value = world * bs * args.steps / elapsed
+    ms = elapsed / args.steps * 1000.0
+    metric = "samples_per_sec_whole_node"
+    model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}", "mlp_wide": f"wide-mlp-3072x{args.hidden}",
+                  "vgg": "vgg11-cifar"}[args.model]
+    base = baseline_value(f"{args.model}_x{world}") if args.impl == "ddpx" else None
+    rec = {
+        "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if args.model != "vgg" else "fp32",
+        "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
+        "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
+                   "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
+                   "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)", "grad_comm": "fp32",
+                   "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4)},
+    }
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "a") as f:
+                f.write(line + "\n")
+    if world > 1:
+        if args.impl == "ddpx" and hasattr(net, "close"):
+            net.close()
+            net.comm.close()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,60 @@
+// ddpx — MI355X (gfx950 / CDNA4) native kernels: shared device helpers.
+//
+// Everything here is written for CDNA4 directly: 64-lane wavefronts, MFMA
+// fragments, LDS (160 KiB/CU), 8 XCDs with private L2s.  No CUDA shims.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DDPX_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef short short8v __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+#define LDS_AS __attribute__((address_space(3)))
+
+namespace ddpx {
+
+constexpr int kWave = 64;
+constexpr int kNumXcd = 8;
+
+// bf16 <-> f32 (round-to-nearest-even; NaN kept NaN by the hardware cvt).
+__device__ __forceinline__ float bf2f(unsigned short v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;  // hipcc emits v_cvt_pk_bf16_f32 on gfx950
+  return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+// Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming §5 T1):
+// workgroups dealt round-robin over the 8 XCDs are renumbered so that each XCD
+// receives one contiguous range of logical tiles (neighbouring tiles share
+// operand panels through that XCD's L2).  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & (kNumXcd - 1);
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace ddpx

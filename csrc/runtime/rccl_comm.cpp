@@ -1,0 +1,352 @@
+// ddpx — native RCCL communicator + gradient-bucket reducer for MI355X.
+//
+// Replaces, natively, what the reference gets implicitly from PyTorch:
+//   * c10d ProcessGroupNCCL  (/root/reference/multigpu.py:32):
+//     a communicator per process group, collectives on a dedicated
+//     high-priority HIP stream ordered with events, async-error polling and a
+//     timeout watchdog that aborts the communicator.
+//   * the DDP Reducer        (/root/reference/multigpu.py:89):
+//     per-bucket ready counters; the moment a bucket's last gradient is
+//     produced, an event on the compute stream gates an all-reduce on the
+//     comm stream, so the collective overlaps the rest of backward.
+//   * _broadcast_coalesced   (SURVEY §2.2 N4): broadcasts of persistent flat
+//     buffers (no per-step flatten).
+// On ROCm the RCCL library is the one torch already loaded (same soname), so
+// there is one RCCL instance per process.  The unique id travels through the
+// c10d TCPStore (Python side).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#define DDPX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Pending {
+  hipEvent_t ev;
+  Clock::time_point t0;
+  const char* what;
+};
+
+struct Comm {
+  ncclComm_t nccl = nullptr;
+  int rank = 0, nranks = 1, device = 0;
+  hipStream_t stream = nullptr;  // dedicated comm stream (high priority)
+  // watchdog
+  std::mutex mu;
+  std::deque<Pending> pending;
+  std::vector<hipEvent_t> free_events;
+  std::thread watchdog;
+  std::atomic<bool> stop{false};
+  std::atomic<int> error{0};  // 0 ok, 1 async nccl error, 2 timeout, 3 aborted
+  double timeout_s = 0.0;
+  bool track = false;
+};
+
+int check(ncclResult_t r) { return r == ncclSuccess ? 0 : 1000 + (int)r; }
+
+void watchdog_loop(Comm* c) {
+  while (!c->stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (c->error.load()) continue;
+    ncclResult_t ae = ncclSuccess;
+    if (c->nccl && ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress) {
+      fprintf(stderr, "[ddpx rank %d] RCCL async error %d (%s); aborting communicator\n", c->rank, (int)ae,
+              ncclGetErrorString(ae));
+      c->error.store(1);
+      ncclCommAbort(c->nccl);
+      c->nccl = nullptr;
+      continue;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    while (!c->pending.empty()) {
+      Pending& p = c->pending.front();
+      hipError_t q = hipEventQuery(p.ev);
+      if (q == hipSuccess) {
+        c->free_events.push_back(p.ev);
+        c->pending.pop_front();
+        continue;
+      }
+      const double age = std::chrono::duration<double>(Clock::now() - p.t0).count();
+      if (c->timeout_s > 0 && age > c->timeout_s) {
+        fprintf(stderr, "[ddpx rank %d] collective '%s' exceeded timeout %.1fs; aborting communicator\n",
+                c->rank, p.what, c->timeout_s);
+        c->error.store(2);
+        if (c->nccl) ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+      }
+      break;
+    }
+  }
+}
+
+void track_op(Comm* c, hipStream_t s, const char* what) {
+  if (!c->track) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone) return;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipEvent_t ev;
+  if (!c->free_events.empty()) {
+    ev = c->free_events.back();
+    c->free_events.pop_back();
+  } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    return;
+  }
+  hipEventRecord(ev, s);
+  c->pending.push_back({ev, Clock::now(), what});
+}
+
+// ---------------------------------------------------------------------------
+// Reducer: gradient buckets -> all-reduce on the comm stream.
+struct Bucket {
+  void* ptr = nullptr;
+  size_t count = 0;
+  int dtype = ncclFloat32;
+  int expected = 0;
+  int pending = 0;
+  bool launched = false;
+  hipEvent_t ready = nullptr, done = nullptr;
+};
+
+struct Reducer {
+  Comm* comm = nullptr;
+  int op = ncclAvg;
+  std::vector<Bucket> buckets;
+  int launched = 0;
+};
+
+}  // namespace
+
+DDPX_API int ddpx_comm_unique_id(char* out, int nbytes) {
+  if (nbytes < (int)sizeof(ncclUniqueId)) return -1;
+  ncclUniqueId id;
+  int e = check(ncclGetUniqueId(&id));
+  if (e) return e;
+  memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+DDPX_API int ddpx_comm_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int device, int high_priority,
+                                double timeout_s, int* err) {
+  *err = 0;
+  hipError_t he = hipSetDevice(device);
+  if (he != hipSuccess) {
+    *err = (int)he;
+    return nullptr;
+  }
+  Comm* c = new Comm();
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);
+  he = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high_priority ? hi : lo);
+  if (he != hipSuccess) {
+    *err = (int)he;
+    delete c;
+    return nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(&id, uid, sizeof(id));
+  int e = check(ncclCommInitRank(&c->nccl, nranks, id, rank));
+  if (e) {
+    *err = e;
+    hipStreamDestroy(c->stream);
+    delete c;
+    return nullptr;
+  }
+  c->timeout_s = timeout_s;
+  c->track = timeout_s > 0;
+  c->watchdog = std::thread(watchdog_loop, c);
+  return c;
+}
+
+DDPX_API void* ddpx_comm_stream(void* h) { return static_cast<Comm*>(h)->stream; }
+DDPX_API int ddpx_comm_error(void* h) { return static_cast<Comm*>(h)->error.load(); }
+
+DDPX_API int ddpx_comm_destroy(void* h, int abort) {
+  Comm* c = static_cast<Comm*>(h);
+  c->stop.store(true);
+  if (c->watchdog.joinable()) c->watchdog.join();
+  int e = 0;
+  if (c->nccl) {
+    if (abort) e = check(ncclCommAbort(c->nccl));
+    else {
+      hipStreamSynchronize(c->stream);
+      e = check(ncclCommDestroy(c->nccl));
+    }
+  }
+  for (auto& p : c->pending) hipEventDestroy(p.ev);
+  for (auto ev : c->free_events) hipEventDestroy(ev);
+  hipStreamDestroy(c->stream);
+  delete c;
+  return e;
+}
+
+static hipStream_t pick_stream(Comm* c, hipStream_t s) { return s ? s : c->stream; }
+
+DDPX_API int ddpx_comm_allreduce(void* h, const void* send, void* recv, size_t count, int dtype, int op,
+                                 hipStream_t s) {
+  Comm* c = static_cast<Comm*>(h);
+  if (!c->nccl) return 3;
+  s = pick_stream(c, s);
+  int e = check(ncclAllReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, c->nccl, s));
+  track_op(c, s, "all_reduce");
+  return e;
+}
+
+DDPX_API int ddpx_comm_broadcast(void* h, const void* send, void* recv, size_t count, int dtype, int root,
+                                 hipStream_t s) {
+  Comm* c = static_cast<Comm*>(h);
+  if (!c->nccl) return 3;
+  s = pick_stream(c, s);
+  int e = check(ncclBroadcast(send, recv, count, (ncclDataType_t)dtype, root, c->nccl, s));
+  track_op(c, s, "broadcast");
+  return e;
+}
+
+DDPX_API int ddpx_comm_reduce_scatter(void* h, const void* send, void* recv, size_t recvcount, int dtype, int op,
+                                      hipStream_t s) {
+  Comm* c = static_cast<Comm*>(h);
+  if (!c->nccl) return 3;
+  s = pick_stream(c, s);
+  int e = check(ncclReduceScatter(send, recv, recvcount, (ncclDataType_t)dtype, (ncclRedOp_t)op, c->nccl, s));
+  track_op(c, s, "reduce_scatter");
+  return e;
+}
+
+DDPX_API int ddpx_comm_allgather(void* h, const void* send, void* recv, size_t sendcount, int dtype,
+                                 hipStream_t s) {
+  Comm* c = static_cast<Comm*>(h);
+  if (!c->nccl) return 3;
+  s = pick_stream(c, s);
+  int e = check(ncclAllGather(send, recv, sendcount, (ncclDataType_t)dtype, c->nccl, s));
+  track_op(c, s, "all_gather");
+  return e;
+}
+
+DDPX_API int ddpx_comm_group_start() { return check(ncclGroupStart()); }
+DDPX_API int ddpx_comm_group_end() { return check(ncclGroupEnd()); }
+
+// ---------------------------------------------------------------------------
+DDPX_API void* ddpx_reducer_create(void* comm, int nbuckets, int op) {
+  Reducer* r = new Reducer();
+  r->comm = static_cast<Comm*>(comm);
+  r->op = op;
+  r->buckets.resize(nbuckets);
+  for (auto& b : r->buckets) {
+    hipEventCreateWithFlags(&b.ready, hipEventDisableTiming);
+    hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+  }
+  return r;
+}
+
+DDPX_API int ddpx_reducer_set_bucket(void* h, int i, void* ptr, size_t count, int dtype, int expected) {
+  Reducer* r = static_cast<Reducer*>(h);
+  if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  Bucket& b = r->buckets[i];
+  b.ptr = ptr;
+  b.count = count;
+  b.dtype = dtype;
+  b.expected = expected;
+  b.pending = expected;
+  b.launched = false;
+  return 0;
+}
+
+DDPX_API int ddpx_reducer_prepare(void* h) {
+  Reducer* r = static_cast<Reducer*>(h);
+  for (auto& b : r->buckets) {
+    b.pending = b.expected;
+    b.launched = false;
+  }
+  r->launched = 0;
+  return 0;
+}
+
+static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
+  Comm* c = r->comm;
+  hipError_t he = hipEventRecord(b.ready, compute);
+  if (he != hipSuccess) return (int)he;
+  he = hipStreamWaitEvent(c->stream, b.ready, 0);
+  if (he != hipSuccess) return (int)he;
+  int e = ddpx_comm_allreduce(c, b.ptr, b.ptr, b.count, b.dtype, r->op, c->stream);
+  if (e) return e;
+  he = hipEventRecord(b.done, c->stream);
+  if (he != hipSuccess) return (int)he;
+  b.launched = true;
+  r->launched++;
+  return 0;
+}
+
+// Mark n gradients of bucket i as produced on `compute`.  Launches the bucket's
+// all-reduce when it becomes complete.  Returns 1 if launched, 0 if not yet,
+// <0 / >1 error code.
+DDPX_API int ddpx_reducer_mark_ready(void* h, int i, int n, hipStream_t compute) {
+  Reducer* r = static_cast<Reducer*>(h);
+  if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  Bucket& b = r->buckets[i];
+  if (b.launched) return -2;  // marked twice in one backward
+  b.pending -= n;
+  if (b.pending > 0) return 0;
+  if (b.pending < 0) return -3;
+  int e = launch_bucket(r, b, compute);
+  return e ? e : 1;
+}
+
+// Make `s` wait for bucket i's all-reduce (e.g. so the optimizer can update
+// that bucket's parameters while later buckets are still on the wire).
+DDPX_API int ddpx_reducer_wait_bucket(void* h, int i, hipStream_t s) {
+  Reducer* r = static_cast<Reducer*>(h);
+  Bucket& b = r->buckets[i];
+  if (!b.launched) return -1;
+  return (int)hipStreamWaitEvent(s, b.done, 0);
+}
+
+// End of backward: launch stragglers (unused parameters), then join every
+// bucket's completion into `compute`.  Returns the number of buckets that had
+// to be force-launched.
+DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
+  Reducer* r = static_cast<Reducer*>(h);
+  int forced = 0;
+  for (auto& b : r->buckets) {
+    if (!b.launched) {
+      int e = launch_bucket(r, b, compute);
+      if (e) return -1000 - e;
+      forced++;
+    }
+  }
+  for (auto& b : r->buckets) {
+    hipError_t he = hipStreamWaitEvent(compute, b.done, 0);
+    if (he != hipSuccess) return -(int)he;
+  }
+  return forced;
+}
+
+DDPX_API int ddpx_reducer_destroy(void* h) {
+  Reducer* r = static_cast<Reducer*>(h);
+  for (auto& b : r->buckets) {
+    hipEventDestroy(b.ready);
+    hipEventDestroy(b.done);
+  }
+  delete r;
+  return 0;
+}

@@ -1,0 +1,29 @@
+"""Model zoo: the reference's VGG and DeepNN, and the BASELINE MLPs."""
+from __future__ import annotations
+
+import torch
+
+from .deepnn import DeepNN
+from .mlp import MLP
+from .vgg import VGG
+
+__all__ = ["VGG", "DeepNN", "MLP", "build_model"]
+
+
+def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "native"):
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dtype == "auto":
+        dtype = "bf16" if (dev.type == "cuda" and name.startswith("mlp")) else "fp32"
+    cdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    if name == "vgg":
+        m = VGG()
+        m.use_native = False
+    elif name == "deepnn":
+        m = DeepNN()
+    elif name in ("mlp", "mlp_wide"):
+        h = hidden or (16384 if name == "mlp_wide" else 4096)
+        m = MLP(hidden=h, layers=layers, compute_dtype=cdt)
+        m.use_native = kernels == "native"
+    else:
+        raise ValueError(f"unknown model {name!r}")
+    return m

@@ -1,0 +1,95 @@
+"""Toy / wide MLP — the workload BASELINE.json's headline benchmark names.
+
+The reference defines no MLP; SURVEY §7.3 fixes the design: inputs are the
+CIFAR-shaped images flattened to 3072 features, then ``layers-1`` hidden
+``Linear → ReLU`` blocks and a ``Linear(hidden → 10)`` classifier:
+
+    toy  : 3072 → 4096 → 4096 → 10     (29.4 M params)
+    wide : 3072 → 16384 → 16384 → 10   (318.9 M params)
+
+Parameters are plain ``nn.Linear`` modules named ``fc{i}`` so a checkpoint loads
+into a vanilla torch MLP with the same names.
+
+On MI355X the whole network runs as ONE autograd node (``ddpx.ops.mlp``): bf16
+MFMA GEMMs with bias+ReLU fused in the epilogue, the classifier fused with
+softmax-cross-entropy, and a backward that writes fp32 weight gradients
+straight into the DDP bucket storage in grad-ready order.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class MLP(nn.Module):
+    def __init__(self, in_features: int = 3072, hidden: int = 4096, layers: int = 3, num_classes: int = 10,
+                 compute_dtype: torch.dtype = torch.bfloat16):
+        super().__init__()
+        if layers < 2:
+            raise ValueError("MLP needs at least 2 layers (1 hidden + classifier)")
+        dims = [in_features] + [hidden] * (layers - 1) + [num_classes]
+        for i in range(layers):
+            lin = nn.Linear(dims[i], dims[i + 1])
+            self.add_module(f"fc{i}", lin)
+        self.in_features = in_features
+        self.hidden = hidden
+        self.num_layers = layers
+        self.num_classes = num_classes
+        self.compute_dtype = compute_dtype
+        self.use_native = True
+
+    def linears(self):
+        return [getattr(self, f"fc{i}") for i in range(self.num_layers)]
+
+    def _native_ok(self, x):
+        if not (self.use_native and x.is_cuda and self.compute_dtype == torch.bfloat16):
+            return False
+        fc0 = self.fc0
+        return getattr(fc0.weight, "_ddpx_shadow", None) is not None and not x.requires_grad
+
+    def _flatten(self, x):
+        return x.reshape(x.shape[0], -1)
+
+    def _torch_forward(self, x):
+        x = self._flatten(x)
+        lins = self.linears()
+        if x.is_cuda and self.compute_dtype == torch.bfloat16:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                for lin in lins[:-1]:
+                    x = F.relu(lin(x))
+                return lins[-1](x).float()
+        x = x.float()
+        for lin in lins[:-1]:
+            x = F.relu(lin(x))
+        return lins[-1](x)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._native_ok(x):
+            from ..ops import mlp as mlp_ops
+            return mlp_ops.mlp_logits(self, self._flatten(x))
+        return self._torch_forward(x)
+
+    def forward_loss(self, x: torch.Tensor, targets: torch.Tensor):
+        """Fused forward + mean cross-entropy.  Returns (loss, logits-or-None)."""
+        if self._native_ok(x):
+            from ..ops import mlp as mlp_ops
+            return mlp_ops.mlp_loss(self, self._flatten(x), targets), None
+        logits = self._torch_forward(x)
+        return F.cross_entropy(logits, targets), logits
+
+    # ---- ddpx engine protocol -------------------------------------------------
+    def native_active(self, device) -> bool:
+        return (torch.device(device).type == "cuda" and self.use_native
+                and self.compute_dtype == torch.bfloat16)
+
+    def ddpx_spec(self, device):
+        """Flat-store layout request: bf16 compute shadow + all params written by native kernels."""
+        if self.native_active(device):
+            from ..runtime import native
+            native.kernels()  # fail loudly if the extension is missing on a GPU
+            return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters())}
+        return {}
+
+    def input_layout(self, device) -> str:
+        return "flat_bf16" if self.native_active(device) else "nchw_f32"

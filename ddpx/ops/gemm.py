@@ -1,0 +1,131 @@
+"""Host wrappers for the gfx950 bf16 MFMA GEMM (``csrc/kernels/gemm_bf16.hip``).
+
+Every wrapper validates shapes, dtypes, contiguity and alignment on the host
+before launching: the kernel's grid and loaders assume exactly these layouts.
+The three Linear products map onto one kernel with per-operand layouts, so no
+transpose is ever materialised:
+
+=========  ============================  ===========  ===========
+product    math                          A layout     B layout
+=========  ============================  ===========  ===========
+forward    Y[M,N]  = X[M,K] · W[N,K]ᵀ    K-contig     K-contig
+dgrad      dX[M,K] = dY[M,N] · W[N,K]    K-contig     N-contig
+wgrad      dW[N,K] = dY[M,N]ᵀ · X[M,K]   M-contig     N-contig
+=========  ============================  ===========  ===========
+"""
+from __future__ import annotations
+
+import torch
+
+from ..runtime import native
+
+EPI_F32 = 0
+EPI_BF16 = 1
+EPI_BIAS_BF16 = 2
+EPI_BIAS_RELU_BF16 = 3
+EPI_BIAS_F32 = 4
+EPI_RELUMASK_BF16 = 5
+
+_OUT_DTYPE = {
+    EPI_F32: torch.float32,
+    EPI_BF16: torch.bfloat16,
+    EPI_BIAS_BF16: torch.bfloat16,
+    EPI_BIAS_RELU_BF16: torch.bfloat16,
+    EPI_BIAS_F32: torch.float32,
+    EPI_RELUMASK_BF16: torch.bfloat16,
+}
+
+
+def _req(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _check_bf16_2d(t, name):
+    _req(t.is_cuda, f"{name} must be a GPU tensor")
+    _req(t.dtype == torch.bfloat16, f"{name} must be bf16, got {t.dtype}")
+    _req(t.dim() == 2, f"{name} must be 2-D, got shape {tuple(t.shape)}")
+    _req(t.stride(1) == 1, f"{name} must be row-contiguous")
+    _req(t.stride(0) % 8 == 0, f"{name} leading dimension must be a multiple of 8")
+    _req(t.data_ptr() % 16 == 0, f"{name} must be 16-byte aligned")
+
+
+def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
+             accumulate=False, alpha=1.0, tile=-1, stream=None):
+    lib = native.kernels()
+    rc = lib.ddpx_gemm_bf16(
+        a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux), M, N, K, lda, ldb, ldc,
+        ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate), float(alpha), tile,
+        native.stream_handle(stream))
+    native.check(rc, f"ddpx_gemm_bf16(M={M},N={N},K={K},epi={epi})")
+    return c
+
+
+def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, tile=-1):
+    """Y = act(X Wᵀ + b).  X [M,K] bf16, W [N,K] bf16, b [N] fp32."""
+    _check_bf16_2d(x, "x")
+    _check_bf16_2d(w, "w")
+    M, K = x.shape
+    N, K2 = w.shape
+    _req(K == K2, f"inner dims differ: x {tuple(x.shape)} vs w {tuple(w.shape)}")
+    if bias is not None:
+        _req(bias.dtype == torch.float32 and bias.numel() == N and bias.is_contiguous(), "bias must be fp32 [N]")
+    if out_dtype == torch.bfloat16:
+        epi = EPI_BIAS_RELU_BF16 if relu else (EPI_BIAS_BF16 if bias is not None else EPI_BF16)
+        _req(not (relu and bias is None), "relu epilogue requires a bias")
+    else:
+        _req(not relu, "fp32 output epilogue has no relu")
+        epi = EPI_BIAS_F32 if bias is not None else EPI_F32
+    if out is None:
+        out = torch.empty((M, N), dtype=_OUT_DTYPE[epi], device=x.device)
+    _req(out.shape == (M, N) and out.is_contiguous() and out.dtype == _OUT_DTYPE[epi], "bad out tensor")
+    return gemm_raw(x, w, out, M=M, N=N, K=K, lda=x.stride(0), ldb=w.stride(0), ldc=N, a_kcontig=True,
+                    b_kcontig=True, epi=epi, bias=bias, tile=tile)
+
+
+def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1):
+    """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below."""
+    _check_bf16_2d(dy, "dy")
+    _check_bf16_2d(w, "w")
+    M, N = dy.shape
+    N2, K = w.shape
+    _req(N == N2, f"dy {tuple(dy.shape)} incompatible with w {tuple(w.shape)}")
+    epi = EPI_BF16
+    if relu_mask_of is not None:
+        _check_bf16_2d(relu_mask_of, "relu_mask_of")
+        _req(tuple(relu_mask_of.shape) == (M, K), "mask shape must equal dX shape")
+        epi = EPI_RELUMASK_BF16
+    if out is None:
+        out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
+    _req(out.shape == (M, K) and out.is_contiguous() and out.dtype == torch.bfloat16, "bad out tensor")
+    return gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
+                    b_kcontig=False, epi=epi, aux=relu_mask_of,
+                    ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile)
+
+
+def linear_wgrad(dy, x, out, accumulate=False, tile=-1):
+    """dW[N,K] (=|+=) dYᵀ X in fp32 (written straight into the gradient bucket)."""
+    _check_bf16_2d(dy, "dy")
+    _check_bf16_2d(x, "x")
+    M, N = dy.shape
+    M2, K = x.shape
+    _req(M == M2, f"batch dims differ: dy {tuple(dy.shape)} vs x {tuple(x.shape)}")
+    _req(out.dtype in (torch.float32, torch.bfloat16), "dW must be fp32 or bf16")
+    _req(tuple(out.shape) == (N, K) and out.is_contiguous(), f"dW must be contiguous [{N},{K}]")
+    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
+    _req(not (accumulate and epi == EPI_BF16), "bf16 gradients cannot accumulate in the epilogue")
+    return gemm_raw(dy, x, out, M=N, N=K, K=M, lda=dy.stride(0), ldb=x.stride(0), ldc=K, a_kcontig=False,
+                    b_kcontig=False, epi=epi, accumulate=accumulate, tile=tile)
+
+
+def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-1):
+    """General C = A·B for tests: A given as [M,K] (K-contig) or [K,M]; B as [N,K] or [K,N]."""
+    _check_bf16_2d(a, "a")
+    _check_bf16_2d(b, "b")
+    M, K = a.shape if a_kcontig else (a.shape[1], a.shape[0])
+    N, K2 = b.shape if b_kcontig else (b.shape[1], b.shape[0])
+    _req(K == K2, "inner dims differ")
+    epi = EPI_F32 if out_dtype == torch.float32 else EPI_BF16
+    out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    return gemm_raw(a, b, out, M=M, N=N, K=K, lda=a.stride(0), ldb=b.stride(0), ldc=N, a_kcontig=a_kcontig,
+                    b_kcontig=b_kcontig, epi=epi, tile=tile)

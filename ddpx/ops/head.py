@@ -1,0 +1,115 @@
+"""Fused classifier head: Linear(K→10) + softmax cross-entropy (+ argmax count).
+
+Native on GPU (``csrc/kernels/head_xent.hip``); torch reference math on CPU.
+Reference: ``/root/reference/singlegpu.py:73,105,200-206``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..runtime import native
+
+
+def _check(h, w, b, targets):
+    if h.dim() != 2 or w.dim() != 2 or h.shape[1] != w.shape[1]:
+        raise ValueError(f"head: h {tuple(h.shape)} incompatible with w {tuple(w.shape)}")
+    if w.shape[0] != 10:
+        raise ValueError("head: native head is specialised for 10 classes")
+    if h.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise ValueError("head: h and w must be bf16 on GPU")
+    if b.dtype != torch.float32 or b.numel() != w.shape[0]:
+        raise ValueError("head: bias must be fp32 [C]")
+    if h.stride(1) != 1 or h.stride(0) % 8 or not w.is_contiguous():
+        raise ValueError("head: h must be row-contiguous with ld % 8 == 0, w contiguous")
+    if targets is not None and (targets.dtype != torch.int64 or targets.numel() != h.shape[0]):
+        raise ValueError("head: targets must be int64 [M]")
+
+
+def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correct=None):
+    """Returns (loss 0-d fp32 | None, logits [M,C] fp32 | None, dlogits [M,C] fp32 | None)."""
+    M, K = h.shape
+    C = w.shape[0]
+    if not h.is_cuda:
+        logits = F.linear(h.float(), w.float(), b)
+        loss = F.cross_entropy(logits, targets) if targets is not None else None
+        dl = None
+        if want_grad and targets is not None:
+            dl = (torch.softmax(logits, 1) - F.one_hot(targets, C).float()) / M
+        if correct is not None and targets is not None:
+            correct += (logits.argmax(1) == targets).sum().to(correct.dtype)
+        return loss, logits, dl
+    _check(h, w, b, targets)
+    dev = h.device
+    logits = torch.empty((M, C), dtype=torch.float32, device=dev) if want_logits else None
+    have_t = targets is not None
+    loss_rows = torch.empty((M,), dtype=torch.float32, device=dev) if have_t else None
+    dl = torch.empty((M, C), dtype=torch.float32, device=dev) if (want_grad and have_t) else None
+    lib = native.kernels()
+    s = native.stream_handle()
+    rc = lib.ddpx_head_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, C, h.stride(0),
+                           1.0 / M, native.ptr(logits), native.ptr(loss_rows), native.ptr(dl), native.ptr(correct), s)
+    native.check(rc, "ddpx_head_fwd")
+    loss = None
+    if have_t:
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        native.check(lib.ddpx_mean(loss_rows.data_ptr(), M, loss.data_ptr(), s), "ddpx_mean")
+    return loss, logits, dl
+
+
+def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_mask=True, accumulate=False):
+    """Backward of the fused head.
+
+    dW [C,K] fp32, db [C] fp32 (=|+=); dH [M,K] bf16 = (grad · W) ⊙ (h>0 if relu_mask);
+    dbprev [K] fp32 = Σ_m dH (bias gradient of the layer that produced h).
+    """
+    M, K = h.shape
+    C = w.shape[0]
+    if not h.is_cuda:
+        g = dlogits * grad_out
+        gw = g.t() @ h.float()
+        gb = g.sum(0)
+        if accumulate:
+            dW.add_(gw)
+            db.add_(gb)
+        else:
+            dW.copy_(gw)
+            db.copy_(gb)
+        if dH is not None:
+            gh = g @ w.float()
+            if relu_mask:
+                gh = gh * (h > 0)
+            dH.copy_(gh)
+            if dbprev is not None:
+                s = dH.float().sum(0)
+                dbprev.add_(s) if accumulate else dbprev.copy_(s)
+        return dH
+    _check(h, w, db, None)
+    if K % 64:
+        raise ValueError("head_backward: K must be a multiple of 64")
+    if dH is not None and (dH.shape != h.shape or dH.dtype != torch.bfloat16 or dH.stride(0) != h.stride(0)):
+        raise ValueError("head_backward: dH must match h")
+    if tuple(dW.shape) != (C, K) or dW.dtype != torch.float32 or not dW.is_contiguous():
+        raise ValueError("head_backward: dW must be fp32 contiguous [C,K]")
+    lib = native.kernels()
+    go = grad_out if torch.is_tensor(grad_out) else None
+    if go is not None:
+        go = go.to(torch.float32).contiguous()
+    rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
+                           native.ptr(dH), dW.data_ptr(), db.data_ptr(), native.ptr(dbprev), int(relu_mask),
+                           int(accumulate), native.stream_handle())
+    native.check(rc, "ddpx_head_bwd")
+    return dH
+
+
+def accuracy_count(logits, targets, correct):
+    """correct (int32 0-d device tensor) += #(argmax(logits) == targets)."""
+    if not logits.is_cuda:
+        correct += (logits.argmax(1) == targets).sum().to(correct.dtype)
+        return correct
+    M, C = logits.shape
+    lg = logits.float().contiguous()
+    lib = native.kernels()
+    native.check(lib.ddpx_accuracy(lg.data_ptr(), targets.data_ptr(), M, C, correct.data_ptr(),
+                                   native.stream_handle()), "ddpx_accuracy")
+    return correct

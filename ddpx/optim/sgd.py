@@ -1,0 +1,116 @@
+"""Fused flat-buffer SGD (momentum, weight decay) — drop-in for torch.optim.SGD.
+
+Reference: ``torch.optim.SGD(model.parameters(), lr=0.4, momentum=0.9,
+weight_decay=5e-4)`` at ``/root/reference/singlegpu.py:136-141`` (default
+foreach path, ``torch/optim/sgd.py:383-478``: 4 multi-tensor passes / step).
+
+Here all parameters are views of one flat fp32 buffer (``FlatParams``), so a
+step is ONE kernel launch (``ddpx_sgd_flat``) that reads p, g, momentum once
+and writes p, momentum and the bf16 compute shadow once — or one launch per
+DDP bucket when the optimizer is overlapped with the gradient all-reduce
+(each slice starts as soon as its bucket's collective lands).
+
+The class subclasses ``torch.optim.Optimizer`` so torch LR schedulers
+(``LambdaLR``) drive it unchanged.  ``capturable=True`` reads the learning rate
+from a device scalar, which makes ``step()`` safe inside a HIP graph.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from ..ops.elementwise import sgd_flat_
+from ..runtime.flat_params import FlatParams, flat_of
+
+
+class SGD(Optimizer):
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, capturable: bool = False):
+        if dampening != 0.0:
+            raise ValueError("ddpx.optim.SGD implements dampening=0 (the reference's setting)")
+        if nesterov and momentum <= 0:
+            raise ValueError("Nesterov momentum requires a momentum")
+        params = list(params)
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+        if len(self.param_groups) != 1:
+            raise ValueError("ddpx.optim.SGD supports a single parameter group")
+        flat = flat_of(params)
+        if flat is None:
+            raise ValueError("parameters are not flattened: wrap the model with ddpx.prepare_model() first")
+        ids = {id(p) for p in params}
+        if ids != {id(p) for p in flat.params}:
+            raise ValueError("SGD must own exactly the parameters of one FlatParams store")
+        self.flat: FlatParams = flat
+        self.momentum_buffer = torch.zeros_like(flat.master) if momentum else None
+        self.capturable = capturable
+        self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if capturable else None
+        self.bucket_source = None  # set by DDP when the optimizer overlaps the all-reduce
+        self.step_count = 0
+
+    # ------------------------------------------------------------------ API
+    def zero_grad(self, set_to_none: bool = True):  # noqa: D401 - torch signature
+        self.flat.zero_grad()
+
+    def sync_lr(self):
+        """Copy the host learning rate into the device scalar (outside graph capture)."""
+        if self.lr_dev is not None:
+            self.lr_dev.fill_(float(self.param_groups[0]["lr"]))
+
+    def _lr_arg(self):
+        return self.lr_dev if self.capturable else float(self.param_groups[0]["lr"])
+
+    def _update(self, start, end, g):
+        f = self.flat
+        buf = self.momentum_buffer[start:end] if self.momentum_buffer is not None else f.master[start:end]
+        sh = f.shadow[start:end] if f.shadow is not None else None
+        sgd_flat_(f.master[start:end], buf, f.grad[start:end], sh, self._lr_arg(), g["momentum"],
+                  g["weight_decay"], nesterov=g["nesterov"])
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g = self.param_groups[0]
+        if not (self.flat.master.is_cuda and torch.cuda.is_current_stream_capturing()):
+            self.flat.fix_unwritten()
+        src = self.bucket_source
+        if src is not None and src.overlap_active():
+            for (start, end) in src.bucket_ranges_in_completion_order():
+                src.wait_range(start, end)
+                self._update(start, end, g)
+            src.optimizer_done()
+        else:
+            self._update(0, self.flat.total, g)
+        self.step_count += 1
+        return loss
+
+    # ------------------------------------------------------- (de)serialise
+    def state_dict(self):
+        sd = super().state_dict()
+        state = {}
+        if self.momentum_buffer is not None and self.step_count > 0:
+            for i, p in enumerate(self.param_groups[0]["params"]):
+                j = self.flat.index[id(p)]
+                state[i] = {"momentum_buffer": self.momentum_buffer[self.flat.slice(j)].view(p.shape).clone()}
+        sd["state"] = state
+        sd["ddpx_step_count"] = self.step_count
+        return sd
+
+    def load_state_dict(self, state_dict):
+        state_dict = dict(state_dict)
+        st = state_dict.pop("state", {})
+        self.step_count = int(state_dict.pop("ddpx_step_count", 0))
+        groups = state_dict["param_groups"]
+        for k, v in groups[0].items():
+            if k != "params":
+                self.param_groups[0][k] = v
+        if self.momentum_buffer is not None:
+            for i, p in enumerate(self.param_groups[0]["params"]):
+                s = st.get(i, st.get(str(i)))
+                if s is not None and s.get("momentum_buffer") is not None:
+                    j = self.flat.index[id(p)]
+                    self.momentum_buffer[self.flat.slice(j)].copy_(s["momentum_buffer"].reshape(-1))
+        self.sync_lr()

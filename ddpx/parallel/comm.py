@@ -1,0 +1,218 @@
+"""Communication backends behind one small interface.
+
+* :class:`RcclComm` — the MI355X path: a native RCCL communicator
+  (``csrc/runtime/rccl_comm.cpp``) bootstrapped through the c10d TCPStore,
+  with its own high-priority HIP stream and a timeout watchdog.  Collectives
+  are issued on explicit streams, so they overlap compute and are captured
+  by HIP graphs.
+* :class:`TorchComm` — ``torch.distributed`` (gloo on CPU, used by the CPU
+  test-suite; or stock ProcessGroupNCCL for A/B runs).
+
+Reference equivalent: ``init_process_group(backend="nccl")`` at
+``/root/reference/multigpu.py:32`` and the collectives DDP issues implicitly
+(SURVEY §2.4 C0–C7).
+"""
+from __future__ import annotations
+
+import itertools
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..runtime import native
+
+# RCCL enums (rccl.h)
+NCCL_DTYPE = {
+    torch.int64: 4,
+    torch.float16: 6,
+    torch.float32: 7,
+    torch.float64: 8,
+    torch.bfloat16: 9,
+    torch.uint8: 1,
+    torch.int32: 2,
+}
+NCCL_OP = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+
+_uid_counter = itertools.count()
+
+
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+    native: bool = False
+    supports_avg: bool = True
+
+    def allreduce_(self, t: torch.Tensor, op: str = "avg", stream=None, async_op=False):
+        raise NotImplementedError
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0, stream=None):
+        raise NotImplementedError
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "avg", stream=None):
+        raise NotImplementedError
+
+    def allgather(self, out: torch.Tensor, inp: torch.Tensor, stream=None):
+        raise NotImplementedError
+
+    def barrier(self):
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.barrier()
+
+    def all_gather_object(self, obj):
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return [obj]
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return out
+
+    def check(self):
+        pass
+
+    def close(self, abort=False):
+        pass
+
+
+class TorchComm(Comm):
+    """torch.distributed-backed collectives (gloo for CPU tensors, nccl for GPU)."""
+
+    def __init__(self, group=None):
+        if not dist.is_initialized():
+            raise RuntimeError("TorchComm requires torch.distributed to be initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.native = False
+
+    def _avg_ok(self, t):
+        return t.is_cuda and dist.get_backend(self.group) in ("nccl", "cpu:gloo,cuda:nccl")
+
+    def allreduce_(self, t, op="avg", stream=None, async_op=False):
+        if self.world_size == 1:
+            return None
+        if op == "avg" and not self._avg_ok(t):
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            if async_op:
+                return _ScaleOnWait(work, t, 1.0 / self.world_size)
+            t.div_(self.world_size)
+            return None
+        rop = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX,
+               "min": dist.ReduceOp.MIN}[op]
+        return dist.all_reduce(t, op=rop, group=self.group, async_op=async_op)
+
+    def broadcast_(self, t, src=0, stream=None):
+        if self.world_size > 1:
+            dist.broadcast(t, src=src, group=self.group)
+
+    def reduce_scatter(self, out, inp, op="avg", stream=None):
+        if self.world_size == 1:
+            out.copy_(inp)
+            return
+        chunks = list(inp.chunk(self.world_size))
+        if inp.is_cuda:
+            dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
+        else:  # gloo has no reduce_scatter: all-reduce then slice
+            tmp = inp.clone()
+            dist.all_reduce(tmp, group=self.group)
+            out.copy_(tmp.chunk(self.world_size)[self.rank])
+        del chunks
+        if op == "avg":
+            out.div_(self.world_size)
+
+    def allgather(self, out, inp, stream=None):
+        if self.world_size == 1:
+            out.copy_(inp)
+            return
+        dist.all_gather_into_tensor(out, inp, group=self.group) if inp.is_cuda else dist.all_gather(
+            list(out.chunk(self.world_size)), inp, group=self.group)
+
+
+class _ScaleOnWait:
+    def __init__(self, work, t, s):
+        self.work, self.t, self.s = work, t, s
+
+    def wait(self):
+        self.work.wait()
+        self.t.mul_(self.s)
+
+
+class RcclComm(Comm):
+    """Native RCCL communicator for one process per MI355X."""
+
+    def __init__(self, device: torch.device, timeout_s: float | None = None, high_priority: bool = True):
+        if not dist.is_initialized():
+            raise RuntimeError("RcclComm bootstraps through the default c10d store: init_process_group first")
+        rt = native.runtime()
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+        self.device = torch.device(device)
+        self.native = True
+        store = dist.distributed_c10d._get_default_store()
+        key = f"ddpx/rccl_uid/{next(_uid_counter)}"
+        if self.rank == 0:
+            uid = (native.ctypes.c_char * 128)()
+            native.check(rt.ddpx_comm_unique_id(uid, 128), "ncclGetUniqueId")
+            store.set(key, bytes(uid))
+        uid = store.get(key)
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("DDPX_COMM_TIMEOUT", "600"))
+        err = native.ctypes.c_int(0)
+        torch.cuda.set_device(self.device)
+        self.handle = rt.ddpx_comm_create(uid, self.world_size, self.rank, self.device.index or 0,
+                                          int(high_priority), float(timeout_s), native.ctypes.byref(err))
+        if not self.handle:
+            raise RuntimeError(f"ncclCommInitRank failed (code {err.value})")
+        self._rt = rt
+        self.stream = torch.cuda.ExternalStream(rt.ddpx_comm_stream(self.handle), device=self.device)
+
+    def _s(self, stream):
+        return native.stream_handle(stream) if stream is not None else native.stream_handle()
+
+    def _dt(self, t):
+        try:
+            return NCCL_DTYPE[t.dtype]
+        except KeyError:
+            raise TypeError(f"RCCL: unsupported dtype {t.dtype}") from None
+
+    def allreduce_(self, t, op="avg", stream=None, async_op=False):
+        if not t.is_contiguous():
+            raise ValueError("allreduce_: tensor must be contiguous")
+        rc = self._rt.ddpx_comm_allreduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t),
+                                          NCCL_OP[op], self._s(stream))
+        native.check(rc, "ncclAllReduce")
+        return None
+
+    def broadcast_(self, t, src=0, stream=None):
+        if not t.is_contiguous():
+            raise ValueError("broadcast_: tensor must be contiguous")
+        rc = self._rt.ddpx_comm_broadcast(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), src,
+                                          self._s(stream))
+        native.check(rc, "ncclBroadcast")
+
+    def reduce_scatter(self, out, inp, op="avg", stream=None):
+        rc = self._rt.ddpx_comm_reduce_scatter(self.handle, inp.data_ptr(), out.data_ptr(), out.numel(),
+                                               self._dt(inp), NCCL_OP[op], self._s(stream))
+        native.check(rc, "ncclReduceScatter")
+
+    def allgather(self, out, inp, stream=None):
+        rc = self._rt.ddpx_comm_allgather(self.handle, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp),
+                                          self._s(stream))
+        native.check(rc, "ncclAllGather")
+
+    def check(self):
+        e = self._rt.ddpx_comm_error(self.handle)
+        if e:
+            raise RuntimeError({1: "RCCL asynchronous error", 2: "RCCL collective timed out",
+                                3: "RCCL communicator aborted"}.get(e, f"RCCL error {e}"))
+
+    def close(self, abort=False):
+        if getattr(self, "handle", None):
+            self._rt.ddpx_comm_destroy(self.handle, int(abort))
+            self.handle = None
+
+
+def default_comm(device: torch.device | None = None) -> Comm:
+    """RcclComm for GPU tensors (unless DDPX_COMM=torch), TorchComm otherwise."""
+    if device is not None and torch.device(device).type == "cuda" and os.environ.get("DDPX_COMM", "rccl") == "rccl":
+        return RcclComm(device)
+    return TorchComm()

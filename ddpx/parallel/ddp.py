@@ -1,0 +1,355 @@
+"""DistributedDataParallel for one process per MI355X.
+
+Behaviour parity with ``DDP(model, device_ids=[gpu_id])`` as the reference
+uses it (``/root/reference/multigpu.py:89``):
+
+* construction: verify parameter shapes across ranks (C1), broadcast all
+  parameters and buffers from rank 0 (C2) — the reference never seeds, so
+  this is what makes the replicas identical;
+* every forward: broadcast the module buffers (BN running stats) from rank 0
+  (C3, ``broadcast_buffers=True``);
+* backward: gradients are averaged across ranks bucket by bucket while
+  backward is still running (C6); bucket k's all-reduce is issued the moment
+  its last gradient is produced.
+
+MI355X-specific design:
+
+* Buckets are contiguous slices of the flat gradient buffer (``FlatParams``),
+  assigned by torch's size rule (``_compute_bucket_assignment_by_size``) on the
+  grad-ready order from the first iteration on — no pack/unpack, no rebuild
+  step (C4/C5 become unnecessary).
+* Bucket caps default to 1 MiB first / 25 MiB after, overridable
+  (``bucket_cap_mb``, ``first_bucket_mb``) to tune for point-to-point xGMI
+  rings.
+* With :class:`~ddpx.parallel.comm.RcclComm` the reducer is native C++
+  (events + RCCL on a dedicated high-priority stream, ``ncclAvg``).  With a
+  ``TorchComm`` (gloo, CPU tests) an equivalent Python reducer is used.
+* ``overlap_optimizer=True`` leaves the buckets un-joined at the end of
+  backward; ``ddpx.optim.SGD`` then updates each bucket's slice as soon as its
+  collective lands, overlapping the optimizer with the remaining traffic.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ..runtime import native
+from ..runtime.flat_params import FlatParams, flat_of
+from .comm import NCCL_DTYPE, NCCL_OP, Comm, RcclComm, TorchComm
+
+DEFAULT_FIRST_BUCKET_MB = 1.0   # dist._DEFAULT_FIRST_BUCKET_BYTES
+DEFAULT_BUCKET_CAP_MB = 25.0    # DDP bucket_cap_mb default
+
+
+def compute_bucket_assignment(sizes_bytes, limits_bytes):
+    """torch's greedy rule: close a bucket once it reaches the current limit."""
+    buckets, cur, cur_size, li = [], [], 0, 0
+    for i, s in enumerate(sizes_bytes):
+        cur.append(i)
+        cur_size += s
+        if cur_size >= limits_bytes[min(li, len(limits_bytes) - 1)]:
+            buckets.append(cur)
+            cur, cur_size = [], 0
+            li += 1
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+class FlatBuffers:
+    """Module buffers rebound as views of one flat tensor per dtype (broadcast in one call each)."""
+
+    def __init__(self, module: nn.Module):
+        entries = [(m, n, b) for m in module.modules() for n, b in m._buffers.items() if b is not None]
+        self.flats = {}
+        by_dtype = {}
+        for m, n, b in entries:
+            by_dtype.setdefault(b.dtype, []).append((m, n, b))
+        for dt, items in by_dtype.items():
+            total = sum(b.numel() for _, _, b in items)
+            flat = torch.empty(total, dtype=dt, device=items[0][2].device)
+            off = 0
+            for m, n, b in items:
+                view = flat[off:off + b.numel()].view(b.shape)
+                view.copy_(b)
+                m._buffers[n] = view
+                off += b.numel()
+            self.flats[dt] = flat
+
+    def tensors(self):
+        return list(self.flats.values())
+
+
+class _PyReducer:
+    """Bucket state machine over torch.distributed async collectives (CPU / gloo)."""
+
+    def __init__(self, comm: TorchComm, ranges):
+        self.comm = comm
+        self.ranges = ranges
+        self.tensors = None
+        self.expected = None
+        self.pending = None
+        self.works = None
+
+    def setup(self, grad_flat, expected):
+        self.tensors = [grad_flat[s:e] for s, e in self.ranges]
+        self.expected = list(expected)
+        self.prepare()
+
+    def prepare(self):
+        self.pending = list(self.expected)
+        self.works = [None] * len(self.ranges)
+        self.launched = [False] * len(self.ranges)
+
+    def _launch(self, b):
+        self.works[b] = self.comm.allreduce_(self.tensors[b], op="avg", async_op=True)
+        self.launched[b] = True
+
+    def mark_ready(self, b, n=1):
+        if self.launched[b]:
+            raise RuntimeError(f"bucket {b} marked ready twice in one backward")
+        self.pending[b] -= n
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def wait_bucket(self, b, stream=None):
+        w = self.works[b]
+        if w is not None:
+            w.wait()
+            self.works[b] = None
+
+    def finalize(self, join=True):
+        forced = 0
+        for b in range(len(self.ranges)):
+            if not self.launched[b]:
+                self._launch(b)
+                forced += 1
+        if join:
+            for b in range(len(self.ranges)):
+                self.wait_bucket(b)
+        return forced
+
+
+class _NativeReducer:
+    """ctypes front-end of the C++ reducer (csrc/runtime/rccl_comm.cpp)."""
+
+    def __init__(self, comm: RcclComm, ranges):
+        self.comm = comm
+        self.ranges = ranges
+        self.rt = native.runtime()
+        self.h = self.rt.ddpx_reducer_create(comm.handle, len(ranges), NCCL_OP["avg"])
+
+    def setup(self, grad_flat, expected):
+        dt = NCCL_DTYPE[grad_flat.dtype]
+        self._keep = grad_flat
+        for b, (s, e) in enumerate(self.ranges):
+            t = grad_flat[s:e]
+            native.check(self.rt.ddpx_reducer_set_bucket(self.h, b, t.data_ptr(), t.numel(), dt, expected[b]),
+                         "reducer_set_bucket")
+
+    def prepare(self):
+        self.rt.ddpx_reducer_prepare(self.h)
+
+    def mark_ready(self, b, n=1):
+        rc = self.rt.ddpx_reducer_mark_ready(self.h, b, n, native.stream_handle())
+        if rc not in (0, 1):
+            raise RuntimeError(f"reducer mark_ready(bucket={b}) failed: {rc}")
+
+    def wait_bucket(self, b, stream=None):
+        rc = self.rt.ddpx_reducer_wait_bucket(self.h, b, native.stream_handle(stream))
+        if rc != 0:
+            raise RuntimeError(f"reducer wait_bucket({b}) failed: {rc}")
+
+    def finalize(self, join=True):
+        if join:
+            rc = self.rt.ddpx_reducer_finalize(self.h, native.stream_handle())
+            if rc < 0:
+                raise RuntimeError(f"reducer finalize failed: {rc}")
+            return rc
+        return 0
+
+    def close(self):
+        if self.h:
+            self.rt.ddpx_reducer_destroy(self.h)
+            self.h = None
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, comm: Comm | None = None,
+                 bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
+                 broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True):
+        super().__init__()
+        self.module = module
+        dev = next(module.parameters()).device
+        self.device = dev
+        self.flat: FlatParams = flat_of(module) or FlatParams(module)
+        if comm is None:
+            from .comm import default_comm
+            comm = default_comm(dev)
+        self.comm = comm
+        self.world_size = comm.world_size
+        self.rank = comm.rank
+        self.broadcast_buffers = broadcast_buffers
+        self.overlap_optimizer = overlap_optimizer
+        self._sync_enabled = True
+        self._queued = False
+        self._overlap_pending = False
+
+        # C1: parameter metadata must agree across ranks.
+        if verify and self.world_size > 1:
+            meta = [(tuple(p.shape), str(p.dtype)) for p in self.flat.params]
+            allm = comm.all_gather_object(meta)
+            for r, m in enumerate(allm):
+                if m != meta:
+                    raise RuntimeError(f"DDP: parameter shapes differ between rank {self.rank} and rank {r}")
+
+        # Buffers as flat per-dtype tensors (one broadcast each).
+        self.buffers_flat = FlatBuffers(module) if any(True for _ in module.buffers()) else None
+
+        # C2: make replicas identical.
+        self._broadcast_state()
+
+        # Buckets: contiguous flat ranges over grad-ready order.
+        esz = self.flat.grad.element_size()
+        sizes = [n * esz for n in self.flat.numels]
+        limits = [int(first_bucket_mb * 1024 * 1024), int(bucket_cap_mb * 1024 * 1024)]
+        assign = compute_bucket_assignment(sizes, limits)
+        self.bucket_params = assign
+        self.bucket_of = [0] * len(self.flat.params)
+        ranges, expected = [], []
+        for b, idxs in enumerate(assign):
+            for i in idxs:
+                self.bucket_of[i] = b
+            ranges.append(self.flat.span(idxs[0], idxs[-1]))
+            expected.append(len(idxs))
+        self.bucket_ranges = ranges
+        if self.world_size > 1:
+            self.reducer = _NativeReducer(comm, ranges) if isinstance(comm, RcclComm) else _PyReducer(comm, ranges)
+            self.reducer.setup(self.flat.grad, expected)
+        else:
+            self.reducer = None
+        self.flat.sink = self
+        self._completion_order = []
+
+    # ------------------------------------------------------------- state sync
+    @torch.no_grad()
+    def _broadcast_state(self):
+        if self.world_size == 1:
+            return
+        self.comm.broadcast_(self.flat.master, 0)
+        if self.buffers_flat is not None:
+            for t in self.buffers_flat.tensors():
+                self.comm.broadcast_(t, 0)
+        self.flat.refresh_shadow()
+
+    @torch.no_grad()
+    def _sync_buffers(self):
+        if self.world_size > 1 and self.broadcast_buffers and self.buffers_flat is not None:
+            for t in self.buffers_flat.tensors():
+                self.comm.broadcast_(t, 0)
+
+    # ---------------------------------------------------------------- forward
+    def _pre_forward(self):
+        self.comm.check()
+        if torch.is_grad_enabled() and self.reducer is not None and self._sync_enabled:
+            if self._overlap_pending:
+                raise RuntimeError("DDP: optimizer.step() did not consume the previous iteration's buckets")
+            self.reducer.prepare()
+            self._completion_order = []
+        self._queued = False
+        if self.module.training:
+            self._sync_buffers()
+
+    def forward(self, *args, **kwargs):
+        self._pre_forward()
+        return self.module(*args, **kwargs)
+
+    def forward_loss(self, *args, **kwargs):
+        self._pre_forward()
+        return self.module.forward_loss(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = old
+
+    # ------------------------------------------------------ gradient protocol
+    def grad_ready(self, i: int):
+        if self.reducer is None or not self._sync_enabled:
+            return
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b = self.bucket_of[i]
+        self.reducer.mark_ready(b, 1)
+        if self.reducer_launched(b):
+            self._completion_order.append(b)
+
+    def reducer_launched(self, b):
+        r = self.reducer
+        if isinstance(r, _PyReducer):
+            return r.launched[b]
+        # native: the bucket launched iff all its params have been marked
+        return self._marks_complete(b)
+
+    def _marks_complete(self, b):
+        idxs = self.bucket_params[b]
+        return all(self.flat.written[i] for i in idxs)
+
+    def _finalize(self):
+        if self.reducer is None:
+            return
+        if self.overlap_optimizer:
+            self._overlap_pending = True
+            # launch stragglers but do not join: the optimizer waits per bucket
+            if isinstance(self.reducer, _PyReducer):
+                self.reducer.finalize(join=False)
+            else:
+                missing = [b for b in range(len(self.bucket_ranges)) if b not in self._completion_order]
+                if missing:
+                    self.reducer.finalize(join=True)
+                    self._overlap_pending = False
+        else:
+            self.reducer.finalize(join=True)
+
+    # ----------------------------------------- optimizer overlap (SGD hooks)
+    def overlap_active(self):
+        return self.overlap_optimizer and self._overlap_pending
+
+    def bucket_ranges_in_completion_order(self):
+        order = list(self._completion_order)
+        order += [b for b in range(len(self.bucket_ranges)) if b not in order]
+        self._iter_order = order
+        return [self.bucket_ranges[b] for b in order]
+
+    def wait_range(self, start, end):
+        b = self.bucket_ranges.index((start, end))
+        self.reducer.wait_bucket(b)
+
+    def optimizer_done(self):
+        self._overlap_pending = False
+
+    def attach_optimizer(self, opt):
+        opt.bucket_source = self
+
+    def sync_grads(self):
+        """Join all outstanding bucket collectives (overlap mode) into the current stream."""
+        if self._overlap_pending:
+            for b in range(len(self.bucket_ranges)):
+                self.reducer.wait_bucket(b)
+            self._overlap_pending = False
+
+    # ----------------------------------------------------------------- misc
+    def state_dict(self, *args, **kwargs):
+        return super().state_dict(*args, **kwargs)
+
+    def close(self):
+        if self.reducer is not None and hasattr(self.reducer, "close"):
+            self.reducer.close()

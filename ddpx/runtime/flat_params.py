@@ -1,0 +1,167 @@
+"""Flat parameter / gradient / shadow storage for a module.
+
+MI355X-first memory layout:
+
+* every trainable parameter becomes a view into ONE contiguous fp32 ``master``
+  buffer, laid out in *gradient-ready order* (reverse registration order, the
+  order backward produces gradients — the same order torch DDP's reducer
+  rebuilds its buckets into, ``torch/nn/parallel/distributed.py:1551``);
+* gradients live in a parallel flat buffer; ``p.main_grad`` is the view.  DDP
+  buckets are contiguous slices of it, so an all-reduce never packs/unpacks;
+* an optional parallel bf16 ``shadow`` holds the compute copy of the weights
+  the MFMA GEMMs read; the fused SGD kernel refreshes it in the same pass that
+  updates ``master`` (no separate cast kernel per step);
+* each parameter offset is 64-element aligned so every slice is 256-B aligned
+  for the 16-B vector loads of the kernels.
+
+Gradients arrive in two ways:
+
+1. native ops (``ddpx.ops``) write straight into ``main_grad`` with the GEMM
+   epilogue and call :meth:`grad_done`;
+2. parameters used by stock torch ops get a post-accumulate-grad hook that
+   moves ``p.grad`` into ``main_grad`` and then calls :meth:`grad_done`.
+
+``zero_grad`` is O(#params) host work: it only resets the "written" flags; the
+first writer of an iteration overwrites instead of accumulating
+(``set_to_none=True`` semantics of ``/root/reference/singlegpu.py:103``).
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+
+ALIGN = 64
+
+
+def _round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+class FlatParams:
+    def __init__(self, module: torch.nn.Module, grad_dtype=torch.float32, shadow_dtype=None,
+                 native_params=(), align: int = ALIGN):
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("module has no trainable parameters")
+        device = params[0].device
+        for p in params:
+            if p.device != device:
+                raise ValueError("all parameters must be on one device")
+            if p.dtype != torch.float32:
+                raise ValueError("FlatParams expects fp32 master parameters")
+        self.device = device
+        self.params = list(reversed(params))  # gradient-ready order
+        self.names = {}
+        for name, p in module.named_parameters():
+            self.names[id(p)] = name
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.offsets, self.numels = [], []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            self.numels.append(p.numel())
+            off = _round_up(off + p.numel(), align)
+        self.total = off
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total, dtype=grad_dtype, device=device)
+        self.shadow = torch.zeros(self.total, dtype=shadow_dtype, device=device) if shadow_dtype else None
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                view = self.master[o:o + n].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.main_grad = self.grad[o:o + n].view(p.shape)
+                if self.shadow is not None:
+                    p._ddpx_shadow = self.shadow[o:o + n].view(p.shape)
+                p._ddpx_flat = self
+        self.refresh_shadow()
+        self.native = {id(p) for p in native_params}
+        self.written = [False] * len(self.params)
+        self.sink = None
+        self._warned_unused = False
+        self._hooks = []
+        for p in self.params:
+            if id(p) not in self.native:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
+
+    # -- views --------------------------------------------------------------
+    def slice(self, i):
+        o, n = self.offsets[i], self.numels[i]
+        return slice(o, o + n)
+
+    def span(self, first: int, last: int):
+        """Flat element range [start, end) covering params first..last (inclusive, aligned end)."""
+        start = self.offsets[first]
+        end = self.offsets[last + 1] if last + 1 < len(self.params) else self.total
+        return start, end
+
+    def shadow_of(self, p):
+        return getattr(p, "_ddpx_shadow", None)
+
+    def refresh_shadow(self):
+        if self.shadow is None:
+            return
+        from ..ops.elementwise import cast_bf16_
+        cast_bf16_(self.master, self.shadow)
+
+    # -- gradient protocol -----------------------------------------------------
+    def grad_target(self, p):
+        """(main_grad view, accumulate?) for a native op about to write p's gradient."""
+        i = self.index[id(p)]
+        return p.main_grad, self.written[i]
+
+    def grad_done(self, p):
+        i = self.index[id(p)]
+        self.written[i] = True
+        if self.sink is not None:
+            self.sink.grad_ready(i)
+
+    def _on_accumulated(self, p):
+        i = self.index[id(p)]
+        g = p.grad
+        if g is None:
+            return
+        if self.written[i]:
+            p.main_grad.add_(g)
+        else:
+            p.main_grad.copy_(g)
+        p.grad = None
+        self.written[i] = True
+        if self.sink is not None:
+            self.sink.grad_ready(i)
+
+    def zero_grad(self):
+        self.written = [False] * len(self.params)
+        for p in self.params:
+            p.grad = None
+
+    def fix_unwritten(self):
+        """Zero gradients nobody produced this iteration (stale values would otherwise be applied)."""
+        missing = [i for i, w in enumerate(self.written) if not w]
+        if missing:
+            if not self._warned_unused:
+                names = [self.names.get(id(self.params[i]), str(i)) for i in missing]
+                warnings.warn(f"ddpx: parameters without gradient this step (zeroed): {names}")
+                self._warned_unused = True
+            for i in missing:
+                self.grad[self.slice(i)].zero_()
+        return missing
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def flat_of(module_or_params):
+    """Find the FlatParams that owns a module's (or a param list's) parameters."""
+    if isinstance(module_or_params, torch.nn.Module):
+        ps = list(module_or_params.parameters())
+    else:
+        ps = list(module_or_params)
+    for p in ps:
+        f = getattr(p, "_ddpx_flat", None)
+        if f is not None:
+            return f
+    return None

@@ -1,0 +1,19 @@
+"""Placing a model onto the ddpx engine (device + flat parameter store)."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .flat_params import FlatParams, flat_of
+
+
+def prepare_model(model: nn.Module, device, grad_dtype=torch.float32) -> FlatParams:
+    """Move ``model`` to ``device`` and flatten its parameters (idempotent)."""
+    device = torch.device(device)
+    model.to(device)
+    f = flat_of(model)
+    if f is not None:
+        return f
+    spec = model.ddpx_spec(device) if hasattr(model, "ddpx_spec") else {}
+    return FlatParams(model, grad_dtype=grad_dtype, shadow_dtype=spec.get("shadow_dtype"),
+                      native_params=spec.get("native_params", ()))

@@ -1,0 +1,194 @@
+"""Orchestration shared by ``singlegpu.py`` and ``multigpu.py``.
+
+Mirrors the reference's ``load_train_objs`` / ``prepare_dataloader`` /
+``main`` / ``ddp_setup`` / ``__main__`` (``/root/reference/singlegpu.py:132-263``,
+``multigpu.py:24-33,122-263``), keeping the positional CLI
+(``TOTAL_EPOCHS SAVE_EVERY [--batch_size 512]``), the stdout lines and the
+``checkpoint.pt`` format, and adding the SURVEY §5.6 flags.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..data.datasets import get_datasets
+from ..data.loader import DeviceLoader
+from ..data.sampler import DistributedIndexSampler
+from ..models import build_model
+from ..optim.schedule import one_cycle, resolve_steps_per_epoch
+from ..optim.sgd import SGD
+from ..parallel.comm import RcclComm, TorchComm
+from ..parallel.ddp import DistributedDataParallel
+from ..runtime.setup import prepare_model
+from ..utils.metrics import MetricsWriter
+from ..utils.size import MiB, get_model_size
+from .checkpoint import FULL_CKPT_PATH, load_full_checkpoint
+from .evaluate import evaluate
+from .trainer import Trainer
+
+REF_LR = 0.4
+REF_MOMENTUM = 0.9
+REF_WD = 5e-4
+
+
+def build_parser(description: str) -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description=description)
+    p.add_argument("total_epochs", type=int, help="Total epochs to train the model")
+    p.add_argument("save_every", type=int, help="How often to save a snapshot")
+    p.add_argument("--batch_size", default=512, type=int, help="Input batch size on each device (default: 512)")
+    p.add_argument("--model", default="vgg", choices=["vgg", "deepnn", "mlp", "mlp_wide"])
+    p.add_argument("--hidden", type=int, default=None, help="MLP hidden width (default 4096, wide 16384)")
+    p.add_argument("--layers", type=int, default=3, help="MLP Linear layers (default 3)")
+    p.add_argument("--data", default="auto", choices=["auto", "cifar10", "synthetic"])
+    p.add_argument("--data_root", default="data/cifar10")
+    p.add_argument("--train_size", type=int, default=50000, help="synthetic train-set size")
+    p.add_argument("--test_size", type=int, default=10000, help="synthetic test-set size")
+    p.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"])
+    p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    p.add_argument("--kernels", default="native", choices=["native", "torch"])
+    p.add_argument("--bucket_cap_mb", type=float, default=25.0)
+    p.add_argument("--first_bucket_mb", type=float, default=1.0)
+    p.add_argument("--steps_per_epoch", default="compat", help="'compat' (98/49 as the reference), 'auto' or N")
+    p.add_argument("--seed", type=int, default=None, help="seed model init (reference: unseeded)")
+    p.add_argument("--graph", action="store_true", help="capture the training step in a HIP graph")
+    p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
+    p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
+    p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
+    p.add_argument("--resume", action="store_true", help=f"resume from {FULL_CKPT_PATH}")
+    p.add_argument("--full_checkpoint", action="store_true", help=f"also write {FULL_CKPT_PATH}")
+    p.add_argument("--metrics", default=None, help="JSON-lines metrics file")
+    p.add_argument("--eval_batch", type=int, default=512)
+    p.add_argument("--no_eval", action="store_true")
+    p.add_argument("--nprocs", type=int, default=None, help="multigpu: processes to spawn (default: #GPUs)")
+    return p
+
+
+def resolve_device(args, local_rank: int = 0) -> torch.device:
+    if args.device == "cpu" or (args.device == "auto" and not torch.cuda.is_available()):
+        return torch.device("cpu")
+    return torch.device("cuda", local_rank)
+
+
+def resolve_data(args):
+    kind = args.data
+    if kind == "auto":
+        have = os.path.isdir(os.path.join(args.data_root, "cifar-10-batches-bin")) or os.path.isdir(
+            os.path.join(args.data_root, "cifar-10-batches-py"))
+        kind = "cifar10" if have else "synthetic"
+    return kind
+
+
+def input_layout(model, device, dtype):
+    if getattr(model, "input_layout", None):
+        return model.input_layout(device)
+    return "nchw_f32"
+
+
+def load_train_objs(args, device, distributed: bool, world_size: int, loader_len_hint: int):
+    """(train_set, model, optimizer, test_set, scheduler) — the reference's factory, ddpx engine underneath."""
+    kind = resolve_data(args)
+    train_set, test_set = get_datasets(kind, args.data_root, seed=0, train_size=args.train_size,
+                                       test_size=args.test_size)
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
+                        kernels=args.kernels)
+    prepare_model(model, device)
+    optimizer = SGD(model.parameters(), lr=REF_LR, momentum=REF_MOMENTUM, weight_decay=REF_WD,
+                    capturable=bool(args.graph and device.type == "cuda"))
+    spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)
+    scheduler = one_cycle(optimizer, spe)
+    return train_set, model, optimizer, test_set, scheduler
+
+
+def prepare_dataloader(dataset, batch_size, device, layout, rank=0, world_size=1, seed=0):
+    sampler = DistributedIndexSampler(len(dataset), world_size, rank, shuffle=True, seed=seed)
+    return DeviceLoader(dataset, batch_size, device, sampler=sampler, train=True, layout=layout, seed=seed + rank)
+
+
+def _loader_len(n, batch_size, world_size):
+    per_rank = -(-n // world_size)
+    return -(-per_rank // batch_size)
+
+
+def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distributed: bool = False):
+    device = resolve_device(args, local_rank)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    train_n = args.train_size if resolve_data(args) == "synthetic" else 50000
+    dataset, model, optimizer, testdata, scheduler = load_train_objs(
+        args, device, distributed, world_size, _loader_len(train_n, args.batch_size, world_size))
+    layout = input_layout(model, device, args.dtype)
+    train_data = prepare_dataloader(dataset, args.batch_size, device, layout, rank, world_size)
+    net = model
+    comm = None
+    if distributed:
+        if device.type == "cuda" and args.comm == "rccl":
+            comm = RcclComm(device)
+        else:
+            comm = TorchComm()
+        net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
+                                      first_bucket_mb=args.first_bucket_mb,
+                                      overlap_optimizer=args.overlap_optimizer)
+        if args.overlap_optimizer:
+            net.attach_optimizer(optimizer)
+    metrics = MetricsWriter(args.metrics, rank) if args.metrics else None
+    trainer = Trainer(net, train_data, optimizer, local_rank if device.type == "cuda" else rank, args.save_every,
+                      scheduler, distributed=distributed, rank=rank, graph=args.graph, metrics=metrics,
+                      full_checkpoint=args.full_checkpoint)
+    if args.resume and os.path.exists(FULL_CKPT_PATH):
+        trainer.start_epoch = load_full_checkpoint(FULL_CKPT_PATH, model, optimizer, scheduler,
+                                                   map_location=device)
+        if distributed:
+            net._broadcast_state()
+
+    start_time = time.time()
+    trainer.train(args.total_epochs)
+    end_time = time.time()
+    training_time = end_time - start_time
+    print(f"Total training time: {training_time:.2f} seconds")
+
+    fp32_model_size = get_model_size(model)
+    print(f"fp32 model has size={fp32_model_size / MiB:.2f} MiB")
+    if not args.no_eval:
+        test_data = DeviceLoader(testdata, args.eval_batch, device, train=False, layout=layout)
+        fp32_model_accuracy = evaluate(model, test_data)
+        print(f"fp32 model has accuracy={fp32_model_accuracy:.2f}%")
+    if metrics is not None:
+        metrics.log(event="done", training_time=training_time)
+        metrics.close()
+    if comm is not None:
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        if isinstance(net, DistributedDataParallel):
+            net.close()
+        comm.close()
+    return model
+
+
+# ------------------------------------------------------------------ multi
+def ddp_setup(rank: int, world_size: int, device_type: str):
+    """Rendezvous (reference: multigpu.py:24-33).  Env MASTER_ADDR/PORT win over the defaults."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "12355")
+    if device_type == "cuda":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)))
+        backend = "cpu:gloo,cuda:nccl"
+    else:
+        backend = "gloo"
+    dist.init_process_group(backend=backend, rank=rank, world_size=world_size)
+
+
+def main_multi(rank: int, world_size: int, args):
+    """Per-process entry (mp.spawn target or torchrun worker)."""
+    device_type = resolve_device(args).type
+    ddp_setup(rank, world_size, device_type)
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    try:
+        run(args, rank=rank, world_size=world_size, local_rank=local_rank, distributed=True)
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,127 @@
+"""Trainer — the reference's hot loop, MI355X-native underneath.
+
+Same structure, prints and checkpoint rule as ``Trainer`` in
+``/root/reference/singlegpu.py:85-128`` / ``multigpu.py:74-119``:
+
+* ``_run_batch``: zero_grad → forward → cross-entropy → backward →
+  optimizer.step → scheduler.step (per batch);
+* ``_run_epoch``: prints ``[GPU{id}] Epoch {e} | Batchsize: {b} | Steps: {n}``,
+  sets the sampler epoch (distributed), iterates the loader;
+* ``train``: saves ``checkpoint.pt`` when ``epoch % save_every == 0`` (rank 0
+  only when distributed).
+
+Differences (all deliberate):
+* batches are produced on the GPU (no H2D copy, no CPU augmentation);
+* the batch size for the print is computed, not by loading a throw-away batch
+  (the reference's ``len(next(iter(loader))[0])`` augments one extra batch);
+* the loss uses the model's fused ``forward_loss`` when it has one;
+* ``graph=True`` captures the full-size step into a HIP graph after
+  ``graph_warmup`` eager steps and replays it (partial last batch runs eager);
+* optional JSON-lines metrics (``metrics``) and full-state checkpoints.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..runtime.graphs import CapturedStep
+from . import checkpoint as ckpt
+
+
+class Trainer:
+    def __init__(self, model: nn.Module, train_data, optimizer, gpu_id, save_every: int, scheduler,
+                 distributed: bool = False, rank: int = 0, graph: bool = False, graph_warmup: int = 2,
+                 metrics=None, full_checkpoint: bool = False, ckpt_path: str = ckpt.CKPT_PATH) -> None:
+        self.gpu_id = gpu_id
+        self.model = model
+        self.train_data = train_data
+        self.optimizer = optimizer
+        self.save_every = save_every
+        self.scheduler = scheduler
+        self.distributed = distributed
+        self.rank = rank
+        self.use_graph = graph and torch.cuda.is_available() and next(model.parameters()).is_cuda
+        self.graph_warmup = graph_warmup
+        self.metrics = metrics
+        self.full_checkpoint = full_checkpoint
+        self.ckpt_path = ckpt_path
+        self._graph = None
+        self._graph_batch = None
+        self.global_step = 0
+        self.last_loss = None
+        self.start_epoch = 0
+
+    # ------------------------------------------------------------- one step
+    def _forward_loss(self, source, targets):
+        if hasattr(ckpt.unwrap(self.model), "forward_loss"):
+            loss, _ = self.model.forward_loss(source, targets)
+            return loss
+        output = self.model(source)
+        return F.cross_entropy(output, targets)
+
+    def _step_body(self, source, targets):
+        self.optimizer.zero_grad()
+        loss = self._forward_loss(source, targets)
+        loss.backward()
+        self.optimizer.step()
+        return loss
+
+    def _run_batch(self, source, targets):
+        bs = source.shape[0]
+        if self.use_graph and self._graph is None and self.global_step >= self.graph_warmup \
+                and self._graph_batch is None:
+            self._graph_batch = bs
+        if self.use_graph and self._graph_batch == bs:
+            if self._graph is None:
+                self.optimizer.sync_lr()
+                self._graph = CapturedStep(self._step_body, source, targets)
+            else:
+                self._graph.load(source, targets)
+            self.optimizer.sync_lr()
+            loss = self._graph()
+        else:
+            if hasattr(self.optimizer, "sync_lr"):
+                self.optimizer.sync_lr()
+            loss = self._step_body(source, targets)
+        self.scheduler.step()
+        self.global_step += 1
+        self.last_loss = loss
+        return loss
+
+    def _batch_size_for_print(self):
+        n = len(self.train_data.sampler) if hasattr(self.train_data, "sampler") else None
+        bs = self.train_data.batch_size
+        return min(bs, n) if n is not None else bs
+
+    def _run_epoch(self, epoch):
+        b_sz = self._batch_size_for_print()
+        print(f"[GPU{self.gpu_id}] Epoch {epoch} | Batchsize: {b_sz} | Steps: {len(self.train_data)}")
+        if hasattr(self.train_data, "set_epoch"):
+            self.train_data.set_epoch(epoch)
+        t0 = time.time()
+        n = 0
+        for source, targets in self.train_data:
+            self._run_batch(source, targets)
+            n += source.shape[0]
+        if self.metrics is not None:
+            loss = float(self.last_loss.detach().float().item()) if self.last_loss is not None else float("nan")
+            dt = time.time() - t0
+            self.metrics.log(epoch=epoch, step=self.global_step, loss=loss, samples=n, seconds=dt,
+                             samples_per_s=n / max(dt, 1e-9), lr=self.optimizer.param_groups[0]["lr"])
+
+    def _save_checkpoint(self, epoch):
+        path = ckpt.save_checkpoint(self.model, self.ckpt_path)
+        print(f"Epoch {epoch} | Training checkpoint saved at {path}")
+        if self.full_checkpoint:
+            ckpt.save_full_checkpoint(ckpt.FULL_CKPT_PATH, self.model, self.optimizer, self.scheduler, epoch)
+
+    def train(self, max_epochs: int):
+        for epoch in range(self.start_epoch, max_epochs):
+            self._run_epoch(epoch)
+            if (not self.distributed or self.rank == 0) and epoch % self.save_every == 0:
+                self._save_checkpoint(epoch)
+        if torch.cuda.is_available() and next(self.model.parameters()).is_cuda:
+            torch.cuda.synchronize()

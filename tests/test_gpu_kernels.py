@@ -1,0 +1,175 @@
+"""Numerics of every native HIP kernel vs a plain PyTorch fp32 reference of the same op."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _rand_bf16(*shape, dev):
+    return (torch.randn(*shape, device=dev) * 0.5).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72)])
+def test_gemm_layouts(gpu, tile, layout, MNK):
+    from ddpx.ops.gemm import matmul
+    M, N, K = MNK
+    ak, bk = layout
+    if not ak and M % 8:
+        pytest.skip("M-contig A requires M % 8 == 0")
+    torch.manual_seed(0)
+    A = _rand_bf16(M, K, dev=gpu)
+    B = _rand_bf16(K, N, dev=gpu)  # logical [K,N]
+    a_store = A if ak else A.t().contiguous()        # [M,K] or [K,M]
+    b_store = B.t().contiguous() if bk else B         # [N,K] or [K,N]
+    C = matmul(a_store, b_store, a_kcontig=ak, b_kcontig=bk, tile=tile)
+    ref = A.float() @ B.float()
+    assert _rel(C, ref) < 2e-3
+
+
+def test_gemm_identity_asymmetric(gpu):
+    """A = I with an asymmetric B catches a transposed C/D write (guide §3)."""
+    from ddpx.ops.gemm import matmul
+    n = 128
+    A = torch.eye(n, device=gpu, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=gpu, dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
+    for ak in (True, False):
+        for bk in (True, False):
+            C = matmul(A if ak else A.t().contiguous(), B.t().contiguous() if bk else B, a_kcontig=ak, b_kcontig=bk)
+            assert torch.equal(C, B.float()), (ak, bk)
+
+
+def test_linear_fwd_dgrad_wgrad(gpu):
+    from ddpx.ops import gemm as G
+    torch.manual_seed(1)
+    M, K, N = 512, 3072, 1024
+    x = _rand_bf16(M, K, dev=gpu)
+    w = _rand_bf16(N, K, dev=gpu)
+    b = torch.randn(N, device=gpu)
+    y = G.linear_fwd(x, w, b, relu=True)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    assert _rel(y, ref) < 5e-3
+    dy = _rand_bf16(M, N, dev=gpu)
+    dx = G.linear_dgrad(dy, w, relu_mask_of=x)
+    refdx = (dy.float() @ w.float()) * (x.float() > 0)
+    assert _rel(dx, refdx) < 5e-3
+    dw = torch.empty(N, K, device=gpu)
+    G.linear_wgrad(dy, x, dw)
+    refdw = dy.float().t() @ x.float()
+    assert _rel(dw, refdw) < 2e-3
+    G.linear_wgrad(dy, x, dw, accumulate=True)
+    assert _rel(dw, 2 * refdw) < 2e-3
+
+
+def test_head_fwd_bwd(gpu):
+    from ddpx.ops.head import head_backward, head_forward
+    torch.manual_seed(2)
+    M, K, C = 512, 4096, 10
+    h = torch.relu(_rand_bf16(M, K, dev=gpu).float()).to(torch.bfloat16)
+    w = _rand_bf16(C, K, dev=gpu)
+    b = torch.randn(C, device=gpu)
+    t = torch.randint(0, C, (M,), device=gpu)
+    correct = torch.zeros((), dtype=torch.int32, device=gpu)
+    loss, logits, dl = head_forward(h, w, b, t, correct=correct)
+    hf = h.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    bf = b.clone().requires_grad_(True)
+    ref_logits = hf @ wf.t() + bf
+    ref_loss = torch.nn.functional.cross_entropy(ref_logits, t)
+    assert _rel(logits, ref_logits) < 1e-4
+    assert abs(loss.item() - ref_loss.item()) < 1e-4 * max(1.0, abs(ref_loss.item()))
+    assert correct.item() == (ref_logits.argmax(1) == t).sum().item()
+    ref_loss.backward()
+    dW = torch.empty(C, K, device=gpu)
+    db = torch.empty(C, device=gpu)
+    dH = torch.empty_like(h)
+    dbp = torch.empty(K, device=gpu)
+    go = torch.tensor(1.0, device=gpu)
+    head_backward(dl, go, h, w, dW, db, dH=dH, dbprev=dbp, relu_mask=True)
+    assert _rel(dW, wf.grad) < 1e-4
+    assert _rel(db, bf.grad) < 1e-4
+    ref_dh = hf.grad * (h.float() > 0)
+    assert _rel(dH, ref_dh) < 5e-3
+    assert _rel(dbp, dH.float().sum(0)) < 1e-4
+
+
+def test_sgd_flat_matches_torch(gpu):
+    from ddpx.ops.elementwise import sgd_flat_
+    torch.manual_seed(3)
+    n = 100003
+    p = torch.randn(n, device=gpu)
+    g = torch.randn(n, device=gpu)
+    tp = p.clone().requires_grad_(False)
+    opt = torch.optim.SGD([torch.nn.Parameter(tp)], lr=0.4, momentum=0.9, weight_decay=5e-4)
+    buf = torch.zeros(n, device=gpu)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    lr_dev = torch.tensor(0.4, device=gpu)
+    for step in range(3):
+        opt.param_groups[0]["params"][0].grad = g.clone()
+        opt.step()
+        sgd_flat_(p, buf, g, sh, lr_dev if step % 2 else 0.4, 0.9, 5e-4)
+    ref = opt.param_groups[0]["params"][0].detach()
+    assert torch.allclose(p, ref, rtol=1e-5, atol=1e-6)
+    assert torch.equal(sh, p.to(torch.bfloat16))
+
+
+def test_colsum_and_cast(gpu):
+    from ddpx.ops.elementwise import cast_bf16_, colsum_bf16
+    x = _rand_bf16(517, 1000, dev=gpu)
+    out = torch.empty(1000, device=gpu)
+    colsum_bf16(x, out)
+    assert _rel(out, x.float().sum(0)) < 1e-5
+    f = torch.randn(12345, device=gpu)
+    bb = torch.empty(12345, dtype=torch.bfloat16, device=gpu)
+    cast_bf16_(f, bb)
+    assert torch.equal(bb, f.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("layout", ["nchw_f32", "nchw_bf16", "nhwc_bf16", "flat_bf16"])
+def test_augment_matches_cpu(gpu, layout):
+    from ddpx.data.datasets import synthetic_cifar
+    from ddpx.data.loader import augment_cpu, augment_gpu
+    ds = synthetic_cifar(300, seed=1)
+    idx = torch.randperm(300)[:77]
+    for train in (True, False):
+        xc, yc = augment_cpu(ds.images, ds.labels, idx, seed=12345, train=train, layout=layout)
+        xg, yg = augment_gpu(ds.images.to(gpu), ds.labels.to(gpu), idx.to(gpu), seed=12345, train=train,
+                             layout=layout)
+        assert torch.equal(yc, yg.cpu())
+        assert torch.equal(xc, xg.cpu())
+
+
+def test_mlp_native_matches_torch(gpu):
+    """Native fused MLP (loss + all grads) vs the same MLP in torch fp32 with bf16-rounded weights."""
+    import ddpx
+    from ddpx.models import MLP
+    torch.manual_seed(4)
+    m = MLP(hidden=512, layers=3)
+    ref = MLP(hidden=512, layers=3, compute_dtype=torch.float32)
+    ref.load_state_dict(m.state_dict())
+    ddpx.prepare_model(m, gpu)
+    ref.to(gpu)
+    with torch.no_grad():
+        for p in ref.parameters():
+            if p.dim() == 2:
+                p.copy_(p.to(torch.bfloat16).float())
+    x = torch.rand(256, 3072, device=gpu).to(torch.bfloat16)
+    t = torch.randint(0, 10, (256,), device=gpu)
+    loss, _ = m.forward_loss(x, t)
+    loss.backward()
+    rl = torch.nn.functional.cross_entropy(ref(x.float()), t)
+    rl.backward()
+    assert abs(loss.item() - rl.item()) < 2e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.main_grad, q.grad) < 3e-2, n
+
+
+def test_native_libs_loaded(gpu):
+    from ddpx.runtime import native
+    libs = native.loaded_libraries()
+    assert any("libddpx_kernels.so" in p for p in libs), libs
