@@ -64,7 +64,7 @@ def augment_cpu(images_u8, labels, idx, seed, train=True, pad=4, layout="nchw_f3
         out = xp[bi, ci, rows[:, None, :, None], cols[:, None, None, :]]
     else:
         out = x.float()
-    out = out / 255.0
+    out = out * (1.0 / 255.0)  # same fp32 constant multiply as the HIP kernel (bit-identical)
     if layout in ("nhwc_bf16", "nhwc_f32"):
         out = out.permute(0, 2, 3, 1).contiguous()
     if layout in ("flat_bf16", "flat_f32"):

@@ -54,6 +54,7 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--steps_per_epoch", default="compat", help="'compat' (98/49 as the reference), 'auto' or N")
     p.add_argument("--seed", type=int, default=None, help="seed model init (reference: unseeded)")
+    p.add_argument("--lr", type=float, default=REF_LR, help="peak LR of the one-cycle schedule (reference 0.4)")
     p.add_argument("--graph", action="store_true", help="capture the training step in a HIP graph")
     p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
@@ -98,7 +99,7 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels)
     prepare_model(model, device)
-    optimizer = SGD(model.parameters(), lr=REF_LR, momentum=REF_MOMENTUM, weight_decay=REF_WD,
+    optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"))
     spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)
     scheduler = one_cycle(optimizer, spe)

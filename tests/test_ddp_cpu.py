@@ -1,0 +1,126 @@
+"""ddpx DistributedDataParallel vs torch DDP on CPU gloo process groups (ws = 2, 4)."""
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from tests._dist_util import free_port, init_gloo
+
+
+def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps):
+    import ddpx
+    from ddpx.models import VGG, DeepNN
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from torch.nn.parallel import DistributedDataParallel as TorchDDP
+    init_gloo(rank, ws, port)
+    try:
+        torch.manual_seed(100 + rank)  # replicas start DIFFERENT: DDP init must broadcast rank 0
+        cls = {"vgg": VGG, "deepnn": DeepNN}[model_name]
+        ours = cls()
+        ref = cls()
+        if model_name == "deepnn":
+            ours.classifier[2].p = 0.0
+            ref.classifier[2].p = 0.0
+        ref.load_state_dict(ours.state_dict())
+        ddpx.prepare_model(ours, "cpu")
+        d_ours = DistributedDataParallel(ours, comm=TorchComm(), bucket_cap_mb=bucket_mb, first_bucket_mb=0.25,
+                                         overlap_optimizer=overlap)
+        d_ref = TorchDDP(ref, bucket_cap_mb=bucket_mb)
+        o_ours = SGD(ours.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+        if overlap:
+            d_ours.attach_optimizer(o_ours)
+        o_ref = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+        # after construction both replicas equal rank 0's initial state
+        for p, q in zip(ours.parameters(), ref.parameters()):
+            assert torch.allclose(p, q), "init broadcast mismatch"
+        g = torch.Generator().manual_seed(rank)
+        for _ in range(steps):
+            x = torch.rand((4, 3, 32, 32), generator=g)
+            t = torch.randint(0, 10, (4,), generator=g)
+            for net, opt in ((d_ours, o_ours), (d_ref, o_ref)):
+                opt.zero_grad()
+                F.cross_entropy(net(x), t).backward()
+                opt.step()
+        for (n, p), (_, q) in zip(ours.named_parameters(), ref.named_parameters()):
+            assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), (rank, n, (p - q).abs().max().item())
+        for (n, b), (_, c) in zip(ours.named_buffers(), ref.named_buffers()):
+            assert torch.allclose(b.float(), c.float(), atol=2e-5, rtol=1e-4), (rank, n)
+        # replicas identical across ranks
+        flat = ours.parameters().__iter__().__next__()._ddpx_flat.master.clone()
+        lst = [torch.empty_like(flat) for _ in range(ws)]
+        dist.all_gather(lst, flat)
+        for other in lst:
+            assert torch.equal(other, lst[0])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,model,overlap,bucket", [
+    (2, "deepnn", False, 25.0),
+    (2, "vgg", False, 25.0),
+    (2, "vgg", True, 4.0),
+    (4, "deepnn", True, 1.0),
+])
+def test_ddp_matches_torch_ddp(ws, model, overlap, bucket):
+    mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3), nprocs=ws, join=True)
+
+
+def _no_sync_worker(rank, ws, port):
+    import ddpx
+    from ddpx.models import DeepNN
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    init_gloo(rank, ws, port)
+    try:
+        torch.manual_seed(0)
+        m = DeepNN()
+        m.classifier[2].p = 0.0
+        single = DeepNN()
+        single.classifier[2].p = 0.0
+        single.load_state_dict(m.state_dict())
+        ddpx.prepare_model(m, "cpu")
+        d = DistributedDataParallel(m, comm=TorchComm())
+        opt = SGD(m.parameters(), lr=0.1)
+        # two micro-batches per rank, accumulated locally, one all-reduce
+        xs = [torch.rand((2, 3, 32, 32), generator=torch.Generator().manual_seed(10 * r + k))
+              for r in range(ws) for k in range(2)]
+        ts = [torch.randint(0, 10, (2,), generator=torch.Generator().manual_seed(10 * r + k + 5))
+              for r in range(ws) for k in range(2)]
+        opt.zero_grad()
+        with d.no_sync():
+            F.cross_entropy(d(xs[2 * rank]), ts[2 * rank]).backward()
+        F.cross_entropy(d(xs[2 * rank + 1]), ts[2 * rank + 1]).backward()
+        opt.step()
+        # reference: full-batch gradient on one process = mean over ranks of summed micro-batch grads
+        so = torch.optim.SGD(single.parameters(), lr=0.1)
+        so.zero_grad()
+        loss = sum(F.cross_entropy(single(x), t) for x, t in zip(xs, ts)) / ws
+        loss.backward()
+        so.step()
+        for p, q in zip(m.parameters(), single.parameters()):
+            assert torch.allclose(p, q, atol=1e-5, rtol=1e-4)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_no_sync_accumulation():
+    mp.spawn(_no_sync_worker, args=(2, free_port()), nprocs=2, join=True)
+
+
+def _fail_worker(rank, ws, port):
+    init_gloo(rank, ws, port)
+    if rank == 1:
+        raise RuntimeError("injected failure on rank 1")
+    dist.barrier()  # rank 0 would hang here without failure propagation
+
+
+def test_rank_failure_propagates():
+    import time
+    t0 = time.time()
+    with pytest.raises(Exception, match="injected failure"):
+        mp.spawn(_fail_worker, args=(2, free_port()), nprocs=2, join=True)
+    assert time.time() - t0 < 120

@@ -1,0 +1,81 @@
+"""singlegpu.py / multigpu.py as the reference's users run them (CPU, gloo)."""
+import os
+import re
+import subprocess
+import sys
+
+import torch
+
+from tests._dist_util import free_port
+from tests.test_models import VanillaVGG
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, cwd, extra_env=None, timeout=600):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT
+    env["OMP_NUM_THREADS"] = "2"
+    if extra_env:
+        env.update(extra_env)
+    r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return r.stdout
+
+
+def test_singlegpu_cpu_vgg_prints_and_checkpoint(tmp_path):
+    out = _run([os.path.join(ROOT, "singlegpu.py"), "2", "1", "--batch_size", "64", "--device", "cpu",
+                "--data", "synthetic", "--train_size", "256", "--test_size", "128"], tmp_path)
+    lines = out.splitlines()
+    assert "[GPU0] Epoch 0 | Batchsize: 64 | Steps: 4" in lines
+    assert "Epoch 0 | Training checkpoint saved at checkpoint.pt" in lines
+    assert "Epoch 1 | Training checkpoint saved at checkpoint.pt" in lines
+    assert any(re.fullmatch(r"Total training time: \d+\.\d\d seconds", ln) for ln in lines)
+    assert "fp32 model has size=35.20 MiB" in lines
+    assert any(re.search(r"fp32 model has accuracy=\d+\.\d\d%", ln) for ln in lines)
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    assert len(sd) == 50 and "backbone.conv0.weight" in sd and not any(k.startswith("module.") for k in sd)
+    VanillaVGG().load_state_dict(sd, strict=True)
+
+
+def test_singlegpu_cpu_mlp_learns(tmp_path):
+    out = _run([os.path.join(ROOT, "singlegpu.py"), "3", "5", "--model", "mlp", "--hidden", "128",
+                "--batch_size", "128", "--device", "cpu", "--data", "synthetic", "--train_size", "2048",
+                "--test_size", "512", "--steps_per_epoch", "auto", "--metrics", "m.jsonl", "--lr", "0.02"], tmp_path)
+    acc = float(re.search(r"accuracy=(\d+\.\d\d)%", out).group(1))
+    assert acc > 30.0, out  # learnable synthetic data: well above chance (10%)
+    assert (tmp_path / "m.jsonl").exists()
+
+
+def test_multigpu_cpu_spawn(tmp_path):
+    out = _run([os.path.join(ROOT, "multigpu.py"), "1", "1", "--batch_size", "32", "--device", "cpu",
+                "--nprocs", "2", "--model", "deepnn", "--data", "synthetic", "--train_size", "256",
+                "--test_size", "64"], tmp_path, extra_env={"MASTER_PORT": str(free_port())})
+    # two processes share the pipe: lines may interleave, so check substrings
+    assert "[GPU0] Epoch 0 | Batchsize: 32 | Steps: 4" in out
+    assert "[GPU1] Epoch 0 | Batchsize: 32 | Steps: 4" in out
+    assert out.count("Epoch 0 | Training checkpoint saved at checkpoint.pt") == 1  # rank 0 only
+    assert out.count("Total training time:") == 2  # every rank
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    assert not any(k.startswith("module.") for k in sd)
+
+
+def test_multigpu_torchrun(tmp_path):
+    out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr", "127.0.0.1",
+                "--master-port", str(free_port()), os.path.join(ROOT, "multigpu.py"), "1", "1", "--batch_size", "64",
+                "--device", "cpu", "--model", "mlp", "--hidden", "64", "--data", "synthetic", "--train_size", "512",
+                "--test_size", "64", "--no_eval"], tmp_path)
+    assert "[GPU0] Epoch 0 | Batchsize: 64 | Steps: 4" in out
+    assert "[GPU1] Epoch 0 | Batchsize: 64 | Steps: 4" in out
+
+
+def test_resume_full_checkpoint(tmp_path):
+    common = [os.path.join(ROOT, "singlegpu.py"), "--model", "mlp", "--hidden", "64", "--batch_size", "64",
+              "--device", "cpu", "--data", "synthetic", "--train_size", "256", "--test_size", "64", "--no_eval",
+              "--full_checkpoint", "--seed", "0"]
+    _run([common[0], "2", "1", *common[1:]], tmp_path)
+    out = _run([common[0], "3", "1", *common[1:], "--resume"], tmp_path)
+    assert "[GPU0] Epoch 0" not in out and "[GPU0] Epoch 2 | Batchsize: 64 | Steps: 4" in out
+    st = torch.load(tmp_path / "checkpoint_full.pt", weights_only=True)
+    assert st["epoch"] == 2 and st["optimizer"]["state"]
