@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--overlap_optimizer", action="store_true")
+    p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="gradient buffer / all-reduce dtype (bf16 = values of bf16 MFMA wgrads, as autocast)")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
@@ -95,7 +97,7 @@ def build_ddpx(args, device, world):
     from ddpx.runtime.setup import prepare_model
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16" if args.model != "vgg"
                         else "fp32", device=device)
-    prepare_model(model, device)
+    prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph)
     net = model
     if world > 1:
@@ -218,7 +220,7 @@ def main():
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
-                   "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)", "grad_comm": "fp32",
+                   "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)", "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4)},
     }
     if rank == 0:

@@ -22,16 +22,30 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-// One thread per (sample, channel, row): 32 output pixels.
+// NCHW / flat layouts: one thread per (sample, channel, row, 8-pixel group);
+// each thread gathers its 8 source bytes (L2/Infinity-Cache hits) and writes
+// 8 contiguous outputs with one 16-B (bf16) or two 16-B (fp32) stores.
+// NHWC layouts: one thread per (sample, row, pixel), C channels each.
 __global__ void __launch_bounds__(256)
 augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
                const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad, uint64_t seed,
                int train, int layout, void* __restrict__ out, int64_t* __restrict__ tgt_out) {
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32);
+  const int G = W / 8;  // 8-pixel groups per row (W % 8 == 0 checked on the host)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= B * C * H) return;
-  const int y = t % H;
-  const int c = (t / H) % C;
-  const int b = t / (H * C);
+  const int total = nhwc ? B * H * W : B * C * H * G;
+  if (t >= total) return;
+  int b, c = 0, y, xg = 0, xo = 0;
+  if (nhwc) {
+    xo = t % W;
+    y = (t / W) % H;
+    b = t / (W * H);
+  } else {
+    xg = t % G;
+    y = (t / G) % H;
+    c = (t / (G * H)) % C;
+    b = t / (G * H * C);
+  }
   const int64_t src = idx ? idx[b] : b;
   int dy = pad, dx = pad, flip = 0;
   if (train) {
@@ -40,29 +54,39 @@ augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ l
     dx = (int)((r >> 16) % (uint64_t)(2 * pad + 1));
     flip = (int)((r >> 40) & 1);
   }
-  if (tgt_out && c == 0 && y == 0) tgt_out[b] = labels[src];
-  const uint8_t* img = images + (size_t)src * C * H * W + (size_t)c * H * W;
+  if (tgt_out && y == 0 && c == 0 && xg == 0 && xo == 0) tgt_out[b] = labels[src];
   const int sy = y + dy - pad;
   const bool row_ok = (sy >= 0) && (sy < H);
   const float inv = 1.f / 255.f;
-  for (int x = 0; x < W; ++x) {
-    const int ox = flip ? (W - 1 - x) : x;  // flip applied after the crop
+  const uint8_t* img = images + (size_t)src * C * H * W;
+  if (!nhwc) {
+    const uint8_t* row = img + (size_t)c * H * W + (size_t)(row_ok ? sy : 0) * W;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ox = xg * 8 + j;                 // output column
+      const int x = flip ? (W - 1 - ox) : ox;    // column of the cropped image
+      const int sx = x + dx - pad;
+      v[j] = (row_ok && sx >= 0 && sx < W) ? (float)row[sx] * inv : 0.f;
+    }
+    const size_t o = (((size_t)b * C + c) * H + y) * W + xg * 8;
+    if (layout == OUT_NCHW_BF16) {
+      u32x4 pk = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+      *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned short*>(out) + o) = pk;
+    } else {
+      f32x4* d = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + o);
+      d[0] = (f32x4){v[0], v[1], v[2], v[3]};
+      d[1] = (f32x4){v[4], v[5], v[6], v[7]};
+    }
+  } else {
+    const int x = flip ? (W - 1 - xo) : xo;
     const int sx = x + dx - pad;
-    float v = 0.f;
-    if (row_ok && sx >= 0 && sx < W) v = (float)img[sy * W + sx] * inv;
-    switch (layout) {
-      case OUT_NCHW_F32:
-        reinterpret_cast<float*>(out)[(((size_t)b * C + c) * H + y) * W + ox] = v;
-        break;
-      case OUT_NCHW_BF16:
-        reinterpret_cast<unsigned short*>(out)[(((size_t)b * C + c) * H + y) * W + ox] = f2bf(v);
-        break;
-      case OUT_NHWC_BF16:
-        reinterpret_cast<unsigned short*>(out)[(((size_t)b * H + y) * W + ox) * C + c] = f2bf(v);
-        break;
-      default:
-        reinterpret_cast<float*>(out)[(((size_t)b * H + y) * W + ox) * C + c] = v;
-        break;
+    const bool ok = row_ok && sx >= 0 && sx < W;
+    const size_t o = (((size_t)b * H + y) * W + xo) * C;
+    for (int cc = 0; cc < C; ++cc) {
+      const float v = ok ? (float)img[(size_t)cc * H * W + sy * W + sx] * inv : 0.f;
+      if (layout == OUT_NHWC_BF16) reinterpret_cast<unsigned short*>(out)[o + cc] = f2bf(v);
+      else reinterpret_cast<float*>(out)[o + cc] = v;
     }
   }
 }
@@ -75,7 +99,9 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
                           int W, int pad, uint64_t seed, int train, int layout, void* out, int64_t* tgt_out,
                           hipStream_t s) {
   if (B <= 0) return 0;
-  const int n = B * C * H;
+  if (W % 8) return -1;
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32);
+  const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);
   return (int)hipGetLastError();

@@ -1,87 +1,115 @@
-// ddpx — fused classifier head: Linear(K -> C) + softmax cross-entropy
-// (forward) and its backward fused with the preceding ReLU's mask and bias
+// ddpx — fused classifier head: Linear(K -> C<=16) + softmax cross-entropy
+// (forward), and its backward fused with the preceding ReLU's mask and bias
 // gradient.
 //
 // Reference ops replaced:
 //   classifier Linear  /root/reference/singlegpu.py:73,81 (`self.classifier(x)`)
 //   F.cross_entropy    /root/reference/singlegpu.py:105
 //   argmax/eq/sum eval /root/reference/singlegpu.py:200-206
-// With C = 10 classes the head is far too skinny for MFMA tiles (N = 10): it is
-// a streaming dot-product problem, so it runs one wave per sample row with
-// 16-B vector loads, the 10 logits reduced across the 64 lanes by shuffles,
-// and the whole softmax / NLL / dlogits / argmax done in registers.
+//
+// With C = 10 classes the head is skinny (N = 10): the work is a few MFLOP
+// and a few MB of streaming, so the design goal is PARALLELISM and no long
+// dependent chains:
+//   forward  = split-K MFMA partial logits (16 rows x 16 padded classes per
+//              workgroup slice, 4 waves split the slice's K) + a row-parallel
+//              finalize (bias, log-softmax, NLL, dlogits, argmax) + a
+//              deterministic mean;
+//   backward = row-split x column-tile workgroups (>= 256 of them) that
+//              each produce dH for their tile and partial dW / bias sums,
+//              followed by a fixed-order reduction of the partials
+//              (bitwise reproducible, no float atomics).
 #include "ddpx_common.h"
 
 namespace ddpx {
 
-// Forward: one wave per row m.
-//   logits[m][c] = sum_k H[m][k] * W[c][k] + b[c]          (fp32 out, optional)
-//   loss_rows[m] = logsumexp(logits[m]) - logits[m][t_m]   (optional)
-//   dlogits[m][c] = (softmax[m][c] - [c==t_m]) * inv_m       (optional)
-//   correct += [argmax(logits[m]) == t_m]                  (optional)
-template <int C>
+constexpr int kHeadC = 16;  // classes padded to one MFMA tile
+
+// partial[ks][m][16] = sum_{k in slice ks} H[m][k] * W[c][k]   (c >= C -> 0)
 __global__ void __launch_bounds__(256)
-head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __restrict__ W,
-                const float* __restrict__ b, const int64_t* __restrict__ tgt, int M, int K, int ldh,
-                float inv_m, float* __restrict__ logits, float* __restrict__ loss_rows,
-                float* __restrict__ dlogits, int* __restrict__ correct) {
-  const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= M) return;
-  float acc[C];
+head_logits_partial_kernel(const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M,
+                           int K, int C, int ldh, int kslice, float* __restrict__ partial) {
+  __shared__ float red[4][16][17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 16, ks = blockIdx.y;
+  const int kbeg = ks * kslice;
+  const int kend = min(K, kbeg + kslice);
+  const int wlen = (kslice + 3) / 4;
+  const int wb = kbeg + wave * wlen;
+  const int we = min(kend, wb + wlen);
+  const int row = m0 + (lane & 15);
+  const int cls = lane & 15;
+  const int ko = 8 * (lane >> 4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k = wb; k < we; k += 32) {
+    const int kk = k + ko;
+    u32x4 av = {0u, 0u, 0u, 0u}, bv = {0u, 0u, 0u, 0u};
+    if (row < M && kk < we) av = *reinterpret_cast<const u32x4*>(H + (size_t)row * ldh + kk);
+    if (cls < C && kk < we) bv = *reinterpret_cast<const u32x4*>(W + (size_t)cls * K + kk);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
+                                                  acc, 0, 0, 0);
+  }
+  // C/D map: col (class) = lane&15, row = 4*(lane>>4) + r
 #pragma unroll
-  for (int c = 0; c < C; ++c) acc[c] = 0.f;
-  const unsigned short* hrow = H + (size_t)m * ldh;
-  for (int k = lane * 8; k < K; k += 512) {
-    const u32x4 hv = *reinterpret_cast<const u32x4*>(hrow + k);
-    float h[8];
+  for (int r = 0; r < 4; ++r) red[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  const int t = threadIdx.x;
+  const int rr = t >> 4, cc = t & 15;
+  const float s = (red[0][rr][cc] + red[1][rr][cc]) + (red[2][rr][cc] + red[3][rr][cc]);
+  if (m0 + rr < M) partial[((size_t)ks * M + m0 + rr) * kHeadC + cc] = s;
+}
+
+// One thread per row: logits, log-softmax, NLL, dlogits, argmax.
+__global__ void __launch_bounds__(256)
+head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
+                     const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
+                     float* __restrict__ loss_rows, float* __restrict__ dlogits, int* __restrict__ correct) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  int hit = 0;
+  if (m < M) {
+    float z[kHeadC];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      h[2 * j] = __uint_as_float(hv[j] << 16);
-      h[2 * j + 1] = __uint_as_float(hv[j] & 0xffff0000u);
-    }
+    for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
+    for (int ks = 0; ks < KS; ++ks) {
+      const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const u32x4 wv = *reinterpret_cast<const u32x4*>(W + (size_t)c * K + k);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[c] = fmaf(h[2 * j], __uint_as_float(wv[j] << 16), acc[c]);
-        acc[c] = fmaf(h[2 * j + 1], __uint_as_float(wv[j] & 0xffff0000u), acc[c]);
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = pp[q];
+        z[4 * q] += v[0];
+        z[4 * q + 1] += v[1];
+        z[4 * q + 2] += v[2];
+        z[4 * q + 3] += v[3];
       }
     }
-  }
-  float z[C];
+    float mx = -INFINITY;
+    int am = 0;
 #pragma unroll
-  for (int c = 0; c < C; ++c) z[c] = wave_sum(acc[c]) + b[c];
-  // every lane now holds all C logits
-  float mx = z[0];
-  int am = 0;
-#pragma unroll
-  for (int c = 1; c < C; ++c)
-    if (z[c] > mx) { mx = z[c]; am = c; }
-  float se = 0.f;
-#pragma unroll
-  for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
-  const float lse = mx + __logf(se);
-  const int t = tgt ? (int)tgt[m] : 0;
-  if (lane < C) {
-    float zc = z[0];
-#pragma unroll
-    for (int c = 1; c < C; ++c) zc = (lane == c) ? z[c] : zc;
-    if (logits) logits[(size_t)m * C + lane] = zc;
-    if (dlogits) {
-      const float pr = __expf(zc - lse);
-      dlogits[(size_t)m * C + lane] = (pr - (lane == t ? 1.f : 0.f)) * inv_m;
+    for (int c = 0; c < kHeadC; ++c) {
+      if (c < C) {
+        z[c] += b[c];
+        if (z[c] > mx) { mx = z[c]; am = c; }
+      }
     }
-  }
-  if (lane == 0) {
-    if (loss_rows) {
-      float zt = z[0];
+    float se = 0.f;
 #pragma unroll
-      for (int c = 1; c < C; ++c) zt = (t == c) ? z[c] : zt;
-      loss_rows[m] = lse - zt;
+    for (int c = 0; c < kHeadC; ++c)
+      if (c < C) se += __expf(z[c] - mx);
+    const float lse = mx + __logf(se);
+    const int t = tgt ? (int)tgt[m] : 0;
+    float zt = 0.f;
+#pragma unroll
+    for (int c = 0; c < kHeadC; ++c) {
+      if (c < C) {
+        if (c == t) zt = z[c];
+        if (logits) logits[(size_t)m * C + c] = z[c];
+        if (dlogits) dlogits[(size_t)m * C + c] = (__expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * inv_m;
+      }
     }
-    if (correct && am == t) atomicAdd(correct, 1);
+    if (loss_rows) loss_rows[m] = lse - zt;
+    hit = tgt ? (am == t) : 0;
+  }
+  if (correct) {
+    const unsigned long long bal = __ballot(hit);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(correct, __popcll(bal));  // integer: deterministic
   }
 }
 
@@ -100,25 +128,26 @@ __global__ void __launch_bounds__(1024) mean_kernel(const float* __restrict__ x,
   }
 }
 
-// Backward.  One workgroup per 64-column slice of K, looping over all M rows
-// (8 lanes x 8 bf16 per row, 32 rows in flight per workgroup):
-//   g[m][k]    = go * sum_c dlogits[m][c] * W[c][k]
-//   dH[m][k]   = relu_mask ? g * (H[m][k] > 0) : g                  (bf16)
-//   dW[c][k]  (=|+=) go * sum_m dlogits[m][c] * H[m][k]            (fp32)
-//   dbprev[k] (=|+=) sum_m dH[m][k]        (bias grad of the layer that produced H)
-//   db[c]     (=|+=) go * sum_m dlogits[m][c]                        (workgroup 0)
+// Backward partials.  Workgroup (column tile ct of 64, row split rs):
+//   g[m][k]  = go * sum_c dlogits[m][c] * W[c][k]
+//   dH[m][k] = relu_mask ? g * (H[m][k] > 0) : g                       (bf16, stored)
+//   pdw[rs][c][k]  = go * sum_{m in split} dlogits[m][c] * H[m][k]
+//   pdb[rs][k]     = sum_{m in split} dH[m][k]     (bias grad of the layer that produced H)
+// 8 lanes x 8 columns per row, 32 rows per pass, ROWS_PER_SPLIT/32 passes.
 template <int C>
 __global__ void __launch_bounds__(256)
-head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
-                const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K,
-                int ldh, unsigned short* __restrict__ dH, float* __restrict__ dW, float* __restrict__ db,
-                float* __restrict__ dbprev, int relu_mask, int accumulate) {
+head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
+                        const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K,
+                        int ldh, int rows_per_split, unsigned short* __restrict__ dH, float* __restrict__ pdw,
+                        float* __restrict__ pdb, int relu_mask) {
   __shared__ float red[4][64][C + 1];
   const float go = go_ptr ? *go_ptr : 1.f;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int cg = tid & 7;         // column group: 8 columns
-  const int r0 = tid >> 3;        // 0..31 row within a 32-row slab
+  const int cg = tid & 7, r0 = tid >> 3;
   const int k = blockIdx.x * 64 + cg * 8;
+  const int rs = blockIdx.y;
+  const int mbeg = rs * rows_per_split;
+  const int mend = min(M, mbeg + rows_per_split);
   float wv[C][8];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -129,15 +158,14 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
       wv[c][2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
     }
   }
-  float dw[C][8];
-  float dbp[8];
+  float dw[C][8], dbp[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     dbp[j] = 0.f;
 #pragma unroll
     for (int c = 0; c < C; ++c) dw[c][j] = 0.f;
   }
-  for (int m = r0; m < M; m += 32) {
+  for (int m = mbeg + r0; m < mend; m += 32) {
     float dl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) dl[c] = dlogits[(size_t)m * C + c] * go;
@@ -163,14 +191,12 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = pack_bf2(g[2 * j], g[2 * j + 1]);
     if (dH) *reinterpret_cast<u32x4*>(dH + (size_t)m * ldh + k) = o;
-    // bias grad of the producing layer from the bf16-rounded values actually stored
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       dbp[2 * j] += __uint_as_float(o[j] << 16);
       dbp[2 * j + 1] += __uint_as_float(o[j] & 0xffff0000u);
     }
   }
-  // reduce over the 8 row-lanes of a wave that share a column group (lane bits 3..5)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
 #pragma unroll
@@ -189,25 +215,51 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
     }
   }
   __syncthreads();
-  // 64 columns x (C + 1) outputs per workgroup
   for (int i = tid; i < 64 * (C + 1); i += 256) {
     const int col = i % 64, c = i / 64;
     const float s = (red[0][col][c] + red[1][col][c]) + (red[2][col][c] + red[3][col][c]);
     const int kk = blockIdx.x * 64 + col;
-    if (c < C) {
-      float* d = dW + (size_t)c * K + kk;
-      *d = accumulate ? *d + s : s;
-    } else if (dbprev) {
-      dbprev[kk] = accumulate ? dbprev[kk] + s : s;
-    }
+    if (c < C) pdw[((size_t)rs * C + c) * K + kk] = s;
+    else pdb[(size_t)rs * K + kk] = s;
   }
-  if (blockIdx.x == 0 && db && w == 0) {
-    // db[c] = go * sum_m dlogits[m][c]
+}
+
+// Fixed-order reduction of the row-split partials into the gradient buffers
+// (fp32 or bf16, write or accumulate) + the head bias gradient (workgroup 0).
+template <int C>
+__global__ void __launch_bounds__(256)
+head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict__ pdb, int RS, int K,
+                         const float* __restrict__ dlogits, const float* __restrict__ go_ptr, int M,
+                         void* __restrict__ dW, void* __restrict__ db, void* __restrict__ dbprev, int out_bf16,
+                         int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over (C+1)*K
+  auto put = [&](void* base, size_t idx, float v) {
+    if (out_bf16) {
+      unsigned short* o = reinterpret_cast<unsigned short*>(base) + idx;
+      *o = f2bf(accumulate ? v + bf2f(*o) : v);
+    } else {
+      float* o = reinterpret_cast<float*>(base) + idx;
+      *o = accumulate ? v + *o : v;
+    }
+  };
+  if (i < C * K) {
+    float s = 0.f;
+    for (int r = 0; r < RS; ++r) s += pdw[(size_t)r * C * K + i];
+    put(dW, i, s);
+  } else if (i < (C + 1) * K && dbprev) {
+    const int kk = i - C * K;
+    float s = 0.f;
+    for (int r = 0; r < RS; ++r) s += pdb[(size_t)r * K + kk];
+    put(dbprev, kk, s);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64 && db) {
+    const float go = go_ptr ? *go_ptr : 1.f;
+    const int lane = threadIdx.x;
     for (int c = 0; c < C; ++c) {
       float s = 0.f;
       for (int m = lane; m < M; m += 64) s += dlogits[(size_t)m * C + c];
       s = wave_sum(s) * go;
-      if (lane == 0) db[c] = accumulate ? db[c] + s : s;
+      if (lane == 0) put(db, c, s);
     }
   }
 }
@@ -225,23 +277,50 @@ accuracy_kernel(const float* __restrict__ logits, const int64_t* __restrict__ tg
       if (z[c] > mx) { mx = z[c]; am = c; }
     hit = (am == (int)tgt[m]);
   }
-  // wave-aggregated integer atomic (deterministic result)
   const unsigned long long bal = __ballot(hit);
   if ((threadIdx.x & 63) == 0 && bal) atomicAdd(correct, __popcll(bal));
+}
+
+static int head_ksplit(int M, int K) {
+  const int row_tiles = (M + 15) / 16;
+  int ks = (256 + row_tiles - 1) / row_tiles;
+  const int maxks = max(1, K / 128);
+  if (ks > maxks) ks = maxks;
+  if (ks < 1) ks = 1;
+  return ks;
+}
+
+static int head_row_splits(int M, int K) {
+  const int ctiles = K / 64;
+  int rs = (256 + ctiles - 1) / ctiles;
+  const int maxrs = max(1, M / 32);
+  if (rs > maxrs) rs = maxrs;
+  return max(rs, 1);
 }
 
 }  // namespace ddpx
 
 using namespace ddpx;
 
-DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K,
-                           int C, int ldh, float inv_m, float* logits, float* loss_rows, float* dlogits,
-                           int* correct, hipStream_t s) {
+// Scratch sizes (floats) the host must provide for the head kernels.
+DDPX_API int64_t ddpx_head_fwd_scratch(int M, int K) { return (int64_t)head_ksplit(M, K) * M * kHeadC; }
+DDPX_API int64_t ddpx_head_bwd_scratch(int M, int K, int C) {
+  return (int64_t)head_row_splits(M, K) * (C + 1) * K;
+}
+
+DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K, int C,
+                           int ldh, float inv_m, float* logits, float* loss_rows, float* dlogits, int* correct,
+                           float* scratch, hipStream_t s) {
   if (M <= 0) return 0;
-  if (C != 10) return -1;
+  if (C < 1 || C > kHeadC) return -1;
   if (K % 8 || ldh % 8) return -2;
-  hipLaunchKernelGGL(head_fwd_kernel<10>, dim3((M + 3) / 4), dim3(256), 0, s, (const unsigned short*)H,
-                     (const unsigned short*)W, b, tgt, M, K, ldh, inv_m, logits, loss_rows, dlogits, correct);
+  const int ks = head_ksplit(M, K);
+  int kslice = (K + ks - 1) / ks;
+  kslice = (kslice + 127) / 128 * 128;  // whole 32-k MFMA steps for each of the 4 waves
+  hipLaunchKernelGGL(head_logits_partial_kernel, dim3((M + 15) / 16, ks), dim3(256), 0, s, (const unsigned short*)H,
+                     (const unsigned short*)W, M, K, C, ldh, kslice, scratch);
+  hipLaunchKernelGGL(head_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                     logits, loss_rows, dlogits, correct);
   return (int)hipGetLastError();
 }
 
@@ -250,15 +329,21 @@ DDPX_API int ddpx_mean(const float* x, int n, float* out, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K,
-                           int C, int ldh, void* dH, float* dW, float* db, float* dbprev, int relu_mask,
-                           int accumulate, hipStream_t s) {
+DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K, int C,
+                           int ldh, void* dH, void* dW, void* db, void* dbprev, int relu_mask, int out_bf16,
+                           int accumulate, float* scratch, hipStream_t s) {
   if (M <= 0) return 0;
   if (C != 10) return -1;
   if (K % 64 || ldh % 8) return -2;
-  hipLaunchKernelGGL(head_bwd_kernel<10>, dim3(K / 64), dim3(256), 0, s, dlogits, go, (const unsigned short*)H,
-                     (const unsigned short*)W, M, K, ldh, (unsigned short*)dH, dW, db, dbprev, relu_mask,
-                     accumulate);
+  const int rs = head_row_splits(M, K);
+  const int rps = (M + rs - 1) / rs;
+  float* pdw = scratch;
+  float* pdb = scratch + (size_t)rs * C * K;
+  hipLaunchKernelGGL(head_bwd_partial_kernel<10>, dim3(K / 64, rs), dim3(256), 0, s, dlogits, go,
+                     (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, rps, (unsigned short*)dH, pdw, pdb,
+                     relu_mask);
+  hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + 255) / 256), dim3(256), 0, s, pdw, pdb, rs, K,
+                     dlogits, go, M, dW, db, dbprev, out_bf16, accumulate);
   return (int)hipGetLastError();
 }
 

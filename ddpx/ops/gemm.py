@@ -15,9 +15,14 @@ wgrad      dW[N,K] = dY[M,N]ᵀ · X[M,K]   M-contig     N-contig
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..runtime import native
+
+# "pipe" (LDS-DMA multi-stage ring, default) or "v1" (register-staged, 2 LDS buffers)
+GEMM_IMPL = os.environ.get("DDPX_GEMM", "pipe")
 
 EPI_F32 = 0
 EPI_BF16 = 1
@@ -51,14 +56,33 @@ def _check_bf16_2d(t, name):
 
 
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
-             accumulate=False, alpha=1.0, tile=-1, stream=None):
+             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None):
     lib = native.kernels()
-    rc = lib.ddpx_gemm_bf16(
-        a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux), M, N, K, lda, ldb, ldc,
-        ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate), float(alpha), tile,
-        native.stream_handle(stream))
-    native.check(rc, f"ddpx_gemm_bf16(M={M},N={N},K={K},epi={epi})")
+    impl = impl or GEMM_IMPL
+    s = native.stream_handle(stream)
+    if impl == "v1":
+        if colsum is not None:
+            raise ValueError("v1 GEMM has no fused column sum")
+        rc = lib.ddpx_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux), M, N, K,
+                                lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate),
+                                float(alpha), tile, s)
+    else:
+        rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
+                                native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
+                                int(accumulate), float(alpha), tile, s)
+    native.check(rc, f"ddpx_gemm_{impl}(M={M},N={N},K={K},epi={epi})")
     return c
+
+
+def tiles_m(M, N, tile=-1):
+    return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, tile)
+
+
+def reduce_partials(part, T, N, out, accumulate=False):
+    lib = native.kernels()
+    native.check(lib.ddpx_reduce_partials(part.data_ptr(), T, N, out.data_ptr(), int(out.dtype == torch.bfloat16),
+                                          int(accumulate), native.stream_handle()), "ddpx_reduce_partials")
+    return out
 
 
 def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, tile=-1):
@@ -83,8 +107,12 @@ def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, 
                     b_kcontig=True, epi=epi, bias=bias, tile=tile)
 
 
-def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1):
-    """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below."""
+def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bias_grad_accumulate=False):
+    """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below.
+
+    ``bias_grad`` ([K] fp32 or bf16): also produce Σ_m dX[m, :] — the bias gradient of the layer that
+    produced ``relu_mask_of`` — from per-tile column sums in the GEMM epilogue plus a fixed-order reduce.
+    """
     _check_bf16_2d(dy, "dy")
     _check_bf16_2d(w, "w")
     M, N = dy.shape
@@ -98,9 +126,18 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1):
     if out is None:
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     _req(out.shape == (M, K) and out.is_contiguous() and out.dtype == torch.bfloat16, "bad out tensor")
-    return gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
-                    b_kcontig=False, epi=epi, aux=relu_mask_of,
-                    ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile)
+    part = None
+    if bias_grad is not None:
+        _req(bias_grad.numel() == K and bias_grad.is_contiguous(), "bias_grad must be contiguous [K]")
+        T = tiles_m(M, K, tile)
+        part = torch.empty((T, K), dtype=torch.float32, device=dy.device)
+    gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
+             b_kcontig=False, epi=epi, aux=relu_mask_of,
+             ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
+             impl=None if part is None else "pipe")
+    if part is not None:
+        reduce_partials(part, part.shape[0], K, bias_grad, accumulate=bias_grad_accumulate)
+    return out
 
 
 def linear_wgrad(dy, x, out, accumulate=False, tile=-1):
@@ -113,12 +150,12 @@ def linear_wgrad(dy, x, out, accumulate=False, tile=-1):
     _req(out.dtype in (torch.float32, torch.bfloat16), "dW must be fp32 or bf16")
     _req(tuple(out.shape) == (N, K) and out.is_contiguous(), f"dW must be contiguous [{N},{K}]")
     epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
-    _req(not (accumulate and epi == EPI_BF16), "bf16 gradients cannot accumulate in the epilogue")
+    _req(not (accumulate and epi == EPI_BF16 and GEMM_IMPL == "v1"), "v1 GEMM cannot accumulate bf16")
     return gemm_raw(dy, x, out, M=N, N=K, K=M, lda=dy.stride(0), ldb=x.stride(0), ldc=K, a_kcontig=False,
                     b_kcontig=False, epi=epi, accumulate=accumulate, tile=tile)
 
 
-def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-1):
+def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-1, impl=None):
     """General C = A·B for tests: A given as [M,K] (K-contig) or [K,M]; B as [N,K] or [K,N]."""
     _check_bf16_2d(a, "a")
     _check_bf16_2d(b, "b")
@@ -128,4 +165,4 @@ def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-
     epi = EPI_F32 if out_dtype == torch.float32 else EPI_BF16
     out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     return gemm_raw(a, b, out, M=M, N=N, K=K, lda=a.stride(0), ldb=b.stride(0), ldc=N, a_kcontig=a_kcontig,
-                    b_kcontig=b_kcontig, epi=epi, tile=tile)
+                    b_kcontig=b_kcontig, epi=epi, tile=tile, impl=impl)

@@ -46,9 +46,11 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
     loss_rows = torch.empty((M,), dtype=torch.float32, device=dev) if have_t else None
     dl = torch.empty((M, C), dtype=torch.float32, device=dev) if (want_grad and have_t) else None
     lib = native.kernels()
+    scratch = torch.empty((int(lib.ddpx_head_fwd_scratch(M, K)),), dtype=torch.float32, device=dev)
     s = native.stream_handle()
     rc = lib.ddpx_head_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, C, h.stride(0),
-                           1.0 / M, native.ptr(logits), native.ptr(loss_rows), native.ptr(dl), native.ptr(correct), s)
+                           1.0 / M, native.ptr(logits), native.ptr(loss_rows), native.ptr(dl), native.ptr(correct),
+                           scratch.data_ptr(), s)
     native.check(rc, "ddpx_head_fwd")
     loss = None
     if have_t:
@@ -84,20 +86,24 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
                 s = dH.float().sum(0)
                 dbprev.add_(s) if accumulate else dbprev.copy_(s)
         return dH
-    _check(h, w, db, None)
+    _check(h, w, db if db.dtype == torch.float32 else db.float(), None)
     if K % 64:
         raise ValueError("head_backward: K must be a multiple of 64")
     if dH is not None and (dH.shape != h.shape or dH.dtype != torch.bfloat16 or dH.stride(0) != h.stride(0)):
         raise ValueError("head_backward: dH must match h")
-    if tuple(dW.shape) != (C, K) or dW.dtype != torch.float32 or not dW.is_contiguous():
-        raise ValueError("head_backward: dW must be fp32 contiguous [C,K]")
+    gdt = dW.dtype
+    if tuple(dW.shape) != (C, K) or gdt not in (torch.float32, torch.bfloat16) or not dW.is_contiguous():
+        raise ValueError("head_backward: dW must be contiguous [C,K] fp32/bf16")
+    if db.dtype != gdt or (dbprev is not None and dbprev.dtype != gdt):
+        raise ValueError("head_backward: dW, db, dbprev must share one dtype")
     lib = native.kernels()
     go = grad_out if torch.is_tensor(grad_out) else None
     if go is not None:
         go = go.to(torch.float32).contiguous()
+    scratch = torch.empty((int(lib.ddpx_head_bwd_scratch(M, K, C)),), dtype=torch.float32, device=h.device)
     rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
                            native.ptr(dH), dW.data_ptr(), db.data_ptr(), native.ptr(dbprev), int(relu_mask),
-                           int(accumulate), native.stream_handle())
+                           int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), native.stream_handle())
     native.check(rc, "ddpx_head_bwd")
     return dH
 

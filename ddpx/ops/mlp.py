@@ -8,7 +8,7 @@ its DDP bucket slice, then announced to the reducer):
    for l = L-1 .. 0:
       wgrad  : dW_l = dpre_lᵀ h_l                          (announce W_l → bucket may fire)
       dgrad  : dpre_{l-1} = (dpre_l W_l) ⊙ (h_l > 0)        (skipped for l = 0)
-      colsum : db_{l-1} = Σ_m dpre_{l-1}
+      (db_{l-1} = Σ_m dpre_{l-1} from the dgrad epilogue's per-tile column sums)
 The weight gradient of a layer is issued BEFORE its data gradient so the
 bucket holding it starts its all-reduce while the next GEMMs run.
 """
@@ -17,7 +17,6 @@ from __future__ import annotations
 import torch
 
 from . import gemm as G
-from .elementwise import colsum_bf16
 from .head import head_backward, head_forward
 
 
@@ -69,10 +68,11 @@ def _backward(model, hs, dl, grad_out):
         G.linear_wgrad(dpre, hs[l], dWl, accumulate=accw)
         flat.grad_done(w)
         if l > 0:
-            dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l])
             bp = ps[l - 1][1]
             dbl, accl = flat.grad_target(bp)
-            colsum_bf16(dnext, dbl, accumulate=accl)
+            # ReLU backward + bias gradient of layer l-1 fused into the dgrad epilogue
+            dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_grad=dbl,
+                                   bias_grad_accumulate=accl)
             flat.grad_done(bp)
             dpre = dnext
 

@@ -56,6 +56,7 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=None, help="seed model init (reference: unseeded)")
     p.add_argument("--lr", type=float, default=REF_LR, help="peak LR of the one-cycle schedule (reference 0.4)")
     p.add_argument("--graph", action="store_true", help="capture the training step in a HIP graph")
+    p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"], help="gradient buffer / all-reduce dtype")
     p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
     p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
@@ -98,7 +99,7 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
         torch.manual_seed(args.seed)
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels)
-    prepare_model(model, device)
+    prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"))
     spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)

@@ -13,10 +13,13 @@ def _rand_bf16(*shape, dev):
     return (torch.randn(*shape, device=dev) * 0.5).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("impl_tile", [("v1", -1), ("v1", 0), ("v1", 1), ("v1", 2), ("v1", 3)] +
+                         [("pipe", t) for t in range(-1, 8)])
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72)])
-def test_gemm_layouts(gpu, tile, layout, MNK):
+@pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
+                                 (200, 136, 1000)])
+def test_gemm_layouts(gpu, impl_tile, layout, MNK):
+    impl, tile = impl_tile
     from ddpx.ops.gemm import matmul
     M, N, K = MNK
     ak, bk = layout
@@ -27,7 +30,7 @@ def test_gemm_layouts(gpu, tile, layout, MNK):
     B = _rand_bf16(K, N, dev=gpu)  # logical [K,N]
     a_store = A if ak else A.t().contiguous()        # [M,K] or [K,M]
     b_store = B.t().contiguous() if bk else B         # [N,K] or [K,N]
-    C = matmul(a_store, b_store, a_kcontig=ak, b_kcontig=bk, tile=tile)
+    C = matmul(a_store, b_store, a_kcontig=ak, b_kcontig=bk, tile=tile, impl=impl)
     ref = A.float() @ B.float()
     assert _rel(C, ref) < 2e-3
 
@@ -38,10 +41,12 @@ def test_gemm_identity_asymmetric(gpu):
     n = 128
     A = torch.eye(n, device=gpu, dtype=torch.bfloat16)
     B = (torch.arange(n * n, device=gpu, dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
-    for ak in (True, False):
-        for bk in (True, False):
-            C = matmul(A if ak else A.t().contiguous(), B.t().contiguous() if bk else B, a_kcontig=ak, b_kcontig=bk)
-            assert torch.equal(C, B.float()), (ak, bk)
+    for impl in ("v1", "pipe"):
+        for ak in (True, False):
+            for bk in (True, False):
+                C = matmul(A if ak else A.t().contiguous(), B.t().contiguous() if bk else B, a_kcontig=ak,
+                           b_kcontig=bk, impl=impl)
+                assert torch.equal(C, B.float()), (impl, ak, bk)
 
 
 def test_linear_fwd_dgrad_wgrad(gpu):
@@ -64,6 +69,17 @@ def test_linear_fwd_dgrad_wgrad(gpu):
     assert _rel(dw, refdw) < 2e-3
     G.linear_wgrad(dy, x, dw, accumulate=True)
     assert _rel(dw, 2 * refdw) < 2e-3
+    dwb = torch.empty(N, K, device=gpu, dtype=torch.bfloat16)
+    G.linear_wgrad(dy, x, dwb)
+    G.linear_wgrad(dy, x, dwb, accumulate=True)
+    assert _rel(dwb, 2 * refdw) < 1e-2
+    # ReLU backward with the fused bias gradient (per-tile column sums + fixed-order reduce)
+    db = torch.empty(K, device=gpu)
+    dx2 = G.linear_dgrad(dy, w, relu_mask_of=x, bias_grad=db)
+    assert torch.equal(dx2, dx)
+    assert _rel(db, dx2.float().sum(0)) < 1e-5
+    G.linear_dgrad(dy, w, relu_mask_of=x, bias_grad=db, bias_grad_accumulate=True)
+    assert _rel(db, 2 * dx2.float().sum(0)) < 1e-5
 
 
 def test_head_fwd_bwd(gpu):
@@ -96,6 +112,18 @@ def test_head_fwd_bwd(gpu):
     ref_dh = hf.grad * (h.float() > 0)
     assert _rel(dH, ref_dh) < 5e-3
     assert _rel(dbp, dH.float().sum(0)) < 1e-4
+    # bf16 gradient buffers + accumulate
+    dWb = torch.zeros(C, K, device=gpu, dtype=torch.bfloat16)
+    dbb = torch.zeros(C, device=gpu, dtype=torch.bfloat16)
+    dbpb = torch.zeros(K, device=gpu, dtype=torch.bfloat16)
+    head_backward(dl, go, h, w, dWb, dbb, dH=dH, dbprev=dbpb, relu_mask=True, accumulate=True)
+    assert _rel(dWb, wf.grad) < 1e-2 and _rel(dbb, bf.grad) < 1e-2 and _rel(dbpb, dbp) < 1e-2
+    # odd row counts (last batch of an epoch) and logits-only eval
+    for Mo in (336, 106, 7):
+        lo, lg, dlo = head_forward(h[:Mo], w, b, t[:Mo])
+        rl = h[:Mo].float() @ w.float().t() + b
+        assert _rel(lg, rl) < 1e-4
+        assert abs(lo.item() - torch.nn.functional.cross_entropy(rl, t[:Mo]).item()) < 1e-3
 
 
 def test_sgd_flat_matches_torch(gpu):
