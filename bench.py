@@ -43,12 +43,14 @@ def parse():
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--overlap_optimizer", action="store_true")
+    p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
     p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"],
                    help="gradient buffer / all-reduce dtype (bf16 = values of bf16 MFMA wgrads, as autocast)")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
+    p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args()
 
 
@@ -62,7 +64,7 @@ def baseline_value(metric_key: str):
         return None
 
 
-def setup_dist(n):
+def setup_dist(n, impl):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -73,8 +75,9 @@ def setup_dist(n):
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="cpu:gloo,cuda:nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        # ddpx: GPU collectives go through its own RCCL communicator; the c10d group only
+        # bootstraps it (TCPStore) and carries CPU barriers/timing -> gloo.  torch: stock RCCL PG.
+        dist.init_process_group(backend="gloo" if impl == "ddpx" else "nccl", rank=rank, world_size=world)
     return rank, world, local
 
 
@@ -95,10 +98,13 @@ def build_ddpx(args, device, world):
     from ddpx.parallel.comm import RcclComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
+    torch.manual_seed(args.seed)
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16" if args.model != "vgg"
                         else "fp32", device=device)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
-    opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph)
+    # single process: the SGD update is fused into the kernels that produce each gradient
+    opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
+              fused_backward=(world == 1 and not args.no_fused_optimizer))
     net = model
     if world > 1:
         net = DistributedDataParallel(model, comm=RcclComm(device), bucket_cap_mb=args.bucket_cap_mb,
@@ -115,6 +121,7 @@ def build_torch(args, device, world):
     import torch.nn as nn
     from torch.nn.parallel import DistributedDataParallel as TDDP
     from ddpx.optim.schedule import OneCycleLambda, resolve_steps_per_epoch
+    torch.manual_seed(args.seed)
     if args.model == "vgg":
         from ddpx.models import VGG
         model = VGG().to(device)
@@ -134,7 +141,7 @@ def build_torch(args, device, world):
 
 def main():
     args = parse()
-    rank, world, local = setup_dist(args.gpus)
+    rank, world, local = setup_dist(args.gpus, args.impl)
     device = torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
     idx_all = loader._epoch_indices()
@@ -203,8 +210,8 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # gloo (CPU tensor)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.impl == "ddpx" else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     value = world * bs * args.steps / elapsed
@@ -220,7 +227,9 @@ def main():
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
-                   "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)", "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
+                   "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
+                       " fused-into-backward" if (args.impl == "ddpx" and world == 1 and not args.no_fused_optimizer)
+                       else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4)},
     }
     if rank == 0:

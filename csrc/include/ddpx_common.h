@@ -57,4 +57,28 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Fused SGD (torch.optim.SGD semantics, dampening 0, momentum buffer zero-initialised so the
+// first step equals torch's clone(d)).  Used by epilogues that update parameters in place
+// instead of materialising gradients (single-process training: optimizer fused into backward).
+struct SgdArgs {
+  float* p;               // fp32 master
+  float* buf;             // momentum buffer (may be null when mom == 0)
+  unsigned short* shadow; // bf16 compute copy (may be null)
+  const float* lr;        // device scalar
+  float mom, wd;
+};
+
+__device__ __forceinline__ void sgd_apply(const SgdArgs& s, size_t i, float g, float lr) {
+  float p = s.p[i];
+  float d = g + s.wd * p;
+  if (s.mom != 0.f) {
+    const float b = s.mom * s.buf[i] + d;
+    s.buf[i] = b;
+    d = b;
+  }
+  p -= lr * d;
+  s.p[i] = p;
+  if (s.shadow) s.shadow[i] = f2bf(p);
+}
+
 }  // namespace ddpx

@@ -36,6 +36,7 @@ enum Epi : int {
   EPI_BIAS_RELU_BF16 = 3,
   EPI_BIAS_F32 = 4,
   EPI_RELUMASK_BF16 = 5,
+  EPI_SGD = 6,  // no C: the gradient tile updates master/momentum/shadow in place (fused optimizer)
 };
 
 struct Params {
@@ -50,6 +51,7 @@ struct Params {
   int epi, accumulate;
   float alpha;
   unsigned a_bytes, b_bytes;  // buffer extents for the bounds-checked DMA
+  SgdArgs sgd;
 };
 
 constexpr unsigned kOOB = 0x80000000u;
@@ -136,6 +138,8 @@ __device__ __forceinline__ void store_tile(const Params& p, const f32x4 (&acc)[F
     if (n >= p.N) continue;
     float bias = 0.f;
     if constexpr (E == EPI_BIAS_BF16 || E == EPI_BIAS_RELU_BF16 || E == EPI_BIAS_F32) bias = p.bias[n];
+    float lr = 0.f;
+    if constexpr (E == EPI_SGD) lr = *p.sgd.lr;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -166,6 +170,9 @@ __device__ __forceinline__ void store_tile(const Params& p, const f32x4 (&acc)[F
         } else if constexpr (E == EPI_BIAS_F32) {
           stored = v + bias;
           reinterpret_cast<float*>(p.C)[off] = stored;
+        } else if constexpr (E == EPI_SGD) {
+          stored = v * p.alpha;
+          sgd_apply(p.sgd, off, stored, lr);
         } else {  // EPI_RELUMASK_BF16
           const unsigned short hm = p.aux[(size_t)m * p.ldaux + n];
           const bool pos = (hm & 0x8000u) == 0 && (hm & 0x7fffu) != 0;
@@ -261,6 +268,7 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
     case EPI_BIAS_BF16: store_tile<EPI_BIAS_BF16, FM, FN>(p, acc, mb, nb, csum); break;
     case EPI_BIAS_RELU_BF16: store_tile<EPI_BIAS_RELU_BF16, FM, FN>(p, acc, mb, nb, csum); break;
     case EPI_BIAS_F32: store_tile<EPI_BIAS_F32, FM, FN>(p, acc, mb, nb, csum); break;
+    case EPI_SGD: store_tile<EPI_SGD, FM, FN>(p, acc, mb, nb, csum); break;
     default: store_tile<EPI_RELUMASK_BF16, FM, FN>(p, acc, mb, nb, csum); break;
   }
   if (p.colsum) {
@@ -286,12 +294,15 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
 
 // out[n] (=|+=) sum_t partial[t][n]   (fixed order: deterministic)
 __global__ void __launch_bounds__(256) reduce_partials_kernel(const float* __restrict__ part, int T, int N,
-                                                              float* __restrict__ out, int out_bf16, int accumulate) {
+                                                              float* __restrict__ out, int out_bf16, int accumulate,
+                                                              SgdArgs sgd) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
   float s = 0.f;
   for (int t = 0; t < T; ++t) s += part[(size_t)t * N + n];
-  if (out_bf16) {
+  if (sgd.p) {
+    sgd_apply(sgd, n, s, *sgd.lr);
+  } else if (out_bf16) {
     unsigned short* o = reinterpret_cast<unsigned short*>(out);
     if (accumulate) s += bf2f(o[n]);
     o[n] = f2bf(s);
@@ -327,13 +338,15 @@ static void tile_of(int cfg, int* bm, int* bn) {
   *bn = t[cfg & 7][1];
 }
 
-static int pick(int M, int N) {
+// Default tile per operand-layout class, from the MI355X sweep of the MLP shapes
+// (benchmarks/gemm_sweep.py; profiles/): M=512-row products want many small
+// tiles (64x64, 2-3 WG/CU), the K=512 weight-gradient products 64x128/3 stages.
+static int pick(int M, int N, int K, bool ak, bool bk) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (tiles(128, 128) >= 512) return 0;
-  if (tiles(128, 128) >= 256) return 4;
-  if (tiles(64, 128) >= 256) return 1;
-  if (tiles(128, 64) >= 256) return 2;
-  return 3;
+  if (!ak && !bk) return tiles(64, 128) >= 512 ? 5 : 7;      // wgrad-shaped (reduction over batch)
+  if (ak && !bk) return 3;                                   // dgrad-shaped
+  if (tiles(128, 128) >= 1024 && K >= 2048) return 0;        // big forward GEMMs
+  return 7;                                                  // forward, small M
 }
 
 }  // namespace pipe
@@ -342,8 +355,8 @@ static int pick(int M, int N) {
 using namespace ddpx;
 
 // Number of row tiles (M direction) the kernel will use for cfg (for sizing colsum partials).
-DDPX_API int ddpx_gemm_pipe_tiles_m(int M, int N, int tile_cfg) {
-  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N);
+DDPX_API int ddpx_gemm_pipe_tiles_m(int M, int N, int K, int a_kcontig, int b_kcontig, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
   int bm, bn;
   pipe::tile_of(cfg, &bm, &bn);
   return (M + bm - 1) / bm;
@@ -351,7 +364,8 @@ DDPX_API int ddpx_gemm_pipe_tiles_m(int M, int N, int tile_cfg) {
 
 DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* bias, const void* aux, float* colsum,
                             int M, int N, int K, int lda, int ldb, int ldc, int ldaux, int a_kcontig, int b_kcontig,
-                            int epi, int accumulate, float alpha, int tile_cfg, hipStream_t stream) {
+                            int epi, int accumulate, float alpha, int tile_cfg, float* sgd_p, float* sgd_buf,
+                            void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (a_kcontig ? (K % 8 || lda % 8) : (M % 8 || lda % 8)) return -1;
   if (b_kcontig ? (K % 8 || ldb % 8) : (N % 8 || ldb % 8)) return -2;
@@ -360,8 +374,10 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   const size_t b_bytes = (size_t)(b_kcontig ? (size_t)(N - 1) * ldb + K : (size_t)(K - 1) * ldb + N) * 2;
   if (a_bytes >= 0x80000000ull || b_bytes >= 0x80000000ull) return -4;  // 32-bit buffer offsets
   pipe::Params p{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
-                 M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes};
-  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N);
+                 M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes,
+                 SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd}};
+  if (epi == pipe::EPI_SGD && (!sgd_p || !sgd_lr || (sgd_mom != 0.f && !sgd_buf))) return -5;
+  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
   hipError_t e;
   if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true>(p, cfg, stream);
   else if (a_kcontig) e = pipe::dispatch<true, false>(p, cfg, stream);
@@ -371,9 +387,10 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
 }
 
 DDPX_API int ddpx_reduce_partials(const float* part, int T, int N, void* out, int out_bf16, int accumulate,
-                                  hipStream_t s) {
+                                  float* sgd_p, float* sgd_buf, void* sgd_shadow, const float* sgd_lr, float sgd_mom,
+                                  float sgd_wd, hipStream_t s) {
   if (N <= 0) return 0;
   hipLaunchKernelGGL(pipe::reduce_partials_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, T, N, (float*)out,
-                     out_bf16, accumulate);
+                     out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
   return (int)hipGetLastError();
 }

@@ -139,8 +139,9 @@ __global__ void __launch_bounds__(256)
 head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
                         const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K,
                         int ldh, int rows_per_split, unsigned short* __restrict__ dH, float* __restrict__ pdw,
-                        float* __restrict__ pdb, int relu_mask) {
+                        float* __restrict__ pdb, float* __restrict__ pdbh, int relu_mask) {
   __shared__ float red[4][64][C + 1];
+  __shared__ float redh[16][C];
   const float go = go_ptr ? *go_ptr : 1.f;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int cg = tid & 7, r0 = tid >> 3;
@@ -214,7 +215,20 @@ head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restri
       for (int c = 0; c < C; ++c) red[w][lane * 8 + j][c] = dw[c][j];
     }
   }
+  if (blockIdx.x == 0) {
+    // head bias partial for this row split: pdbh[rs][c] = go * sum_m dlogits[m][c]
+    const int c = tid & 15, rg = tid >> 4;
+    float sh = 0.f;
+    if (c < C)
+      for (int m = mbeg + rg; m < mend; m += 16) sh += dlogits[(size_t)m * C + c];
+    if (c < C) redh[rg][c] = sh * go;
+  }
   __syncthreads();
+  if (blockIdx.x == 0 && tid < C) {
+    float sh = 0.f;
+    for (int rg = 0; rg < 16; ++rg) sh += redh[rg][tid];
+    pdbh[(size_t)rs * C + tid] = sh;
+  }
   for (int i = tid; i < 64 * (C + 1); i += 256) {
     const int col = i % 64, c = i / 64;
     const float s = (red[0][col][c] + red[1][col][c]) + (red[2][col][c] + red[3][col][c]);
@@ -228,13 +242,15 @@ head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restri
 // (fp32 or bf16, write or accumulate) + the head bias gradient (workgroup 0).
 template <int C>
 __global__ void __launch_bounds__(256)
-head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict__ pdb, int RS, int K,
-                         const float* __restrict__ dlogits, const float* __restrict__ go_ptr, int M,
-                         void* __restrict__ dW, void* __restrict__ db, void* __restrict__ dbprev, int out_bf16,
-                         int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over (C+1)*K
-  auto put = [&](void* base, size_t idx, float v) {
-    if (out_bf16) {
+head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict__ pdb,
+                         const float* __restrict__ pdbh, int RS, int K, void* __restrict__ dW,
+                         void* __restrict__ db, void* __restrict__ dbprev, int out_bf16, int accumulate,
+                         SgdArgs sW, SgdArgs sB, SgdArgs sP) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over (C+1)*K + C
+  auto put = [&](const SgdArgs* sg, void* base, size_t idx, float v) {
+    if (sg->p) {  // fused optimizer: update the parameter instead of storing its gradient
+      sgd_apply(*sg, idx, v, *sg->lr);
+    } else if (out_bf16) {
       unsigned short* o = reinterpret_cast<unsigned short*>(base) + idx;
       *o = f2bf(accumulate ? v + bf2f(*o) : v);
     } else {
@@ -245,22 +261,19 @@ head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict_
   if (i < C * K) {
     float s = 0.f;
     for (int r = 0; r < RS; ++r) s += pdw[(size_t)r * C * K + i];
-    put(dW, i, s);
-  } else if (i < (C + 1) * K && dbprev) {
+    put(&sW, dW, i, s);
+  } else if (i < (C + 1) * K) {
+    if (!dbprev && !sP.p) return;
     const int kk = i - C * K;
     float s = 0.f;
     for (int r = 0; r < RS; ++r) s += pdb[(size_t)r * K + kk];
-    put(dbprev, kk, s);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < 64 && db) {
-    const float go = go_ptr ? *go_ptr : 1.f;
-    const int lane = threadIdx.x;
-    for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-      for (int m = lane; m < M; m += 64) s += dlogits[(size_t)m * C + c];
-      s = wave_sum(s) * go;
-      if (lane == 0) put(db, c, s);
-    }
+    put(&sP, dbprev, kk, s);
+  } else if (i < (C + 1) * K + C) {
+    if (!db && !sB.p) return;
+    const int c = i - (C + 1) * K;
+    float s = 0.f;
+    for (int r = 0; r < RS; ++r) s += pdbh[(size_t)r * C + c];
+    put(&sB, db, c, s);
   }
 }
 
@@ -305,7 +318,8 @@ using namespace ddpx;
 // Scratch sizes (floats) the host must provide for the head kernels.
 DDPX_API int64_t ddpx_head_fwd_scratch(int M, int K) { return (int64_t)head_ksplit(M, K) * M * kHeadC; }
 DDPX_API int64_t ddpx_head_bwd_scratch(int M, int K, int C) {
-  return (int64_t)head_row_splits(M, K) * (C + 1) * K;
+  const int64_t rs = head_row_splits(M, K);
+  return rs * (C + 1) * K + rs * C;
 }
 
 DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K, int C,
@@ -331,7 +345,9 @@ DDPX_API int ddpx_mean(const float* x, int n, float* out, hipStream_t s) {
 
 DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K, int C,
                            int ldh, void* dH, void* dW, void* db, void* dbprev, int relu_mask, int out_bf16,
-                           int accumulate, float* scratch, hipStream_t s) {
+                           int accumulate, float* scratch, float* sw_p, float* sw_buf, void* sw_sh, float* sb_p,
+                           float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh, const float* lr,
+                           float mom, float wd, hipStream_t s) {
   if (M <= 0) return 0;
   if (C != 10) return -1;
   if (K % 64 || ldh % 8) return -2;
@@ -339,11 +355,15 @@ DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H,
   const int rps = (M + rs - 1) / rs;
   float* pdw = scratch;
   float* pdb = scratch + (size_t)rs * C * K;
+  float* pdbh = pdb + (size_t)rs * K;
   hipLaunchKernelGGL(head_bwd_partial_kernel<10>, dim3(K / 64, rs), dim3(256), 0, s, dlogits, go,
                      (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, rps, (unsigned short*)dH, pdw, pdb,
-                     relu_mask);
-  hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + 255) / 256), dim3(256), 0, s, pdw, pdb, rs, K,
-                     dlogits, go, M, dW, db, dbprev, out_bf16, accumulate);
+                     pdbh, relu_mask);
+  hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + C + 255) / 256), dim3(256), 0, s, pdw, pdb,
+                     pdbh, rs, K, dW, db, dbprev, out_bf16, accumulate,
+                     SgdArgs{sw_p, sw_buf, (unsigned short*)sw_sh, lr, mom, wd},
+                     SgdArgs{sb_p, sb_buf, (unsigned short*)sb_sh, lr, mom, wd},
+                     SgdArgs{sp_p, sp_buf, (unsigned short*)sp_sh, lr, mom, wd});
   return (int)hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ EPI_BIAS_BF16 = 2
 EPI_BIAS_RELU_BF16 = 3
 EPI_BIAS_F32 = 4
 EPI_RELUMASK_BF16 = 5
+EPI_SGD = 6  # fused optimizer: the product is a gradient applied to (master, momentum, shadow) in place
 
 _OUT_DTYPE = {
     EPI_F32: torch.float32,
@@ -56,32 +57,33 @@ def _check_bf16_2d(t, name):
 
 
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
-             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None):
+             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None):
     lib = native.kernels()
     impl = impl or GEMM_IMPL
     s = native.stream_handle(stream)
     if impl == "v1":
-        if colsum is not None:
-            raise ValueError("v1 GEMM has no fused column sum")
+        if colsum is not None or sgd is not None:
+            raise ValueError("v1 GEMM has no fused column sum / optimizer epilogue")
         rc = lib.ddpx_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux), M, N, K,
                                 lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate),
                                 float(alpha), tile, s)
     else:
         rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
                                 native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
-                                int(accumulate), float(alpha), tile, s)
+                                int(accumulate), float(alpha), tile, *native.sgd_args(sgd), s)
     native.check(rc, f"ddpx_gemm_{impl}(M={M},N={N},K={K},epi={epi})")
     return c
 
 
-def tiles_m(M, N, tile=-1):
-    return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, tile)
+def tiles_m(M, N, K, a_kcontig, b_kcontig, tile=-1):
+    return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, K, int(a_kcontig), int(b_kcontig), tile)
 
 
-def reduce_partials(part, T, N, out, accumulate=False):
+def reduce_partials(part, T, N, out, accumulate=False, sgd=None):
     lib = native.kernels()
-    native.check(lib.ddpx_reduce_partials(part.data_ptr(), T, N, out.data_ptr(), int(out.dtype == torch.bfloat16),
-                                          int(accumulate), native.stream_handle()), "ddpx_reduce_partials")
+    native.check(lib.ddpx_reduce_partials(part.data_ptr(), T, N, native.ptr(out),
+                                          int(out is not None and out.dtype == torch.bfloat16), int(accumulate),
+                                          *native.sgd_args(sgd), native.stream_handle()), "ddpx_reduce_partials")
     return out
 
 
@@ -107,7 +109,8 @@ def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, 
                     b_kcontig=True, epi=epi, bias=bias, tile=tile)
 
 
-def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bias_grad_accumulate=False):
+def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bias_grad_accumulate=False,
+                 bias_sgd=None):
     """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below.
 
     ``bias_grad`` ([K] fp32 or bf16): also produce Σ_m dX[m, :] — the bias gradient of the layer that
@@ -127,21 +130,35 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
         out = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
     _req(out.shape == (M, K) and out.is_contiguous() and out.dtype == torch.bfloat16, "bad out tensor")
     part = None
-    if bias_grad is not None:
-        _req(bias_grad.numel() == K and bias_grad.is_contiguous(), "bias_grad must be contiguous [K]")
-        T = tiles_m(M, K, tile)
+    if bias_grad is not None or bias_sgd is not None:
+        _req(bias_grad is None or (bias_grad.numel() == K and bias_grad.is_contiguous()),
+             "bias_grad must be contiguous [K]")
+        _req(bias_sgd is None or bias_sgd[0].numel() == K, "bias_sgd target must have K elements")
+        T = tiles_m(M, K, N, True, False, tile)
         part = torch.empty((T, K), dtype=torch.float32, device=dy.device)
     gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
              b_kcontig=False, epi=epi, aux=relu_mask_of,
              ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
              impl=None if part is None else "pipe")
     if part is not None:
-        reduce_partials(part, part.shape[0], K, bias_grad, accumulate=bias_grad_accumulate)
+        reduce_partials(part, part.shape[0], K, bias_grad, accumulate=bias_grad_accumulate, sgd=bias_sgd)
     return out
 
 
-def linear_wgrad(dy, x, out, accumulate=False, tile=-1):
-    """dW[N,K] (=|+=) dYᵀ X in fp32 (written straight into the gradient bucket)."""
+def linear_wgrad(dy, x, out, accumulate=False, tile=-1, sgd=None):
+    """dW[N,K] (=|+=) dYᵀ X in fp32/bf16 (written straight into the gradient bucket).
+
+    ``sgd=(master, momentum, shadow, lr, mom, wd)``: fused optimizer — the [N,K] product is applied as
+    the gradient of that parameter (SGD in the epilogue); ``out`` is ignored and may be None.
+    """
+    if sgd is not None:
+        _check_bf16_2d(dy, "dy")
+        _check_bf16_2d(x, "x")
+        M, N = dy.shape
+        _, K = x.shape
+        _req(sgd[0].numel() == N * K, "sgd target size mismatch")
+        return gemm_raw(dy, x, sgd[0], M=N, N=K, K=M, lda=dy.stride(0), ldb=x.stride(0), ldc=K, a_kcontig=False,
+                        b_kcontig=False, epi=EPI_SGD, tile=tile, impl="pipe", sgd=sgd)
     _check_bf16_2d(dy, "dy")
     _check_bf16_2d(x, "x")
     M, N = dy.shape

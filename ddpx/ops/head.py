@@ -18,7 +18,7 @@ def _check(h, w, b, targets):
         raise ValueError("head: native head is specialised for 10 classes")
     if h.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
         raise ValueError("head: h and w must be bf16 on GPU")
-    if b.dtype != torch.float32 or b.numel() != w.shape[0]:
+    if b is not None and (b.dtype != torch.float32 or b.numel() != w.shape[0]):
         raise ValueError("head: bias must be fp32 [C]")
     if h.stride(1) != 1 or h.stride(0) % 8 or not w.is_contiguous():
         raise ValueError("head: h must be row-contiguous with ld % 8 == 0, w contiguous")
@@ -59,11 +59,14 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
     return loss, logits, dl
 
 
-def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_mask=True, accumulate=False):
+def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_mask=True, accumulate=False,
+                  sgd_w=None, sgd_b=None, sgd_prev=None):
     """Backward of the fused head.
 
     dW [C,K] fp32, db [C] fp32 (=|+=); dH [M,K] bf16 = (grad · W) ⊙ (h>0 if relu_mask);
     dbprev [K] fp32 = Σ_m dH (bias gradient of the layer that produced h).
+    sgd_w / sgd_b / sgd_prev: fused optimizer targets (master, momentum, shadow, lr, mom, wd) that
+    replace dW / db / dbprev (the gradients are applied instead of stored).
     """
     M, K = h.shape
     C = w.shape[0]
@@ -86,24 +89,34 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
                 s = dH.float().sum(0)
                 dbprev.add_(s) if accumulate else dbprev.copy_(s)
         return dH
-    _check(h, w, db if db.dtype == torch.float32 else db.float(), None)
+    _check(h, w, None, None)
     if K % 64:
         raise ValueError("head_backward: K must be a multiple of 64")
     if dH is not None and (dH.shape != h.shape or dH.dtype != torch.bfloat16 or dH.stride(0) != h.stride(0)):
         raise ValueError("head_backward: dH must match h")
-    gdt = dW.dtype
-    if tuple(dW.shape) != (C, K) or gdt not in (torch.float32, torch.bfloat16) or not dW.is_contiguous():
-        raise ValueError("head_backward: dW must be contiguous [C,K] fp32/bf16")
-    if db.dtype != gdt or (dbprev is not None and dbprev.dtype != gdt):
-        raise ValueError("head_backward: dW, db, dbprev must share one dtype")
+    fused = sgd_w is not None
+    if fused:
+        if sgd_b is None or (dbprev is not None) or sgd_w[0].numel() != C * K or sgd_b[0].numel() != C:
+            raise ValueError("head_backward: fused optimizer needs sgd_w, sgd_b (and sgd_prev instead of dbprev)")
+        gdt = torch.float32
+    else:
+        gdt = dW.dtype
+        if tuple(dW.shape) != (C, K) or gdt not in (torch.float32, torch.bfloat16) or not dW.is_contiguous():
+            raise ValueError("head_backward: dW must be contiguous [C,K] fp32/bf16")
+        if db.dtype != gdt or (dbprev is not None and dbprev.dtype != gdt):
+            raise ValueError("head_backward: dW, db, dbprev must share one dtype")
     lib = native.kernels()
     go = grad_out if torch.is_tensor(grad_out) else None
     if go is not None:
         go = go.to(torch.float32).contiguous()
     scratch = torch.empty((int(lib.ddpx_head_bwd_scratch(M, K, C)),), dtype=torch.float32, device=h.device)
+    sw, sb, sp = (native.sgd_args(x) for x in (sgd_w, sgd_b, sgd_prev))
+    lr_ptr = sw[3] if fused else None
+    mom, wd = (sw[4], sw[5]) if fused else (0.0, 0.0)
     rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
-                           native.ptr(dH), dW.data_ptr(), db.data_ptr(), native.ptr(dbprev), int(relu_mask),
-                           int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), native.stream_handle())
+                           native.ptr(dH), native.ptr(dW), native.ptr(db), native.ptr(dbprev), int(relu_mask),
+                           int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3], *sp[:3],
+                           lr_ptr, mom, wd, native.stream_handle())
     native.check(rc, "ddpx_head_bwd")
     return dH
 

@@ -50,13 +50,32 @@ def _backward(model, hs, dl, grad_out):
     ps = _params(model)
     L = len(ps) - 1  # number of hidden layers
     wl, bl = ps[-1]
+    bprev = ps[L - 1][1]
+    fused = flat.fused_spec(wl) is not None
+    dpre = torch.empty_like(hs[L])
+    if fused:
+        # optimizer fused into backward: each kernel that produces a gradient applies the SGD
+        # update in its epilogue.  W_L is read (for dH) before the finalize kernel updates it.
+        head_backward(dl, grad_out, hs[L], flat.shadow_of(wl), None, None, dH=dpre, relu_mask=True,
+                      sgd_w=flat.fused_spec(wl), sgd_b=flat.fused_spec(bl), sgd_prev=flat.fused_spec(bprev))
+        for p in (wl, bl, bprev):
+            flat.mark_updated(p)
+        for l in range(L - 1, -1, -1):
+            w, _ = ps[l]
+            dnext = None
+            if l > 0:  # data gradient first: it must read W_l before the fused update rewrites it
+                bp = ps[l - 1][1]
+                dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
+                flat.mark_updated(bp)
+            G.linear_wgrad(dpre, hs[l], None, sgd=flat.fused_spec(w))
+            flat.mark_updated(w)
+            dpre = dnext
+        return
     dW, acc = flat.grad_target(wl)
     db, accb = flat.grad_target(bl)
-    bprev = ps[L - 1][1]
     dbp, accp = flat.grad_target(bprev)
     if not (acc == accb == accp):
         raise NotImplementedError("mixed gradient-accumulation state inside the MLP head")
-    dpre = torch.empty_like(hs[L])
     head_backward(dl, grad_out, hs[L], flat.shadow_of(wl), dW, db, dH=dpre, dbprev=dbp, relu_mask=True,
                   accumulate=acc)
     flat.grad_done(wl)

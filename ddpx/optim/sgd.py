@@ -25,7 +25,8 @@ from ..runtime.flat_params import FlatParams, flat_of
 
 class SGD(Optimizer):
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
-                 weight_decay: float = 0.0, nesterov: bool = False, capturable: bool = False):
+                 weight_decay: float = 0.0, nesterov: bool = False, capturable: bool = False,
+                 fused_backward: bool = False):
         if dampening != 0.0:
             raise ValueError("ddpx.optim.SGD implements dampening=0 (the reference's setting)")
         if nesterov and momentum <= 0:
@@ -44,7 +45,13 @@ class SGD(Optimizer):
         self.flat: FlatParams = flat
         self.momentum_buffer = torch.zeros_like(flat.master) if momentum else None
         self.capturable = capturable
-        self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if capturable else None
+        # fused_backward: single-process training applies each parameter's update inside the kernel
+        # that produces its gradient (no gradient round trip through HBM, no separate SGD pass).
+        self.fused_backward = bool(fused_backward and flat.master.is_cuda and not nesterov)
+        need_dev_lr = capturable or self.fused_backward
+        self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if need_dev_lr else None
+        if self.fused_backward:
+            flat.fused_opt = self
         self.bucket_source = None  # set by DDP when the optimizer overlaps the all-reduce
         self.step_count = 0
 
@@ -52,13 +59,21 @@ class SGD(Optimizer):
     def zero_grad(self, set_to_none: bool = True):  # noqa: D401 - torch signature
         self.flat.zero_grad()
 
+    def fused_active(self) -> bool:
+        return self.fused_backward
+
+    def disable_fused(self):
+        self.fused_backward = False
+        if self.flat.fused_opt is self:
+            self.flat.fused_opt = None
+
     def sync_lr(self):
         """Copy the host learning rate into the device scalar (outside graph capture)."""
         if self.lr_dev is not None:
             self.lr_dev.fill_(float(self.param_groups[0]["lr"]))
 
     def _lr_arg(self):
-        return self.lr_dev if self.capturable else float(self.param_groups[0]["lr"])
+        return self.lr_dev if self.lr_dev is not None else float(self.param_groups[0]["lr"])
 
     def _update(self, start, end, g):
         f = self.flat
@@ -77,7 +92,20 @@ class SGD(Optimizer):
         if not (self.flat.master.is_cuda and torch.cuda.is_current_stream_capturing()):
             self.flat.fix_unwritten()
         src = self.bucket_source
-        if src is not None and src.overlap_active():
+        if any(self.flat.updated):
+            # fused-backward parameters are already stepped; update the rest range by range
+            f = self.flat
+            i, n = 0, len(f.params)
+            while i < n:
+                if f.updated[i]:
+                    i += 1
+                    continue
+                j = i
+                while j + 1 < n and not f.updated[j + 1]:
+                    j += 1
+                self._update(*f.span(i, j), g)
+                i = j + 1
+        elif src is not None and src.overlap_active():
             for (start, end) in src.bucket_ranges_in_completion_order():
                 src.wait_range(start, end)
                 self._update(start, end, g)

@@ -180,12 +180,16 @@ class _NativeReducer:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, comm: Comm | None = None,
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
-                 broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True):
+                 broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
+                 reduce_single: bool = False):
         super().__init__()
         self.module = module
         dev = next(module.parameters()).device
         self.device = dev
         self.flat: FlatParams = flat_of(module) or FlatParams(module)
+        if self.flat.fused_opt is not None:
+            # gradients must be all-reduced before the update: no optimizer-in-backward fusion
+            self.flat.fused_opt.disable_fused()
         if comm is None:
             from .comm import default_comm
             comm = default_comm(dev)
@@ -226,7 +230,7 @@ class DistributedDataParallel(nn.Module):
             ranges.append(self.flat.span(idxs[0], idxs[-1]))
             expected.append(len(idxs))
         self.bucket_ranges = ranges
-        if self.world_size > 1:
+        if self.world_size > 1 or reduce_single:  # reduce_single: exercise the reducer at ws=1 (tests)
             self.reducer = _NativeReducer(comm, ranges) if isinstance(comm, RcclComm) else _PyReducer(comm, ranges)
             self.reducer.setup(self.flat.grad, expected)
         else:

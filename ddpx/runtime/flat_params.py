@@ -78,6 +78,8 @@ class FlatParams:
         self.refresh_shadow()
         self.native = {id(p) for p in native_params}
         self.written = [False] * len(self.params)
+        self.updated = [False] * len(self.params)  # parameter already stepped by a fused-optimizer epilogue
+        self.fused_opt = None  # set by ddpx.optim.SGD(fused_backward=True)
         self.sink = None
         self._warned_unused = False
         self._hooks = []
@@ -111,6 +113,25 @@ class FlatParams:
         i = self.index[id(p)]
         return p.main_grad, self.written[i]
 
+    def fused_spec(self, p):
+        """(master, momentum, shadow, lr, mom, wd) if p's update should be fused into its backward kernel."""
+        o = self.fused_opt
+        if o is None or not o.fused_active():
+            return None
+        i = self.index[id(p)]
+        if self.written[i] or self.updated[i]:
+            return None  # gradient accumulation across backwards: fall back to materialised grads
+        sl = self.slice(i)
+        g = o.param_groups[0]
+        buf = o.momentum_buffer[sl] if o.momentum_buffer is not None else None
+        sh = self.shadow[sl] if self.shadow is not None else None
+        return (self.master[sl], buf, sh, o.lr_dev, g["momentum"], g["weight_decay"])
+
+    def mark_updated(self, p):
+        i = self.index[id(p)]
+        self.updated[i] = True
+        self.written[i] = True
+
     def grad_done(self, p):
         i = self.index[id(p)]
         self.written[i] = True
@@ -133,12 +154,13 @@ class FlatParams:
 
     def zero_grad(self):
         self.written = [False] * len(self.params)
+        self.updated = [False] * len(self.params)
         for p in self.params:
             p.grad = None
 
     def fix_unwritten(self):
         """Zero gradients nobody produced this iteration (stale values would otherwise be applied)."""
-        missing = [i for i, w in enumerate(self.written) if not w]
+        missing = [i for i, w in enumerate(self.written) if not w and not self.updated[i]]
         if missing:
             if not self._warned_unused:
                 names = [self.names.get(id(self.params[i]), str(i)) for i in missing]

@@ -50,13 +50,14 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_cast_f32_bf16", I, P, P, I64, P)
     _sig(lib, "ddpx_colsum_bf16", I, P, P, I, I, I, F, I, P)
     _sig(lib, "ddpx_scale_f32", I, P, I64, F, P)
-    _sig(lib, "ddpx_gemm_pipe", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P)
-    _sig(lib, "ddpx_gemm_pipe_tiles_m", I, I, I, I)
-    _sig(lib, "ddpx_reduce_partials", I, P, I, I, P, I, I, P)
+    _sig(lib, "ddpx_gemm_pipe", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_gemm_pipe_tiles_m", I, I, I, I, I, I, I)
+    _sig(lib, "ddpx_reduce_partials", I, P, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_head_fwd_scratch", I64, I, I)
     _sig(lib, "ddpx_head_bwd_scratch", I64, I, I, I)
     _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P)
-    _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, P, P)
+    _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, F, F,
+         P)
     _sig(lib, "ddpx_mean", I, P, I, P, P)
     _sig(lib, "ddpx_accuracy", I, P, P, I, I, P, P)
     _sig(lib, "ddpx_augment", I, P, P, P, I, I, I, I, I, c_uint64, I, I, P, P, P)
@@ -170,6 +171,14 @@ def stream_handle(stream: "torch.cuda.Stream | None" = None) -> int:
 
 def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
+
+
+def sgd_args(sgd):
+    """(p, buf, shadow, lr, mom, wd) tuple of tensors/floats -> C argument tuple (nulls when None)."""
+    if sgd is None:
+        return (None, None, None, None, 0.0, 0.0)
+    p, buf, sh, lr, mom, wd = sgd
+    return (p.data_ptr(), ptr(buf), ptr(sh), lr.data_ptr(), float(mom), float(wd))
 
 
 def check(rc: int, what: str):

@@ -58,6 +58,8 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--graph", action="store_true", help="capture the training step in a HIP graph")
     p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"], help="gradient buffer / all-reduce dtype")
     p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
+    p.add_argument("--no_fused_optimizer", action="store_true",
+                   help="single GPU: run SGD as its own pass instead of inside the backward kernels")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
     p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
     p.add_argument("--resume", action="store_true", help=f"resume from {FULL_CKPT_PATH}")
@@ -101,7 +103,8 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
                         kernels=args.kernels)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
-                    capturable=bool(args.graph and device.type == "cuda"))
+                    capturable=bool(args.graph and device.type == "cuda"),
+                    fused_backward=bool(not distributed and device.type == "cuda" and not args.no_fused_optimizer))
     spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)
     scheduler = one_cycle(optimizer, spe)
     return train_set, model, optimizer, test_set, scheduler
@@ -173,13 +176,17 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
 
 
 # ------------------------------------------------------------------ multi
-def ddp_setup(rank: int, world_size: int, device_type: str):
-    """Rendezvous (reference: multigpu.py:24-33).  Env MASTER_ADDR/PORT win over the defaults."""
+def ddp_setup(rank: int, world_size: int, device_type: str, comm: str = "rccl"):
+    """Rendezvous (reference: multigpu.py:24-33).  Env MASTER_ADDR/PORT win over the defaults.
+
+    With the native RCCL communicator the c10d group only bootstraps it (TCPStore) and carries
+    CPU-side metadata, so it is gloo; ``--comm torch`` uses stock ProcessGroupNCCL (RCCL) instead.
+    """
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "12355")
     if device_type == "cuda":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)))
-        backend = "cpu:gloo,cuda:nccl"
+        backend = "gloo" if comm == "rccl" else "cpu:gloo,cuda:nccl"
     else:
         backend = "gloo"
     dist.init_process_group(backend=backend, rank=rank, world_size=world_size)
@@ -188,7 +195,7 @@ def ddp_setup(rank: int, world_size: int, device_type: str):
 def main_multi(rank: int, world_size: int, args):
     """Per-process entry (mp.spawn target or torchrun worker)."""
     device_type = resolve_device(args).type
-    ddp_setup(rank, world_size, device_type)
+    ddp_setup(rank, world_size, device_type, args.comm)
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
     try:
         run(args, rank=rank, world_size=world_size, local_rank=local_rank, distributed=True)

@@ -172,29 +172,130 @@ def test_augment_matches_cpu(gpu, layout):
         assert torch.equal(xc, xg.cpu())
 
 
-def test_mlp_native_matches_torch(gpu):
-    """Native fused MLP (loss + all grads) vs the same MLP in torch fp32 with bf16-rounded weights."""
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _mlp_reference(x, t, W, b):
+    """fp32 math with bf16 rounding exactly where the native path stores bf16 (activations, dpre)."""
+    M = x.shape[0]
+    h1 = _bf(torch.relu(x.float() @ W[0].t() + b[0]))
+    h2 = _bf(torch.relu(h1 @ W[1].t() + b[1]))
+    z = h2 @ W[2].t() + b[2]
+    loss = torch.nn.functional.cross_entropy(z, t)
+    dl = (torch.softmax(z, 1) - torch.nn.functional.one_hot(t, 10).float()) / M
+    g = {}
+    g["fc2.weight"], g["fc2.bias"] = dl.t() @ h2, dl.sum(0)
+    d2 = _bf((dl @ W[2]) * (h2 > 0))
+    g["fc1.weight"], g["fc1.bias"] = d2.t() @ h1, d2.sum(0)
+    d1 = _bf((d2 @ W[1]) * (h1 > 0))
+    g["fc0.weight"], g["fc0.bias"] = d1.t() @ x.float(), d1.sum(0)
+    return loss, g
+
+
+@pytest.mark.parametrize("grad_dtype", [torch.float32, torch.bfloat16])
+def test_mlp_native_matches_reference(gpu, grad_dtype):
+    """Native fused MLP (loss + every gradient) vs an fp32 reference with the same bf16 storage points."""
     import ddpx
     from ddpx.models import MLP
     torch.manual_seed(4)
     m = MLP(hidden=512, layers=3)
-    ref = MLP(hidden=512, layers=3, compute_dtype=torch.float32)
-    ref.load_state_dict(m.state_dict())
-    ddpx.prepare_model(m, gpu)
-    ref.to(gpu)
-    with torch.no_grad():
-        for p in ref.parameters():
-            if p.dim() == 2:
-                p.copy_(p.to(torch.bfloat16).float())
+    ddpx.prepare_model(m, gpu, grad_dtype=grad_dtype)
+    W = [_bf(getattr(m, f"fc{i}").weight.detach()) for i in range(3)]
+    b = [getattr(m, f"fc{i}").bias.detach().clone() for i in range(3)]
     x = torch.rand(256, 3072, device=gpu).to(torch.bfloat16)
     t = torch.randint(0, 10, (256,), device=gpu)
     loss, _ = m.forward_loss(x, t)
     loss.backward()
-    rl = torch.nn.functional.cross_entropy(ref(x.float()), t)
-    rl.backward()
-    assert abs(loss.item() - rl.item()) < 2e-2
-    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
-        assert _rel(p.main_grad, q.grad) < 3e-2, n
+    rl, rg = _mlp_reference(x, t, W, b)
+    assert abs(loss.item() - rl.item()) < 1e-3
+    tol = 2e-3 if grad_dtype == torch.float32 else 1e-2
+    for n, p in m.named_parameters():
+        assert _rel(p.main_grad, rg[n]) < tol, n
+
+
+def test_mlp_graph_matches_eager_bf16_grads(gpu):
+    """Captured step == eager step, bit for bit, with bf16 gradient buffers."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.optim.sgd import SGD
+    from ddpx.runtime.graphs import CapturedStep
+    torch.manual_seed(5)
+    a, b = MLP(hidden=512), MLP(hidden=512)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        ddpx.prepare_model(m, gpu, grad_dtype=torch.bfloat16)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    xs = [torch.rand(256, 3072, device=gpu).to(torch.bfloat16) for _ in range(5)]
+    ts = [torch.randint(0, 10, (256,), device=gpu) for _ in range(5)]
+
+    def body(x, y):
+        oa.zero_grad()
+        loss, _ = a.forward_loss(x, y)
+        loss.backward()
+        oa.step()
+        return loss
+
+    oa.sync_lr()
+    body(xs[0], ts[0])
+    g = CapturedStep(body, xs[1], ts[1])
+    la = [g(xs[i], ts[i]).item() for i in range(1, 5)]
+    lb = []
+    for i in range(5):
+        ob.zero_grad()
+        loss, _ = b.forward_loss(xs[i], ts[i])
+        loss.backward()
+        ob.step()
+        lb.append(loss.item())
+    assert la == lb[1:]
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_backward_optimizer_bitwise(gpu, graph):
+    """SGD applied inside the backward epilogues == materialised fp32 grads + flat SGD, bit for bit."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.optim.sgd import SGD
+    from ddpx.runtime.graphs import CapturedStep
+    torch.manual_seed(6)
+    a, b = MLP(hidden=512), MLP(hidden=512)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        ddpx.prepare_model(m, gpu)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True, fused_backward=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    assert oa.fused_active()
+    xs = [torch.rand(256, 3072, device=gpu).to(torch.bfloat16) for _ in range(4)]
+    ts = [torch.randint(0, 10, (256,), device=gpu) for _ in range(4)]
+
+    def body(x, y):
+        oa.zero_grad()
+        loss, _ = a.forward_loss(x, y)
+        loss.backward()
+        oa.step()
+        return loss
+
+    oa.sync_lr()
+    la = [body(xs[0], ts[0]).item()]
+    if graph:
+        g = CapturedStep(body, xs[1], ts[1])
+        la += [g(xs[i], ts[i]).item() for i in range(1, 4)]
+    else:
+        la += [body(xs[i], ts[i]).item() for i in range(1, 4)]
+    lb = []
+    for i in range(4):
+        ob.zero_grad()
+        loss, _ = b.forward_loss(xs[i], ts[i])
+        loss.backward()
+        ob.step()
+        lb.append(loss.item())
+    assert la == lb
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+    assert torch.equal(oa.momentum_buffer, ob.momentum_buffer)
 
 
 def test_native_libs_loaded(gpu):
