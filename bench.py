@@ -81,13 +81,16 @@ def setup_dist(n, impl):
     return rank, world, local
 
 
-def make_data(args, device, rank, world):
+def make_data(args, device, rank, world, layout=None):
     from ddpx.data.datasets import synthetic_cifar
     from ddpx.data.loader import DeviceLoader
     from ddpx.data.sampler import DistributedIndexSampler
     ds = synthetic_cifar(args.train_size, seed=0)
     sampler = DistributedIndexSampler(len(ds), world, rank, shuffle=True, seed=0)
-    layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
+    if layout is None:
+        layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
+        if args.impl == "ddpx" and args.model == "vgg":
+            layout = "nhwc8_bf16"
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
 
 
@@ -99,8 +102,7 @@ def build_ddpx(args, device, world):
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
-    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16" if args.model != "vgg"
-                        else "fp32", device=device)
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16", device=device)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update is fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
@@ -223,7 +225,7 @@ def main():
     rec = {
         "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if args.model != "vgg" else "fp32",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if (args.model != "vgg" or args.impl == "ddpx") else "fp32",
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),

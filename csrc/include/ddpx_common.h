@@ -70,13 +70,12 @@ struct SgdArgs {
 
 __device__ __forceinline__ void sgd_apply(const SgdArgs& s, size_t i, float g, float lr) {
   float p = s.p[i];
-  float d = g + s.wd * p;
+  float d = fmaf(s.wd, p, g);
   if (s.mom != 0.f) {
-    const float b = s.mom * s.buf[i] + d;
-    s.buf[i] = b;
-    d = b;
+    d = fmaf(s.mom, s.buf[i], d);
+    s.buf[i] = d;
   }
-  p -= lr * d;
+  p = fmaf(-lr, d, p);
   s.p[i] = p;
   if (s.shadow) s.shadow[i] = f2bf(p);
 }

@@ -1,0 +1,487 @@
+// ddpx — pipelined bf16 MFMA GEMM core for gfx950 (shared by the plain GEMM and
+// the implicit-GEMM 3x3 convolutions).
+//
+//   C[M][N] = epilogue( sum_k A(m,k) * B(k,n) )
+//
+// Operand storage: A "K-contig" A[m][k] / "M-contig" A[k][m]; B "K-contig"
+// B[n][k] / "N-contig" B[k][n].  Addressing modes turn a (row, k) pair into a
+// byte offset, so the same pipeline serves plain matrices and im2col views of
+// NHWC activations without materialising them:
+//   MODE_PLAIN      row-major matrix with leading dimension ld
+//   MODE_IM2COL_FWD K-contig: row = output pixel, k = (tap, c)  -> x[pixel + off(tap)][c]
+//   MODE_IM2COL_BWD K-contig: row = pixel,        k = (tap, c)  -> dy[pixel - off(tap)][c]
+//   MODE_IM2COL_COL N-contig: k-row = pixel,      col = (tap,c) -> x[pixel + off(tap)][c]
+// (off(tap) = (ky-1, kx-1) for a 3x3 / pad 1 / stride 1 convolution; taps
+// falling outside the image are zero through the buffer bounds check.)
+//
+// Pipeline (cdna_hip_programming §5):
+//  * operand tiles go HBM/L2 -> LDS by `buffer_load_dwordx4 ... lds` (LDS-DMA,
+//    1 KiB per wave-instruction, no VGPR staging); out-of-range lanes get a
+//    voffset past num_records and load zeros (ragged tiles, conv padding);
+//  * STAGES-deep LDS ring, STAGES-1 K-tiles in flight; per iteration a counted
+//    `s_waitcnt vmcnt(N)` for the oldest stage, a raw `s_barrier` (never
+//    __syncthreads: its fence would drain the DMA queue), the next stage's DMA
+//    into the slot freed one iteration ago, then ds_read + MFMA;
+//  * LDS images are lane-linear, so bank swizzles are applied to the per-lane
+//    SOURCE address and undone on the read (rule 21): K-contig tiles [row][64]
+//    with chunk ^= (row>>1)&7 (conflict-free ds_read_b128), M/N-contig tiles
+//    [k][row] with a 32-B-chunk XOR read by ds_read_b64_tr_b16 (T10);
+//  * 4 waves (2x2), v_mfma_f32_16x16x32_bf16, XCD-aware workgroup remap (T1);
+//  * optional split-K over blockIdx.y (fp32 partial slabs, reduced by a
+//    separate fixed-order kernel: deterministic).
+#pragma once
+
+#include "ddpx_common.h"
+
+namespace ddpx {
+namespace pipe {
+
+enum Epi : int {
+  EPI_F32 = 0,            // C(f32)  = alpha*acc (+C)
+  EPI_BF16 = 1,           // C(bf16) = alpha*acc (+C)
+  EPI_BIAS_BF16 = 2,      // C(bf16) = acc + bias[n]
+  EPI_BIAS_RELU_BF16 = 3, // C(bf16) = max(acc + bias[n], 0)
+  EPI_BIAS_F32 = 4,       // C(f32)  = acc + bias[n]
+  EPI_RELUMASK_BF16 = 5,  // C(bf16) = acc * (aux[m][n] > 0)
+  EPI_SGD = 6,            // fused optimizer: acc is the gradient of the parameter at C's index
+  EPI_BNSTAT_BF16 = 7,    // C(bf16) = acc; per-tile column (mean, M2) of the stored values -> colsum
+};
+
+enum Mode : int { MODE_PLAIN = 0, MODE_IM2COL_FWD = 1, MODE_IM2COL_BWD = 2, MODE_IM2COL_COL = 3 };
+
+struct ConvGeom {
+  int H, W, C;  // spatial size and channel count of the NHWC tensor being im2col'd
+  int npix;     // N*H*W
+};
+
+struct Params {
+  const unsigned short* A;
+  const unsigned short* B;
+  void* C;
+  const float* bias;
+  const unsigned short* aux;
+  float* colsum;   // [tiles_m][N] column sums (EPI_*) or [tiles_m][2][N] (mean, M2) for EPI_BNSTAT
+  int M, N, K;
+  int lda, ldb, ldc, ldaux;
+  int epi, accumulate;
+  float alpha;
+  unsigned a_bytes, b_bytes;
+  SgdArgs sgd;
+  ConvGeom conv;
+  int klen;        // split-K: K elements per split (0: no split)
+  long long split_stride;  // elements between the output slabs of consecutive splits
+};
+
+constexpr unsigned kOOB = 0x80000000u;
+
+template <int ROWB>
+__device__ __forceinline__ int tr_swz(int k) {
+  if constexpr (ROWB >= 256) return (k & 3) | (((k >> 3) & 1) << 2);
+  else if constexpr (ROWB == 128) return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+  else return (k >> 3) & 1;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+// Source byte offset of the 8-element chunk at (row, k) [K-contig] or (k-row, col) [M/N-contig].
+template <int MODE, bool KC>
+__device__ __forceinline__ unsigned src_off(const ConvGeom& g, int ld, int row, int k) {
+  if constexpr (MODE == MODE_PLAIN) {
+    return KC ? (unsigned)((row * ld + k) * 2) : (unsigned)((k * ld + row) * 2);
+  } else {
+    // pixel index p and (tap, channel) index q
+    const int p = KC ? row : k;
+    const int q = KC ? k : row;
+    const int tap = q / g.C, c = q - tap * g.C;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    int dy = ky - 1, dx = kx - 1;
+    if constexpr (MODE == MODE_IM2COL_BWD) { dy = -dy; dx = -dx; }
+    const int w = p % g.W;
+    const int h = (p / g.W) % g.H;
+    const int hh = h + dy, ww = w + dx;
+    if (tap >= 9 || hh < 0 || hh >= g.H || ww < 0 || ww >= g.W) return kOOB;
+    return (unsigned)(((p + dy * g.W + dx) * g.C + c) * 2);
+  }
+}
+
+// Stage one ROWS x 64 operand tile into an LDS slot with LDS-DMA.
+template <int ROWS, bool KC, int MODE>
+__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rs, char* slot, const ConvGeom& g, int ld, int row0,
+                                           int nrows, int k0, int kend, int wave, int lane) {
+  constexpr int NI = ROWS / 32;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int inst = j * 4 + wave;
+    if constexpr (KC) {
+      const int r = inst * 8 + (lane >> 3);
+      const int pch = lane & 7;
+      const int c = pch ^ ((r >> 1) & 7);
+      const int gr = row0 + r, gk = k0 + c * 8;
+      const unsigned voff = (gr < nrows && gk < kend) ? src_off<MODE, true>(g, ld, gr, gk) : kOOB;
+      dma16(rs, slot + inst * 1024, voff);
+    } else {
+      constexpr int ROWB = ROWS * 2;
+      constexpr int CPR = ROWB / 16;
+      const int kr = inst * (1024 / ROWB) + lane / CPR;
+      const int q = lane % CPR;
+      const int L = (q >> 1) ^ tr_swz<ROWB>(kr);
+      const int col = L * 16 + (q & 1) * 8;
+      const int gk = k0 + kr, gr = row0 + col;
+      const unsigned voff = (gk < kend && gr < nrows) ? src_off<MODE, false>(g, ld, gr, gk) : kOOB;
+      dma16(rs, slot + inst * 1024, voff);
+    }
+  }
+}
+
+template <int ROWS, bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kbase, int lane) {
+  if constexpr (KC) {
+    const int row = rbase + (lane & 15);
+    const int chunk = (kbase >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+  } else {
+    constexpr int ROWB = ROWS * 2;
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int chunk32 = rbase >> 4;
+    const int k0 = kbase + 8 * g + q;
+    const int k1 = k0 + 4;
+    const int off0 = k0 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k0)) << 5) + p * 8;
+    const int off1 = k1 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k1)) << 5) + p * 8;
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(lds + off0));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(lds + off1));
+    short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---------------------------------------------------------------- epilogue
+// The accumulator tile is staged through LDS as fp32 [BM][BN+4]; every thread
+// then owns one 4-column quad (BN/4 quads, 256 % (BN/4) == 0) for rows
+// r = t/(BN/4) + i*(256/(BN/4)) and moves 16-B vectors: all global operand
+// loads of a thread are issued before any result is computed (the fused SGD
+// epilogue reads p and momentum, the ReLU-mask epilogue reads aux).
+
+template <int E>
+__device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t off, int n, float v, float lr,
+                                         float cin, unsigned short auxv, float pv, float bv, float* p_out,
+                                         float* b_out) {
+  float stored;
+  if constexpr (E == EPI_F32) {
+    stored = v * p.alpha + cin;
+  } else if constexpr (E == EPI_BF16 || E == EPI_BNSTAT_BF16) {
+    stored = bf2f(f2bf(v * p.alpha + cin));
+  } else if constexpr (E == EPI_BIAS_BF16) {
+    stored = bf2f(f2bf(v + p.bias[n]));
+  } else if constexpr (E == EPI_BIAS_RELU_BF16) {
+    stored = bf2f(f2bf(fmaxf(v + p.bias[n], 0.f)));
+  } else if constexpr (E == EPI_BIAS_F32) {
+    stored = v + p.bias[n];
+  } else if constexpr (E == EPI_SGD) {
+    stored = v * p.alpha;
+    float d = fmaf(p.sgd.wd, pv, stored);
+    if (p.sgd.mom != 0.f) {
+      d = fmaf(p.sgd.mom, bv, d);
+      *b_out = d;
+    }
+    *p_out = fmaf(-lr, d, pv);
+  } else {  // EPI_RELUMASK_BF16
+    const bool pos = (auxv & 0x8000u) == 0 && (auxv & 0x7fffu) != 0;
+    stored = pos ? bf2f(f2bf(v)) : 0.f;
+  }
+  return stored;
+}
+
+template <int E, int BM, int BN>
+__device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const float* T, int m0, int n0, int tid,
+                                             float (&csum)[4]) {
+  constexpr int Q = BN / 4;           // column quads per row
+  constexpr int RSTEP = 256 / Q;      // rows between a thread's consecutive vectors
+  constexpr int NV = BM / RSTEP;      // vectors per thread
+  constexpr int TLD = BN + 4;
+  const int cq = tid % Q, r0 = tid / Q;
+  const int n = n0 + 4 * cq;
+  const bool vec = (n + 3 < p.N) && ((p.ldc & 3) == 0);
+  float lr = 0.f;
+  if constexpr (E == EPI_SGD) lr = *p.sgd.lr;
+  constexpr int CH = NV < 4 ? NV : 4;  // vectors whose loads are in flight together (VGPR budget)
+#pragma unroll
+  for (int i0 = 0; i0 < NV; i0 += CH) {
+  f32x4 pin[CH], bin[CH], cin[CH];
+  u32x2 ain[CH];
+  // phase 1: issue every global load of this chunk
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int m = m0 + r0 + (i0 + i) * RSTEP;
+    pin[i] = bin[i] = cin[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    ain[i] = (u32x2){0u, 0u};
+    if (m >= p.M) continue;
+    const size_t off = (size_t)m * p.ldc + n;
+    if (vec) {
+      if constexpr (E == EPI_SGD) {
+        pin[i] = *reinterpret_cast<const f32x4*>(p.sgd.p + off);
+        if (p.sgd.mom != 0.f) bin[i] = *reinterpret_cast<const f32x4*>(p.sgd.buf + off);
+      } else if constexpr (E == EPI_F32) {
+        if (p.accumulate) cin[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(Cbase) + off);
+      } else if constexpr (E == EPI_BF16) {
+        if (p.accumulate) {
+          const u32x2 c = *reinterpret_cast<const u32x2*>(reinterpret_cast<const unsigned short*>(Cbase) + off);
+          cin[i] = (f32x4){__uint_as_float(c[0] << 16), __uint_as_float(c[0] & 0xffff0000u),
+                           __uint_as_float(c[1] << 16), __uint_as_float(c[1] & 0xffff0000u)};
+        }
+      } else if constexpr (E == EPI_RELUMASK_BF16) {
+        ain[i] = *reinterpret_cast<const u32x2*>(p.aux + (size_t)m * p.ldaux + n);
+      }
+    }
+  }
+  // phase 2: compute and store
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int r = r0 + (i0 + i) * RSTEP;
+    const int m = m0 + r;
+    if (m >= p.M) continue;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + r * TLD + 4 * cq);
+    const size_t off = (size_t)m * p.ldc + n;
+    if (vec) {
+      float st[4], po[4], bo[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned short av = (unsigned short)((q & 1) ? (ain[i][q >> 1] >> 16) : (ain[i][q >> 1] & 0xffffu));
+        st[q] = epi_one<E>(p, Cbase, off + q, n + q, v[q], lr, cin[i][q], av, pin[i][q], bin[i][q], &po[q], &bo[q]);
+        csum[q] += st[q];
+      }
+      if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cbase) + off) = (f32x4){st[0], st[1], st[2], st[3]};
+      } else if constexpr (E == EPI_SGD) {
+        *reinterpret_cast<f32x4*>(p.sgd.p + off) = (f32x4){po[0], po[1], po[2], po[3]};
+        if (p.sgd.mom != 0.f) *reinterpret_cast<f32x4*>(p.sgd.buf + off) = (f32x4){bo[0], bo[1], bo[2], bo[3]};
+        if (p.sgd.shadow)
+          *reinterpret_cast<u32x2*>(p.sgd.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      } else {
+        *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(Cbase) + off) =
+            (u32x2){pack_bf2(st[0], st[1]), pack_bf2(st[2], st[3])};
+      }
+    } else {
+      // ragged right edge / odd leading dimension: scalar path
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q >= p.N) continue;
+        const size_t o = off + q;
+        float c0 = 0.f, pv = 0.f, bv = 0.f;
+        unsigned short av = 0;
+        if constexpr (E == EPI_F32) { if (p.accumulate) c0 = reinterpret_cast<const float*>(Cbase)[o]; }
+        if constexpr (E == EPI_BF16) { if (p.accumulate) c0 = bf2f(reinterpret_cast<const unsigned short*>(Cbase)[o]); }
+        if constexpr (E == EPI_RELUMASK_BF16) av = p.aux[(size_t)m * p.ldaux + n + q];
+        if constexpr (E == EPI_SGD) { pv = p.sgd.p[o]; if (p.sgd.mom != 0.f) bv = p.sgd.buf[o]; }
+        float po = 0.f, bo = 0.f;
+        const float st = epi_one<E>(p, Cbase, o, n + q, v[q], lr, c0, av, pv, bv, &po, &bo);
+        csum[q] += st;
+        if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
+          reinterpret_cast<float*>(Cbase)[o] = st;
+        } else if constexpr (E == EPI_SGD) {
+          p.sgd.p[o] = po;
+          if (p.sgd.mom != 0.f) p.sgd.buf[o] = bo;
+          if (p.sgd.shadow) p.sgd.shadow[o] = f2bf(po);
+        } else {
+          reinterpret_cast<unsigned short*>(Cbase)[o] = f2bf(st);
+        }
+      }
+    }
+  }
+}  // chunk
+}
+
+// Column reductions of the stored tile: thread (cq, r0) holds partial sums of 4 columns.
+template <int BN>
+__device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], int tid, float* out /* BN */) {
+  constexpr int Q = BN / 4, RG = 256 / Q;
+  const int cq = tid % Q, rg = tid / Q;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[rg * BN + 4 * cq + q] = cs[q];
+  __syncthreads();
+  if (tid < BN) {
+    float s = 0.f;
+    for (int g = 0; g < RG; ++g) s += red[g * BN + tid];
+    out[tid] = s;
+  }
+  __syncthreads();
+}
+
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE>
+__global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
+  constexpr int BK = 64;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int SLOT = A_BYTES + B_BYTES;
+  constexpr int FM = BM / 32, FN = BN / 32;
+  constexpr int LPW = BM / 32 + BN / 32;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = wg % tiles_m, tn = wg / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int split = blockIdx.y;
+  const int kbeg = p.klen ? split * p.klen : 0;
+  const int kend = p.klen ? min(p.K, kbeg + p.klen) : p.K;
+  void* Cbase = p.C;
+  if (p.klen) Cbase = reinterpret_cast<char*>(p.C) + (size_t)split * p.split_stride * (p.epi == EPI_F32 ? 4 : 2);
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, p.b_bytes, 0x00020000);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  auto issue = [&](int t) {
+    char* slot = smem + (t % STAGES) * SLOT;
+    const int k0 = kbeg + t * BK;
+    stage_tile<BM, AK, AMODE>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+    stage_tile<BN, BKc, BMODE>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+  };
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(STAGES - 2, nk - 1 - t);
+    if (ahead >= 2) wait_vmcnt<2 * LPW>();
+    else if (ahead == 1) wait_vmcnt<LPW>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+
+    const char* sa = smem + (t % STAGES) * SLOT;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / 2) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = frag<BN, BKc>(sb, wn * (BN / 2) + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- stage the accumulator tile through LDS (all DMA has landed: last wait was vmcnt(0)) ----
+  constexpr int TLD = BN + 4;
+  float* T = reinterpret_cast<float*>(smem);
+  static_assert(BM * TLD * 4 + (256 / (BN / 4) + 2) * BN * 4 <= STAGES * SLOT, "epilogue LDS overflow");
+  __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
+  {
+    const int mr = wm * (BM / 2) + 4 * (lane >> 4);
+    const int nc = wn * (BN / 2) + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[(mr + i * 16 + r) * TLD + nc + j * 16] = acc[i][j][r];
+  }
+  __syncthreads();
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  switch (p.epi) {
+    case EPI_F32: epilogue_vec<EPI_F32, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BF16: epilogue_vec<EPI_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_SGD: epilogue_vec<EPI_SGD, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    default: epilogue_vec<EPI_RELUMASK_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+  }
+  if (!p.colsum) return;
+
+  // ---- per-tile column reductions (bias gradient / BatchNorm statistics) ----
+  // scratch after the tile image: [256/(BN/4)][BN] partials + [BN] results
+  float* red = T + BM * TLD;
+  float* colres = red + (256 / (BN / 4)) * BN;
+  __syncthreads();
+  quad_colsum<BN>(red, cs, tid, colres);
+  if (p.epi != EPI_BNSTAT_BF16) {
+    if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
+    return;
+  }
+  // BatchNorm statistics of the stored (bf16-rounded) values: tile mean, then M2 = sum (y - mean)^2.
+  const int rows_valid = min(BM, p.M - m0);
+  float* tmean = colres + BN;
+  if (tid < BN) tmean[tid] = colres[tid] / (float)rows_valid;
+  __syncthreads();
+  {
+    constexpr int Q = BN / 4, RSTEP = 256 / Q, NV = BM / RSTEP;
+    const int cq = tid % Q, r0 = tid / Q;
+    float m2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int r = r0 + i * RSTEP;
+      if (m0 + r >= p.M) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float y = bf2f(f2bf(T[r * TLD + 4 * cq + q] * p.alpha));
+        const float d = y - tmean[4 * cq + q];
+        m2[q] += d * d;
+      }
+    }
+    quad_colsum<BN>(red, m2, tid, colres);
+  }
+  if (tid < BN && n0 + tid < p.N) {
+    p.colsum[((size_t)tm * 2) * p.N + n0 + tid] = tmean[tid];
+    p.colsum[((size_t)tm * 2 + 1) * p.N + n0 + tid] = colres[tid];
+  }
+}
+
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE>
+static hipError_t launch(const Params& p, int splits, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE>), dim3(tiles, splits), dim3(256), 0, s,
+                     p);
+  return hipGetLastError();
+}
+
+static inline void tile_of(int cfg, int* bm, int* bn) {
+  static const int t[8][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  *bm = t[cfg & 7][0];
+  *bn = t[cfg & 7][1];
+}
+
+template <bool AK, bool BKc, int AMODE, int BMODE>
+static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
+    case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
+    case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
+    case 3: return launch<64, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);    //  64 KiB, 2 WG/CU
+    case 4: return launch<128, 128, 3, AK, BKc, AMODE, BMODE>(p, splits, s);  //  96 KiB
+    case 5: return launch<64, 128, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
+    case 6: return launch<128, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
+    default: return launch<64, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  48 KiB, 3 WG/CU
+  }
+}
+
+}  // namespace pipe
+}  // namespace ddpx

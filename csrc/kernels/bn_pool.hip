@@ -1,0 +1,381 @@
+// ddpx — BatchNorm2d (training/eval) + ReLU + MaxPool2d(2) on NHWC bf16, fused.
+//
+// Reference layers (/root/reference/singlegpu.py:64-70, per conv block):
+//   nn.BatchNorm2d(x) -> nn.ReLU(True) [-> nn.MaxPool2d(2)]
+// (SURVEY §2.2 N8/N9/N10).  Semantics kept exactly: batch statistics over
+// N*H*W with the biased variance for normalisation, running_mean/var updated
+// with momentum 0.1 using the UNBIASED variance, num_batches_tracked += 1,
+// eps 1e-5, eval mode uses the running statistics; max-pool backward routes
+// the gradient to the FIRST maximum of each 2x2 window in scan order (torch's
+// max_pool2d_with_indices tie rule).
+//
+// Data flow (MI355X-first):
+//   * the conv forward GEMM epilogue already produced per-tile (mean, M2) of
+//     its bf16 output y; bn_finalize merges them (Chan et al.) per channel —
+//     numerically robust, no E[y^2]-E[y]^2 cancellation over 524288 pixels;
+//   * bn_apply reads y once and writes relu(a*y+b) (pooled when a pool
+//     follows) — 8 channels per thread, 16-B accesses;
+//   * backward never stores indices or masks: the ReLU mask and the pool
+//     argmax are recomputed from y, a, b.  Pass 1 reduces sum(g) and
+//     sum(g*xhat) per channel (per-block partials, fixed-order merge); pass 2
+//     writes dy = a*(g - mean(g) - xhat*mean(g*xhat)) in bf16 for the conv
+//     dgrad/wgrad GEMMs.
+#include "ddpx_common.h"
+
+namespace ddpx {
+namespace bn {
+
+// ---------------------------------------------------------------- finalize
+// stats[t][0][c] = tile mean, stats[t][1][c] = tile M2; tile t covers rows [t*BM, min(M,(t+1)*BM)).
+// 64 threads (one wave) per channel: each lane merges a strided subset of tiles,
+// then a fixed-shape butterfly merges the lanes.
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  if (nb == 0.f) return;
+  if (n == 0.f) { n = nb; mean = meanb; m2 = m2b; return; }
+  const float nn = n + nb;
+  const float d = meanb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+__global__ void __launch_bounds__(256)
+finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, const float* __restrict__ gamma,
+                const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+                int64_t* __restrict__ nbt, float momentum, float eps, int training, float* __restrict__ a_out,
+                float* __restrict__ b_out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    float n = 0.f, mu = 0.f, m2 = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float nt = (float)min(BM, M - t * BM);
+      chan_merge(n, mu, m2, nt, stats[((size_t)t * 2) * C + c], stats[((size_t)t * 2 + 1) * C + c]);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64), qb = __shfl_xor(m2, o, 64);
+      // symmetric merge: lower lane merges upper lane's state (same result in both lanes up to order;
+      // use the lower lane as the canonical order)
+      if ((lane & o) == 0) chan_merge(n, mu, m2, nb, mb, qb);
+      else {
+        float n2 = nb, mu2 = mb, q2 = qb;
+        chan_merge(n2, mu2, q2, n, mu, m2);
+        n = n2; mu = mu2; m2 = q2;
+      }
+    }
+    mean = mu;
+    var = m2 / (float)M;  // biased, for normalisation
+    if (lane == 0) {
+      const float unbiased = M > 1 ? m2 / (float)(M - 1) : m2;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+      if (c == 0 && nbt) nbt[0] += 1;
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  if (lane == 0) {
+    const float rstd = rsqrtf(var + eps);
+    const float a = gamma[c] * rstd;
+    a_out[c] = a;
+    b_out[c] = beta[c] - mean * a;
+    mean_out[c] = mean;
+    rstd_out[c] = rstd;
+  }
+}
+
+// ---------------------------------------------------------------- apply
+__device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(v[j] << 16);
+    f[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
+  return (u32x4){pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7])};
+}
+
+// out = relu(a*y + b), optionally 2x2 max-pooled.  One thread per (output pixel, 8-channel group).
+__global__ void __launch_bounds__(256)
+apply_kernel(const unsigned short* __restrict__ y, const float* __restrict__ a, const float* __restrict__ b, int N,
+             int H, int W, int C, int relu, int pool, unsigned short* __restrict__ out) {
+  const int G = C / 8;
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= N * Ho * Wo * G) return;
+  const int g = t % G;
+  const int pix = t / G;
+  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / (Wo * Ho);
+  float av[8], bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    av[j] = a[g * 8 + j];
+    bv[j] = b[g * 8 + j];
+  }
+  float r[8];
+  if (!pool) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r[j] = fmaf(av[j], f[j], bv[j]);
+      if (relu) r[j] = fmaxf(r[j], 0.f);
+    }
+  } else {
+    u32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int hh = 2 * ho + (q >> 1), ww = 2 * wo + (q & 1);
+      v[q] = *reinterpret_cast<const u32x4*>(y + (((size_t)n * H + hh) * W + ww) * C + g * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float f[8];
+      unpack8(v[q], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = fmaf(av[j], f[j], bv[j]);
+        if (relu) z = fmaxf(z, 0.f);
+        r[j] = fmaxf(r[j], z);
+      }
+    }
+  }
+  *reinterpret_cast<u32x4*>(out + (size_t)pix * C + g * 8) = pack8(r);
+}
+
+// ---------------------------------------------------------------- backward
+// gz for the 8 channels of pre-pool pixel (n, h, w): routes the pooled gradient to the
+// first max of the 2x2 window (recomputed from y) and applies the ReLU mask.
+__device__ __forceinline__ void grad_z(const unsigned short* __restrict__ gout, const unsigned short* __restrict__ y,
+                                       const float (&av)[8], const float (&bv)[8], int n, int h, int w, int H, int W,
+                                       int C, int g, int pool, int relu, const float (&yself)[8], float (&gz)[8]) {
+  float zs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    zs[j] = fmaf(av[j], yself[j], bv[j]);
+  }
+  if (!pool) {
+    float gg[8];
+    unpack8(*reinterpret_cast<const u32x4*>(gout + (((size_t)n * H + h) * W + w) * C + g * 8), gg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gz[j] = (!relu || zs[j] > 0.f) ? gg[j] : 0.f;
+    return;
+  }
+  const int ho = h >> 1, wo = w >> 1, Ho = H >> 1, Wo = W >> 1;
+  const int me = ((h & 1) << 1) | (w & 1);
+  float gg[8];
+  unpack8(*reinterpret_cast<const u32x4*>(gout + (((size_t)n * Ho + ho) * Wo + wo) * C + g * 8), gg);
+  u32x4 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int hh = 2 * ho + (q >> 1), ww = 2 * wo + (q & 1);
+    v[q] = *reinterpret_cast<const u32x4*>(y + (((size_t)n * H + hh) * W + ww) * C + g * 8);
+  }
+  float best[8];
+  int arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float f[8];
+    unpack8(v[q], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = fmaf(av[j], f[j], bv[j]);
+      if (relu) z = fmaxf(z, 0.f);
+      if (z > best[j]) { best[j] = z; arg[j] = q; }  // strict: first max wins
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gz[j] = (arg[j] == me && (!relu || zs[j] > 0.f)) ? gg[j] : 0.f;
+}
+
+// Pass 1: part[blk][0][c] = sum gz, part[blk][1][c] = sum gz * xhat over this block's pixels.
+// Block = 256 threads = (C/8 channel groups) x (256/(C/8) pixel lanes); grid-strided over pixels.
+__global__ void __launch_bounds__(256)
+bwd_reduce_kernel(const unsigned short* __restrict__ gout, const unsigned short* __restrict__ y,
+                  const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ mean,
+                  const float* __restrict__ rstd, int N, int H, int W, int C, int pool, int relu,
+                  float* __restrict__ part) {
+  __shared__ float red[2][256 * 8];
+  const int G = C / 8;
+  const int lanes = 256 / G;  // pixel lanes per block (G <= 64 => >= 4)
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  const int P = N * H * W;
+  float av[8], bv[8], mu[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    av[j] = a[g * 8 + j]; bv[j] = b[g * 8 + j]; mu[j] = mean[g * 8 + j]; rs[j] = rstd[g * 8 + j];
+    s1[j] = 0.f; s2[j] = 0.f;
+  }
+  for (int pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
+    const int w = pix % W, h = (pix / W) % H, n = pix / (W * H);
+    float f[8], gz[8];
+    unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
+    grad_z(gout, y, av, bv, n, h, w, H, W, C, g, pool, relu, f, gz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] += gz[j];
+      s2[j] = fmaf(gz[j], (f[j] - mu[j]) * rs[j], s2[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x * 8 + j] = s1[j];
+    red[1][threadIdx.x * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  // channel c = g*8 + j: sum over the pixel lanes pl (threads t = pl*G + g)
+  for (int i = threadIdx.x; i < 2 * C; i += 256) {
+    const int which = i / C, c = i % C, gg = c / 8, j = c % 8;
+    float s = 0.f;
+    for (int q = 0; q < lanes; ++q) s += red[which][(q * G + gg) * 8 + j];
+    part[((size_t)blockIdx.x * 2 + which) * C + c] = s;
+  }
+}
+
+// Fixed-order merge of the pass-1 partials: dbeta = sum gz, dgamma = sum gz*xhat; also the
+// pass-2 coefficients c1 = dbeta/M, c2 = dgamma/M.  Gradients stored or applied (fused SGD).
+__global__ void __launch_bounds__(256)
+bwd_finalize_kernel(const float* __restrict__ part, int B, int C, int M, float* __restrict__ c1,
+                    float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta, int out_bf16,
+                    int accumulate, SgdArgs sg, SgdArgs sb) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < B; ++k) {
+    s1 += part[((size_t)k * 2) * C + c];
+    s2 += part[((size_t)k * 2 + 1) * C + c];
+  }
+  c1[c] = s1 / (float)M;
+  c2[c] = s2 / (float)M;
+  auto put = [&](const SgdArgs& sgd, void* out, float v) {
+    if (sgd.p) {
+      sgd_apply(sgd, c, v, *sgd.lr);
+    } else if (out_bf16) {
+      unsigned short* d = reinterpret_cast<unsigned short*>(out) + c;
+      *d = f2bf(accumulate ? v + bf2f(*d) : v);
+    } else if (out) {
+      float* d = reinterpret_cast<float*>(out) + c;
+      *d = accumulate ? v + *d : v;
+    }
+  };
+  put(sg, dgamma, s2);
+  put(sb, dbeta, s1);
+}
+
+// Pass 2: dy = a * (gz - c1 - xhat * c2)   (bf16 [P][C])
+__global__ void __launch_bounds__(256)
+bwd_apply_kernel(const unsigned short* __restrict__ gout, const unsigned short* __restrict__ y,
+                 const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ mean,
+                 const float* __restrict__ rstd, const float* __restrict__ c1, const float* __restrict__ c2, int N,
+                 int H, int W, int C, int pool, int relu, unsigned short* __restrict__ dy) {
+  const int G = C / 8;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int P = N * H * W;
+  if (t >= P * G) return;
+  const int g = t % G, pix = t / G;
+  const int w = pix % W, h = (pix / W) % H, n = pix / (W * H);
+  float av[8], bv[8], f[8], gz[8], out[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { av[j] = a[g * 8 + j]; bv[j] = b[g * 8 + j]; }
+  unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
+  grad_z(gout, y, av, bv, n, h, w, H, W, C, g, pool, relu, f, gz);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = g * 8 + j;
+    const float xh = (f[j] - mean[c]) * rstd[c];
+    out[j] = av[j] * (gz[j] - c1[c] - xh * c2[c]);
+  }
+  *reinterpret_cast<u32x4*>(dy + (size_t)pix * C + g * 8) = pack8(out);
+}
+
+// [N][S][C] -> [N][C] mean over S pixels (global average pool) and its backward.
+__global__ void __launch_bounds__(256) avgpool_kernel(const unsigned short* __restrict__ x, int N, int S, int C,
+                                                      unsigned short* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= N * C) return;
+  const int c = t % C, n = t / C;
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += bf2f(x[((size_t)n * S + i) * C + c]);
+  out[t] = f2bf(s / (float)S);
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const unsigned short* __restrict__ g, int N, int S, int C,
+                                                          unsigned short* __restrict__ gx) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= N * S * C) return;
+  const int c = t % C, n = t / (S * C);
+  gx[t] = f2bf(bf2f(g[(size_t)n * C + c]) / (float)S);
+}
+
+}  // namespace bn
+}  // namespace ddpx
+
+using namespace ddpx;
+
+DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
+                              float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
+                              float* a, float* b, float* mean, float* rstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn::finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, stats, T, BM, M, C, gamma, beta, rmean,
+                     rvar, nbt, momentum, eps, training, a, b, mean, rstd);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_bn_apply(const void* y, const float* a, const float* b, int N, int H, int W, int C, int relu,
+                           int pool, void* out, hipStream_t s) {
+  if (C % 8 || (pool && (H % 2 || W % 2))) return -1;
+  const int n = N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 8);
+  hipLaunchKernelGGL(bn::apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)y, a, b, N, H,
+                     W, C, relu, pool, (unsigned short*)out);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_bn_bwd_blocks(int N, int H, int W, int C) {
+  const int lanes = 256 / (C / 8);
+  const int P = N * H * W;
+  int blocks = (P + lanes * 16 - 1) / (lanes * 16);  // >= 16 pixels per lane
+  if (blocks > 1024) blocks = 1024;
+  return blocks < 1 ? 1 : blocks;
+}
+
+DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const float* b, const float* mean,
+                         const float* rstd, int N, int H, int W, int C, int pool, int relu, float* part, float* c1,
+                         float* c2, void* dgamma, void* dbeta, int out_bf16, int accumulate, void* dy, float* sg_p,
+                         float* sg_buf, float* sb_p, float* sb_buf, const float* lr, float mom, float wd,
+                         hipStream_t s) {
+  if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
+  const int B = ddpx_bn_bwd_blocks(N, H, W, C);
+  hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
+                     dgamma, dbeta, out_bf16, accumulate, SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd},
+                     SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
+  const int n = N * H * W * (C / 8);
+  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu,
+                     (unsigned short*)dy);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_avgpool(const void* x, int N, int S, int C, void* out, hipStream_t s) {
+  const int n = N * C;
+  hipLaunchKernelGGL(bn::avgpool_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)x, N, S, C,
+                     (unsigned short*)out);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_avgpool_bwd(const void* g, int N, int S, int C, void* gx, hipStream_t s) {
+  const int n = N * S * C;
+  hipLaunchKernelGGL(bn::avgpool_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)g, N, S,
+                     C, (unsigned short*)gx);
+  return (int)hipGetLastError();
+}

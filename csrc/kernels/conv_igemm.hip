@@ -1,0 +1,195 @@
+// ddpx — 3x3 / stride 1 / pad 1 convolutions as implicit GEMMs on the
+// pipelined MFMA core (ddpx_pipe.h), NHWC bf16 activations.
+//
+// Replaces MIOpen's conv fwd / dgrad / wgrad for the reference's VGG
+// (/root/reference/singlegpu.py:64 `nn.Conv2d(in, x, 3, padding=1, bias=False)`;
+// SURVEY §2.2 N7, §2.3 shape table).  With P = N*H*W pixels:
+//   forward : y[P][Co]        = im2col(x)[P][9Ci]      . Wf[Co][9Ci]^T   (A: IM2COL_FWD, B: K-contig)
+//   dgrad   : dx[P][Ci]       = im2col~(dy)[P][9Co]    . Wd[9Co][Ci]     (A: IM2COL_BWD, B: N-contig)
+//   wgrad   : dW[Co][9Ci]     = dy[P][Co]^T            . im2col(x)[P][9Ci] (A: M-contig, B: IM2COL_COL)
+// where the K index is (tap, channel) with channel fastest, so every 16-B
+// DMA chunk is 8 consecutive channels of one pixel.  Padding taps are zero
+// through the buffer bounds check.  Wf = W permuted to [Co][3][3][Ci],
+// Wd = W permuted to [3][3][Co][Ci] (ddpx_conv_weight_prep, one pass per
+// step, channels padded to a multiple of 8 with zeros — conv0's Ci = 3).
+// The weight gradient (K = P up to 524288) is split over blockIdx.y into
+// fp32 slabs reduced in fixed order by ddpx_conv_wgrad_reduce, which also
+// permutes back to torch's [Co][Ci][3][3] layout (checkpoint format) and
+// either stores the gradient or applies the fused SGD update.
+// The forward epilogue can emit per-tile BatchNorm statistics (mean, M2 of
+// the stored bf16 outputs) for the fused BN that follows (bn.hip).
+#include "ddpx_pipe.h"
+
+namespace ddpx {
+namespace conv {
+
+using namespace pipe;
+
+// fp32 torch weight [Co][Cr][3][3] -> Wf bf16 [Co][9][Cp], Wd bf16 [9][Co][Cp]  (Cp >= Cr, zero padded)
+__global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restrict__ w, int Co, int Cr, int Cp,
+                                                          unsigned short* __restrict__ wf,
+                                                          unsigned short* __restrict__ wd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over Co*9*Cp, output-major (c fastest)
+  if (i >= Co * 9 * Cp) return;
+  const int c = i % Cp;
+  const int t = (i / Cp) % 9;
+  const int o = i / (9 * Cp);
+  const float v = c < Cr ? w[((size_t)o * Cr + c) * 9 + t] : 0.f;
+  const unsigned short h = f2bf(v);
+  if (wf) wf[i] = h;
+  if (wd) wd[((size_t)t * Co + o) * Cp + c] = h;
+}
+
+// out (torch layout [Co][Cr][3][3]) (=|+=) sum_s part[s][Co][9*Cp]   or fused SGD on the parameter
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Cr,
+                                                           int Cp, void* __restrict__ out, int out_bf16,
+                                                           int accumulate, SgdArgs sgd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over torch-layout elements Co*Cr*9
+  if (i >= Co * Cr * 9) return;
+  const int t = i % 9;
+  const int c = (i / 9) % Cr;
+  const int o = i / (9 * Cr);
+  const size_t src = (size_t)o * 9 * Cp + t * Cp + c;
+  const size_t slab = (size_t)Co * 9 * Cp;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += part[k * slab + src];
+  if (sgd.p) {
+    sgd_apply(sgd, i, s, *sgd.lr);
+  } else if (out_bf16) {
+    unsigned short* d = reinterpret_cast<unsigned short*>(out) + i;
+    *d = f2bf(accumulate ? s + bf2f(*d) : s);
+  } else {
+    float* d = reinterpret_cast<float*>(out) + i;
+    *d = accumulate ? s + *d : s;
+  }
+}
+
+static int pick_fwd(int P, int Co) {
+  // conv0/1 (Co 64/128, P = 512K): 128x64 tiles; small spatial layers: 64x64 for >= 256 WGs
+  if ((long long)((P + 127) / 128) * ((Co + 63) / 64) >= 1024) return 6;  // 128x64, 3 stages
+  return 7;                                                               // 64x64, 3 stages
+}
+
+}  // namespace conv
+}  // namespace ddpx
+
+using namespace ddpx;
+using namespace ddpx::pipe;
+
+static bool chk16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+DDPX_API int ddpx_conv_weight_prep(const float* w, int Co, int Cr, int Cp, void* wf, void* wd, hipStream_t s) {
+  if (Cp % 8 || Cp < Cr) return -1;
+  const int n = Co * 9 * Cp;
+  hipLaunchKernelGGL(conv::weight_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, Co, Cr, Cp,
+                     (unsigned short*)wf, (unsigned short*)wd);
+  return (int)hipGetLastError();
+}
+
+// Row tiles the forward GEMM uses (for sizing the BatchNorm statistics partials).
+DDPX_API int ddpx_conv_fwd_tiles_m(int P, int Co, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+  int bm, bn;
+  tile_of(cfg, &bm, &bn);
+  return (P + bm - 1) / bm;
+}
+
+DDPX_API int ddpx_conv_fwd_tile_rows(int P, int Co, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+  int bm, bn;
+  tile_of(cfg, &bm, &bn);
+  return bm;
+}
+
+// y[P][Co] = conv(x, W).  x NHWC [N][H][W][C] bf16 (C % 8 == 0), wf [Co][9][C].
+// stats (optional): [tiles_m][2][Co] per-tile (mean, M2) of the stored bf16 outputs.
+DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats, int N, int H, int W, int C, int Co,
+                           int tile_cfg, hipStream_t s) {
+  if (C % 8 || Co % 8) return -1;
+  if (!chk16(x) || !chk16(wf) || !chk16(y)) return -3;
+  const int P = N * H * W, K = 9 * C;
+  Params p{};
+  p.A = (const unsigned short*)x;
+  p.B = (const unsigned short*)wf;
+  p.C = y;
+  p.colsum = stats;
+  p.M = P; p.N = Co; p.K = K;
+  p.lda = C; p.ldb = K; p.ldc = Co;
+  p.epi = stats ? EPI_BNSTAT_BF16 : EPI_BF16;
+  p.alpha = 1.f;
+  const size_t ab = (size_t)P * C * 2, bb = (size_t)Co * K * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = ConvGeom{H, W, C, P};
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+  return (int)dispatch<true, true, MODE_IM2COL_FWD, MODE_PLAIN>(p, cfg, 1, s);
+}
+
+// dx[P][C] = dgrad(dy, W) (optionally times relu mask of aux — unused by VGG, whose
+// ReLU sits behind BN).  dy [P][Co] bf16, wd [9][Co][C] bf16.
+DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, int H, int W, int C, int Co,
+                             int tile_cfg, hipStream_t s) {
+  if (C % 8 || Co % 8) return -1;
+  if (!chk16(dy) || !chk16(wd) || !chk16(dx)) return -3;
+  const int P = N * H * W, K = 9 * Co;
+  Params p{};
+  p.A = (const unsigned short*)dy;
+  p.B = (const unsigned short*)wd;
+  p.C = dx;
+  p.M = P; p.N = C; p.K = K;
+  p.lda = Co; p.ldb = C; p.ldc = C;
+  p.epi = EPI_BF16;
+  p.alpha = 1.f;
+  const size_t ab = (size_t)P * Co * 2, bb = (size_t)K * C * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = ConvGeom{H, W, Co, P};
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C);
+  return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
+}
+
+// Number of K splits the weight-gradient GEMM uses, and its partial-slab size (floats).
+DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co) {
+  const int tiles = ((Co + 63) / 64) * ((9 * C + 63) / 64);
+  int S = (512 + tiles - 1) / tiles;
+  const int maxS = (P + 1023) / 1024;  // >= 16 K-steps per split
+  if (S > maxS) S = maxS;
+  return S < 1 ? 1 : S;
+}
+
+// part[S][Co][9C] (fp32) = split-K partial weight gradients.  dy [P][Co], x NHWC [N][H][W][C].
+DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, int N, int H, int W, int C, int Co,
+                             hipStream_t s) {
+  if (C % 8 || Co % 8 || S < 1) return -1;
+  if (!chk16(dy) || !chk16(x) || !chk16(part)) return -3;
+  const int P = N * H * W;
+  Params p{};
+  p.A = (const unsigned short*)dy;
+  p.B = (const unsigned short*)x;
+  p.C = part;
+  p.M = Co; p.N = 9 * C; p.K = P;
+  p.lda = Co; p.ldb = C; p.ldc = 9 * C;
+  p.epi = EPI_F32;
+  p.alpha = 1.f;
+  const size_t ab = (size_t)P * Co * 2, bb = (size_t)P * C * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = ConvGeom{H, W, C, P};
+  p.klen = ((P + S - 1) / S + 63) / 64 * 64;
+  p.split_stride = (long long)Co * 9 * C;
+  const int Sreal = (P + p.klen - 1) / p.klen;
+  if (Sreal != S) {
+    // zero the slabs that get no K range so the reduce can always sum S
+    hipMemsetAsync(part + (size_t)Sreal * p.split_stride, 0, (size_t)(S - Sreal) * p.split_stride * 4, s);
+  }
+  return (int)dispatch<false, false, MODE_PLAIN, MODE_IM2COL_COL>(p, 7, Sreal, s);
+}
+
+DDPX_API int ddpx_conv_wgrad_reduce(const float* part, int S, int Co, int Cr, int Cp, void* out, int out_bf16,
+                                    int accumulate, float* sgd_p, float* sgd_buf, void* sgd_shadow,
+                                    const float* sgd_lr, float sgd_mom, float sgd_wd, hipStream_t s) {
+  const int n = Co * Cr * 9;
+  hipLaunchKernelGGL(conv::wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, S, Co, Cr, Cp, out,
+                     out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
+  return (int)hipGetLastError();
+}

@@ -13,7 +13,7 @@
 
 namespace ddpx {
 
-enum OutLayout : int { OUT_NCHW_F32 = 0, OUT_NCHW_BF16 = 1, OUT_NHWC_BF16 = 2, OUT_NHWC_F32 = 3 };
+enum OutLayout : int { OUT_NCHW_F32 = 0, OUT_NCHW_BF16 = 1, OUT_NHWC_BF16 = 2, OUT_NHWC_F32 = 3, OUT_NHWC8_BF16 = 4 };
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -30,7 +30,7 @@ __global__ void __launch_bounds__(256)
 augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
                const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad, uint64_t seed,
                int train, int layout, void* __restrict__ out, int64_t* __restrict__ tgt_out) {
-  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32);
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
   const int G = W / 8;  // 8-pixel groups per row (W % 8 == 0 checked on the host)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int total = nhwc ? B * H * W : B * C * H * G;
@@ -82,6 +82,16 @@ augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ l
     const int x = flip ? (W - 1 - xo) : xo;
     const int sx = x + dx - pad;
     const bool ok = row_ok && sx >= 0 && sx < W;
+    if (layout == OUT_NHWC8_BF16) {
+      // NHWC with the channels zero-padded to 8 (16-B pixels: the conv0 implicit-GEMM input)
+      float v[8];
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc)
+        v[cc] = (ok && cc < C) ? (float)img[(size_t)cc * H * W + sy * W + sx] * inv : 0.f;
+      u32x4 pk = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+      *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned short*>(out) + (((size_t)b * H + y) * W + xo) * 8) = pk;
+      return;
+    }
     const size_t o = (((size_t)b * H + y) * W + xo) * C;
     for (int cc = 0; cc < C; ++cc) {
       const float v = ok ? (float)img[(size_t)cc * H * W + sy * W + sx] * inv : 0.f;
@@ -100,7 +110,8 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
                           hipStream_t s) {
   if (B <= 0) return 0;
   if (W % 8) return -1;
-  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32);
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
+  if (layout == OUT_NHWC8_BF16 && C > 8) return -2;
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);

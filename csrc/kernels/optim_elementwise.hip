@@ -42,19 +42,21 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
     } else {
       gv = reinterpret_cast<const f32x4*>(g)[i];
     }
-    f32x4 d = gv * gscale + wd * pv;
-    f32x4 b;
-    if (mom != 0.f) {
-      if (first) {
-        b = d;
-      } else {
-        b = reinterpret_cast<const f32x4*>(buf)[i];
-        b = mom * b + d;
+    // same fma sequence as sgd_apply() (fused-backward epilogues): bitwise-identical updates
+    f32x4 b = reinterpret_cast<const f32x4*>(buf)[i];
+    f32x4 po, bo;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float d = fmaf(wd, pv[q], gv[q] * gscale);
+      if (mom != 0.f) {
+        const float bb = first ? d : fmaf(mom, b[q], d);
+        bo[q] = bb;
+        d = nesterov ? fmaf(mom, bb, d) : bb;
       }
-      reinterpret_cast<f32x4*>(buf)[i] = b;
-      d = nesterov ? d + mom * b : b;
+      po[q] = fmaf(-lr, d, pv[q]);
     }
-    pv = pv - lr * d;
+    if (mom != 0.f) reinterpret_cast<f32x4*>(buf)[i] = bo;
+    pv = po;
     reinterpret_cast<f32x4*>(p)[i] = pv;
     if (shadow) {
       u32x2 s = {pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3])};
@@ -66,13 +68,13 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
     const int64_t j = (nv << 2) + threadIdx.x;
     float gv = GBF16 ? bf2f(reinterpret_cast<const unsigned short*>(g)[j])
                      : reinterpret_cast<const float*>(g)[j];
-    float d = gv * gscale + wd * p[j];
+    float d = fmaf(wd, p[j], gv * gscale);
     if (mom != 0.f) {
-      float b = first ? d : mom * buf[j] + d;
+      const float b = first ? d : fmaf(mom, buf[j], d);
       buf[j] = b;
-      d = nesterov ? d + mom * b : b;
+      d = nesterov ? fmaf(mom, b, d) : b;
     }
-    p[j] -= lr * d;
+    p[j] = fmaf(-lr, d, p[j]);
     if (shadow) shadow[j] = f2bf(p[j]);
   }
 }

@@ -13,11 +13,12 @@ __all__ = ["VGG", "DeepNN", "MLP", "build_model"]
 def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "native"):
     dev = torch.device(device) if device is not None else torch.device("cpu")
     if dtype == "auto":
-        dtype = "bf16" if (dev.type == "cuda" and name.startswith("mlp")) else "fp32"
+        dtype = "bf16" if dev.type == "cuda" else "fp32"
     cdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     if name == "vgg":
         m = VGG()
-        m.use_native = False
+        # native NHWC bf16 kernels on the GPU unless fp32 (torch/MIOpen) was asked for
+        m.use_native = kernels == "native" and dev.type == "cuda" and dtype != "fp32"
     elif name == "deepnn":
         m = DeepNN()
     elif name in ("mlp", "mlp_wide"):

