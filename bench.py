@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--layers", type=int, default=3)
     p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg"])
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
+    p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--overlap_optimizer", action="store_true")
     p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
@@ -127,6 +128,8 @@ def build_torch(args, device, world):
     if args.model == "vgg":
         from ddpx.models import VGG
         model = VGG().to(device)
+        if args.torch_amp:
+            model = model.to(memory_format=torch.channels_last)
     else:
         dims = [3072] + [args.hidden] * (args.layers - 1) + [10]
         layers = []
@@ -187,7 +190,7 @@ def main():
             b = full[k % len(full)]
             x, y = loader.make_batch(idx_all[b * bs:(b + 1) * bs], k)
             opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model != "vgg"):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model != "vgg" or args.torch_amp):
                 out = net(x)
             loss = torch.nn.functional.cross_entropy(out.float(), y)
             loss.backward()
@@ -225,7 +228,7 @@ def main():
     rec = {
         "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if (args.model != "vgg" or args.impl == "ddpx") else "fp32",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if (args.model != "vgg" or args.impl == "ddpx" or args.torch_amp) else "fp32",
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),

@@ -211,7 +211,9 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
   const bool vec = (n + 3 < p.N) && ((p.ldc & 3) == 0);
   float lr = 0.f;
   if constexpr (E == EPI_SGD) lr = *p.sgd.lr;
-  constexpr int CH = NV < 4 ? NV : 4;  // vectors whose loads are in flight together (VGPR budget)
+  // vectors whose loads are in flight together: the fused-SGD epilogue is a pure stream (p, momentum
+  // in; p, momentum, shadow out) and needs every byte in flight it can get; the others stay at 4
+  constexpr int CH = E == EPI_SGD ? (NV < 8 ? NV : 8) : (NV < 4 ? NV : 4);
 #pragma unroll
   for (int i0 = 0; i0 < NV; i0 += CH) {
   f32x4 pin[CH], bin[CH], cin[CH];
@@ -225,9 +227,9 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
     if (m >= p.M) continue;
     const size_t off = (size_t)m * p.ldc + n;
     if (vec) {
-      if constexpr (E == EPI_SGD) {
-        pin[i] = *reinterpret_cast<const f32x4*>(p.sgd.p + off);
-        if (p.sgd.mom != 0.f) bin[i] = *reinterpret_cast<const f32x4*>(p.sgd.buf + off);
+      if constexpr (E == EPI_SGD) {  // read-once / write-once streams: non-temporal
+        pin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.p + off));
+        if (p.sgd.mom != 0.f) bin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.buf + off));
       } else if constexpr (E == EPI_F32) {
         if (p.accumulate) cin[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(Cbase) + off);
       } else if constexpr (E == EPI_BF16) {
@@ -260,8 +262,9 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
       if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cbase) + off) = (f32x4){st[0], st[1], st[2], st[3]};
       } else if constexpr (E == EPI_SGD) {
-        *reinterpret_cast<f32x4*>(p.sgd.p + off) = (f32x4){po[0], po[1], po[2], po[3]};
-        if (p.sgd.mom != 0.f) *reinterpret_cast<f32x4*>(p.sgd.buf + off) = (f32x4){bo[0], bo[1], bo[2], bo[3]};
+        __builtin_nontemporal_store((f32x4){po[0], po[1], po[2], po[3]}, reinterpret_cast<f32x4*>(p.sgd.p + off));
+        if (p.sgd.mom != 0.f)
+          __builtin_nontemporal_store((f32x4){bo[0], bo[1], bo[2], bo[3]}, reinterpret_cast<f32x4*>(p.sgd.buf + off));
         if (p.sgd.shadow)
           *reinterpret_cast<u32x2*>(p.sgd.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
       } else {

@@ -248,13 +248,22 @@ __global__ void __launch_bounds__(256)
 bwd_finalize_kernel(const float* __restrict__ part, int B, int C, int M, float* __restrict__ c1,
                     float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta, int out_bf16,
                     int accumulate, SgdArgs sg, SgdArgs sb) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  // 16 lanes per channel: strided partial sums, then a fixed butterfly (deterministic)
+  const int sub = threadIdx.x & 15;
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
   float s1 = 0.f, s2 = 0.f;
-  for (int k = 0; k < B; ++k) {
-    s1 += part[((size_t)k * 2) * C + c];
-    s2 += part[((size_t)k * 2 + 1) * C + c];
+  if (c < C) {
+    for (int k = sub; k < B; k += 16) {
+      s1 += part[((size_t)k * 2) * C + c];
+      s2 += part[((size_t)k * 2 + 1) * C + c];
+    }
   }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (c >= C || sub != 0) return;
   c1[c] = s1 / (float)M;
   c2[c] = s2 / (float)M;
   auto put = [&](const SgdArgs& sgd, void* out, float v) {
@@ -356,7 +365,7 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
                      dgamma, dbeta, out_bf16, accumulate, SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd},
                      SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
   const int n = N * H * W * (C / 8);

@@ -148,9 +148,17 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
 }
 
-// Number of K splits the weight-gradient GEMM uses, and its partial-slab size (floats).
-DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co) {
-  const int tiles = ((Co + 63) / 64) * ((9 * C + 63) / 64);
+static int pick_wgrad(int P, int C, int Co) {
+  (void)P;
+  return (Co >= 128 && 9 * C >= 128) ? 4 : 7;  // 128x128 / 3 stages where the weight is big enough
+}
+
+// Number of K splits the weight-gradient GEMM uses for a tile config (cfg < 0: default).
+DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : pick_wgrad(P, C, Co);
+  int bm, bn;
+  tile_of(cfg, &bm, &bn);
+  const int tiles = ((Co + bm - 1) / bm) * ((9 * C + bn - 1) / bn);
   int S = (512 + tiles - 1) / tiles;
   const int maxS = (P + 1023) / 1024;  // >= 16 K-steps per split
   if (S > maxS) S = maxS;
@@ -159,7 +167,7 @@ DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co) {
 
 // part[S][Co][9C] (fp32) = split-K partial weight gradients.  dy [P][Co], x NHWC [N][H][W][C].
 DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, int N, int H, int W, int C, int Co,
-                             hipStream_t s) {
+                             int tile_cfg, hipStream_t s) {
   if (C % 8 || Co % 8 || S < 1) return -1;
   if (!chk16(dy) || !chk16(x) || !chk16(part)) return -3;
   const int P = N * H * W;
@@ -182,7 +190,8 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
     // zero the slabs that get no K range so the reduce can always sum S
     hipMemsetAsync(part + (size_t)Sreal * p.split_stride, 0, (size_t)(S - Sreal) * p.split_stride * 4, s);
   }
-  return (int)dispatch<false, false, MODE_PLAIN, MODE_IM2COL_COL>(p, 7, Sreal, s);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : pick_wgrad(P, C, Co);
+  return (int)dispatch<false, false, MODE_PLAIN, MODE_IM2COL_COL>(p, cfg, Sreal, s);
 }
 
 DDPX_API int ddpx_conv_wgrad_reduce(const float* part, int S, int Co, int Cr, int Cp, void* out, int out_bf16,

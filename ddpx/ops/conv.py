@@ -36,7 +36,7 @@ def weight_prep(w: torch.Tensor, wf: torch.Tensor, wd: torch.Tensor):
                                                         native.stream_handle()), "ddpx_conv_weight_prep")
 
 
-def conv_fwd(x, wf, Co, stats=True):
+def conv_fwd(x, wf, Co, stats=True, tile=-1):
     """y [N*H*W, Co] bf16 (+ per-tile BN statistics [T,2,Co] fp32 and tile rows)."""
     N, H, W, C = x.shape
     _nhwc(x, "x")
@@ -46,35 +46,35 @@ def conv_fwd(x, wf, Co, stats=True):
     y = torch.empty((P, Co), dtype=torch.bfloat16, device=x.device)
     st, T, BM = None, 0, 0
     if stats:
-        T = lib.ddpx_conv_fwd_tiles_m(P, Co, -1)
-        BM = lib.ddpx_conv_fwd_tile_rows(P, Co, -1)
+        T = lib.ddpx_conv_fwd_tiles_m(P, Co, tile)
+        BM = lib.ddpx_conv_fwd_tile_rows(P, Co, tile)
         st = torch.empty((T, 2, Co), dtype=torch.float32, device=x.device)
-    native.check(lib.ddpx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, Co, -1,
+    native.check(lib.ddpx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, Co, tile,
                                    native.stream_handle()), "ddpx_conv_fwd")
     return y, st, T, BM
 
 
-def conv_dgrad(dy, wd, N, H, W, C, Co):
+def conv_dgrad(dy, wd, N, H, W, C, Co, tile=-1):
     """dx [N,H,W,C] bf16 = dgrad(dy [N*H*W, Co], wd [9,Co,C])."""
     _nhwc(dy, "dy", Co)
     _req(wd.numel() == 9 * Co * C, "conv_dgrad: bad weight buffer")
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
-    native.check(native.kernels().ddpx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), N, H, W, C, Co, -1,
+    native.check(native.kernels().ddpx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), N, H, W, C, Co, tile,
                                                   native.stream_handle()), "ddpx_conv_dgrad")
     return dx
 
 
-def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None):
+def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None, tile=-1):
     """Weight gradient in torch layout [Co,Cr,3,3] (written to ``out`` or applied through ``sgd``)."""
     N, H, W, C = x.shape
     _nhwc(x, "x")
     _nhwc(dy, "dy", Co)
     lib = native.kernels()
     P = N * H * W
-    S = lib.ddpx_conv_wgrad_splits(P, C, Co)
+    S = lib.ddpx_conv_wgrad_splits(P, C, Co, tile)
     part = torch.empty((S, Co, 9 * C), dtype=torch.float32, device=x.device)
     s = native.stream_handle()
-    native.check(lib.ddpx_conv_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), S, N, H, W, C, Co, s),
+    native.check(lib.ddpx_conv_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), S, N, H, W, C, Co, tile, s),
                  "ddpx_conv_wgrad")
     if sgd is None:
         _req(out is not None and out.numel() == Co * Cr * 9 and out.is_contiguous(), "conv_wgrad: bad out")

@@ -66,8 +66,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I)
     _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
-    _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I)
-    _sig(lib, "ddpx_conv_wgrad", I, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I, I)
+    _sig(lib, "ddpx_conv_wgrad", I, P, P, P, I, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_bn_finalize", I, P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P)
     _sig(lib, "ddpx_bn_apply", I, P, P, P, I, I, I, I, I, I, P, P)

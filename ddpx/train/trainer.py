@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..runtime.graphs import CapturedStep
+from ..utils.profiling import trace_range
 from . import checkpoint as ckpt
 
 
@@ -64,9 +65,12 @@ class Trainer:
 
     def _step_body(self, source, targets):
         self.optimizer.zero_grad()
-        loss = self._forward_loss(source, targets)
-        loss.backward()
-        self.optimizer.step()
+        with trace_range("forward"):
+            loss = self._forward_loss(source, targets)
+        with trace_range("backward"):
+            loss.backward()
+        with trace_range("optimizer"):
+            self.optimizer.step()
         return loss
 
     def _run_batch(self, source, targets):
@@ -103,8 +107,15 @@ class Trainer:
             self.train_data.set_epoch(epoch)
         t0 = time.time()
         n = 0
-        for source, targets in self.train_data:
-            self._run_batch(source, targets)
+        it = iter(self.train_data)
+        while True:
+            with trace_range("data"):
+                batch = next(it, None)
+            if batch is None:
+                break
+            source, targets = batch
+            with trace_range("step"):
+                self._run_batch(source, targets)
             n += source.shape[0]
         if self.metrics is not None:
             loss = float(self.last_loss.detach().float().item()) if self.last_loss is not None else float("nan")

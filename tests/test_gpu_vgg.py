@@ -105,19 +105,26 @@ def _vgg_pair(gpu, seed=0):
 
 
 def test_vgg_native_matches_torch(gpu):
+    """Whole native VGG (bf16 NHWC) vs torch fp32; the error budget is set by torch's own bf16 autocast
+    error on the same batch (same precision class), since bf16 rounding compounds through 8 BN layers."""
+    import copy
     torch.manual_seed(2)
     m, ref = _vgg_pair(gpu)
+    amp = copy.deepcopy(ref)
     N = 32
-    x = torch.rand(N, 3, 32, 32, device=gpu)
+    x = _bf(torch.rand(N, 3, 32, 32, device=gpu))
     t = torch.randint(0, 10, (N,), device=gpu)
-    x = _bf(x)
     loss, _ = m.forward_loss(x, t)
     loss.backward()
     rl = F.cross_entropy(ref(x), t)
     rl.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        al = F.cross_entropy(amp(x).float(), t)
+    al.backward()
     assert abs(loss.item() - rl.item()) < 3e-2 * max(1.0, rl.item())
-    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
-        assert _rel(p.main_grad, q.grad) < 0.1, n
+    for (n, p), (_, q), (_, r) in zip(m.named_parameters(), ref.named_parameters(), amp.named_parameters()):
+        ours, theirs = _rel(p.main_grad, q.grad), _rel(r.grad, q.grad)
+        assert ours < 3 * theirs + 0.03, (n, ours, theirs)
     for (n, bb), (_, cc) in zip(m.named_buffers(), ref.named_buffers()):
         if bb.dtype == torch.int64:
             assert int(bb) == int(cc), n
