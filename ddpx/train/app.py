@@ -22,6 +22,7 @@ from ..models import build_model
 from ..optim.schedule import one_cycle, resolve_steps_per_epoch
 from ..optim.sgd import SGD
 from ..parallel.comm import RcclComm, TorchComm
+from ..parallel.sync_bn import convert_sync_batchnorm
 from ..parallel.ddp import DistributedDataParallel
 from ..runtime.setup import prepare_model
 from ..utils.metrics import MetricsWriter
@@ -92,8 +93,13 @@ def input_layout(model, device, dtype):
     return "nchw_f32"
 
 
-def load_train_objs(args, device, distributed: bool, world_size: int, loader_len_hint: int):
-    """(train_set, model, optimizer, test_set, scheduler) — the reference's factory, ddpx engine underneath."""
+def load_train_objs(args, device, distributed: bool, world_size: int, loader_len_hint: int, comm=None):
+    """(train_set, model, optimizer, test_set, scheduler) — the reference's factory, ddpx engine underneath.
+
+    ``--sync_bn`` (reference: the commented-out ``convert_sync_batchnorm`` at
+    ``/root/reference/multigpu.py:127``) swaps every BatchNorm2d for :class:`SyncBatchNorm2d` on ``comm``
+    before the flat parameter store is built; the VGG then runs on the torch-op path.
+    """
     kind = resolve_data(args)
     train_set, test_set = get_datasets(kind, args.data_root, seed=0, train_size=args.train_size,
                                        test_size=args.test_size)
@@ -101,6 +107,10 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
         torch.manual_seed(args.seed)
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels)
+    if getattr(args, "sync_bn", False) and distributed:
+        if hasattr(model, "use_native"):
+            model.use_native = False
+        model = convert_sync_batchnorm(model, comm)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"),
@@ -125,17 +135,18 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
     if device.type == "cuda":
         torch.cuda.set_device(device)
     train_n = args.train_size if resolve_data(args) == "synthetic" else 50000
-    dataset, model, optimizer, testdata, scheduler = load_train_objs(
-        args, device, distributed, world_size, _loader_len(train_n, args.batch_size, world_size))
-    layout = input_layout(model, device, args.dtype)
-    train_data = prepare_dataloader(dataset, args.batch_size, device, layout, rank, world_size)
-    net = model
     comm = None
     if distributed:
         if device.type == "cuda" and args.comm == "rccl":
             comm = RcclComm(device)
         else:
             comm = TorchComm()
+    dataset, model, optimizer, testdata, scheduler = load_train_objs(
+        args, device, distributed, world_size, _loader_len(train_n, args.batch_size, world_size), comm)
+    layout = input_layout(model, device, args.dtype)
+    train_data = prepare_dataloader(dataset, args.batch_size, device, layout, rank, world_size)
+    net = model
+    if distributed:
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=args.overlap_optimizer)

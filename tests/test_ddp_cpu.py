@@ -124,3 +124,50 @@ def test_rank_failure_propagates():
     with pytest.raises(Exception, match="injected failure"):
         mp.spawn(_fail_worker, args=(2, free_port()), nprocs=2, join=True)
     assert time.time() - t0 < 120
+
+
+def _syncbn_worker(rank, ws, port):
+    import ddpx
+    from ddpx.models import VGG
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from ddpx.parallel.sync_bn import SyncBatchNorm2d, convert_sync_batchnorm
+    init_gloo(rank, ws, port)
+    try:
+        torch.manual_seed(0)
+        base = VGG()
+        single = VGG()
+        single.load_state_dict(base.state_dict())
+        comm = TorchComm()
+        m = convert_sync_batchnorm(base, comm)
+        assert sum(isinstance(x, SyncBatchNorm2d) for x in m.modules()) == 8
+        assert list(m.state_dict().keys()) == list(single.state_dict().keys())
+        ddpx.prepare_model(m, "cpu")
+        d = DistributedDataParallel(m, comm=comm)
+        init = [p.detach().clone() for p in single.parameters()]
+        opt = SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
+        g = torch.Generator().manual_seed(42)
+        X = torch.rand((4 * ws, 3, 32, 32), generator=g)
+        T = torch.randint(0, 10, (4 * ws,), generator=g)
+        opt.zero_grad()
+        F.cross_entropy(d(X[4 * rank:4 * rank + 4]), T[4 * rank:4 * rank + 4]).backward()
+        opt.step()
+        so = torch.optim.SGD(single.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
+        so.zero_grad()
+        F.cross_entropy(single(X), T).backward()
+        so.step()
+        # compare the UPDATES by relative norm: a ReLU/max-pool decision on a value within ~1e-6 of its
+        # threshold may legitimately flip between two fp32 summation orders
+        for (n, p), (_, q), p0 in zip(m.named_parameters(), single.named_parameters(), init):
+            rel = ((p - q).norm() / (q - p0).norm()).item()
+            assert rel < 2e-2, (n, rel)
+        for (n, b), (_, c) in zip(m.named_buffers(), single.named_buffers()):
+            assert torch.allclose(b.float(), c.float(), atol=1e-5, rtol=1e-4), n
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_batchnorm_equals_full_batch():
+    """With SyncBN, 2 ranks x 4 samples == one process on all 8 samples (BN stats are global)."""
+    mp.spawn(_syncbn_worker, args=(2, free_port()), nprocs=2, join=True)
