@@ -43,14 +43,20 @@ def parse():
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
     p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
     p.add_argument("--no_graph", action="store_true")
-    p.add_argument("--overlap_optimizer", action="store_true")
+    p.add_argument("--overlap_optimizer", type=int, default=None,
+                   help="1: per-bucket optimizer as each collective lands (default 1 for N>1)")
+    p.add_argument("--shard_optimizer", type=int, default=None,
+                   help="1: ZeRO-1 reduce-scatter / shard update / bf16 all-gather (default 1 for N>1)")
     p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
-    p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"],
-                   help="gradient buffer / all-reduce dtype (bf16 = values of bf16 MFMA wgrads, as autocast)")
+    p.add_argument("--grad_dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                   help="gradient buffer / reduction dtype (bf16 = values of the bf16 MFMA wgrads, as under "
+                        "autocast); auto: fp32 at N=1 (grads never leave the fused kernels), bf16 for N>1")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
+    p.add_argument("--ddp_single", action="store_true",
+                   help="N=1: still run the DDP machinery (RCCL reducer at world size 1) to measure its overhead")
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args()
 
@@ -74,7 +80,7 @@ def setup_dist(n, impl):
             print(f"bench.py: --gpus {n} needs a launcher (torchrun --nproc-per-node {n})", file=sys.stderr)
             sys.exit(2)
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or (n == 1 and "--ddp_single" in sys.argv):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # ddpx: GPU collectives go through its own RCCL communicator; the c10d group only
         # bootstraps it (TCPStore) and carries CPU barriers/timing -> gloo.  torch: stock RCCL PG.
@@ -95,6 +101,16 @@ def make_data(args, device, rank, world, layout=None):
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
 
 
+def resolve_defaults(args, world):
+    multi = world > 1 or args.ddp_single
+    if args.grad_dtype == "auto":
+        args.grad_dtype = "bf16" if multi else "fp32"
+    if args.overlap_optimizer is None:
+        args.overlap_optimizer = int(multi)
+    if args.shard_optimizer is None:
+        args.shard_optimizer = int(multi)
+
+
 def build_ddpx(args, device, world):
     from ddpx.models import build_model
     from ddpx.optim.schedule import one_cycle, resolve_steps_per_epoch
@@ -107,13 +123,15 @@ def build_ddpx(args, device, world):
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update is fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
-              fused_backward=(world == 1 and not args.no_fused_optimizer))
+              fused_backward=(world == 1 and not args.ddp_single and not args.no_fused_optimizer))
     net = model
-    if world > 1:
+    if world > 1 or args.ddp_single:
         net = DistributedDataParallel(model, comm=RcclComm(device), bucket_cap_mb=args.bucket_cap_mb,
+                                      reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
-                                      overlap_optimizer=args.overlap_optimizer)
-        if args.overlap_optimizer:
+                                      overlap_optimizer=bool(args.overlap_optimizer),
+                                      shard_optimizer=bool(args.shard_optimizer))
+        if args.overlap_optimizer or args.shard_optimizer:
             net.attach_optimizer(opt)
     sched = one_cycle(opt, resolve_steps_per_epoch("compat", 0, world > 1))
     return model, net, opt, sched
@@ -147,6 +165,7 @@ def build_torch(args, device, world):
 def main():
     args = parse()
     rank, world, local = setup_dist(args.gpus, args.impl)
+    resolve_defaults(args, world)
     device = torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
     idx_all = loader._epoch_indices()
@@ -219,6 +238,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    multi = world > 1 or args.ddp_single
+    consistent = None
+    if multi and args.impl == "ddpx":
+        # outside the timed region: replicas must hold identical weights after K steps
+        net.consolidate()
+        ck = [float(net.flat.master.double().sum().item()), float(net.flat.master.double().abs().sum().item())]
+        allck = [None] * world
+        dist.all_gather_object(allck, ck)
+        consistent = all(c == allck[0] for c in allck)
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
@@ -233,9 +261,12 @@ def main():
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
-                       " fused-into-backward" if (args.impl == "ddpx" and world == 1 and not args.no_fused_optimizer)
+                       " fused-into-backward" if (args.impl == "ddpx" and not multi and not args.no_fused_optimizer)
                        else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
-                   "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4)},
+                   "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4),
+                   "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
+                   "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
+                   "replicas_consistent": consistent},
     }
     if rank == 0:
         line = json.dumps(rec)
@@ -243,7 +274,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "a") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if multi:
         if args.impl == "ddpx" and hasattr(net, "close"):
             net.close()
             net.comm.close()

@@ -110,14 +110,24 @@ void track_op(Comm* c, hipStream_t s, const char* what) {
 
 // ---------------------------------------------------------------------------
 // Reducer: gradient buckets -> all-reduce on the comm stream.
+// mode 0: all-reduce the bucket in place (replicated optimizer).
+// mode 1: reduce-scatter in place (sharded optimizer, ZeRO-1): rank r receives the reduced
+//         shard [r*count/n, (r+1)*count/n) at its own position; after the optimizer updated
+//         that shard, gather() all-gathers the bucket's parameter copy in place.
 struct Bucket {
   void* ptr = nullptr;
   size_t count = 0;
   int dtype = ncclFloat32;
   int expected = 0;
   int pending = 0;
+  int mode = 0;
   bool launched = false;
   hipEvent_t ready = nullptr, done = nullptr;
+  void* gptr = nullptr;  // gather target (bf16 shadow or fp32 master slice of the bucket)
+  size_t gcount = 0;
+  int gdtype = ncclBfloat16;
+  bool gathering = false;
+  hipEvent_t gready = nullptr, gdone = nullptr;
 };
 
 struct Reducer {
@@ -203,6 +213,16 @@ DDPX_API int ddpx_comm_destroy(void* h, int abort) {
 
 static hipStream_t pick_stream(Comm* c, hipStream_t s) { return s ? s : c->stream; }
 
+static size_t dtype_size(int dt) {
+  switch (dt) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return 0;
+  }
+}
+
 DDPX_API int ddpx_comm_allreduce(void* h, const void* send, void* recv, size_t count, int dtype, int op,
                                  hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
@@ -255,20 +275,39 @@ DDPX_API void* ddpx_reducer_create(void* comm, int nbuckets, int op) {
   for (auto& b : r->buckets) {
     hipEventCreateWithFlags(&b.ready, hipEventDisableTiming);
     hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+    hipEventCreateWithFlags(&b.gready, hipEventDisableTiming);
+    hipEventCreateWithFlags(&b.gdone, hipEventDisableTiming);
   }
   return r;
 }
 
-DDPX_API int ddpx_reducer_set_bucket(void* h, int i, void* ptr, size_t count, int dtype, int expected) {
+DDPX_API int ddpx_reducer_set_bucket(void* h, int i, void* ptr, size_t count, int dtype, int expected, int mode) {
   Reducer* r = static_cast<Reducer*>(h);
   if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  if (mode != 0 && mode != 1) return -2;
+  if (mode == 1 && (count % (size_t)r->comm->nranks) != 0) return -3;  // shards must be equal
+  if (dtype_size(dtype) == 0) return -4;
   Bucket& b = r->buckets[i];
   b.ptr = ptr;
   b.count = count;
   b.dtype = dtype;
   b.expected = expected;
   b.pending = expected;
+  b.mode = mode;
   b.launched = false;
+  return 0;
+}
+
+// Parameter copy that gather() all-gathers in place after the owner updated its shard.
+DDPX_API int ddpx_reducer_set_gather(void* h, int i, void* ptr, size_t count, int dtype) {
+  Reducer* r = static_cast<Reducer*>(h);
+  if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  if (count % (size_t)r->comm->nranks != 0) return -3;
+  if (dtype_size(dtype) == 0) return -4;
+  Bucket& b = r->buckets[i];
+  b.gptr = ptr;
+  b.gcount = count;
+  b.gdtype = dtype;
   return 0;
 }
 
@@ -288,7 +327,14 @@ static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
   if (he != hipSuccess) return (int)he;
   he = hipStreamWaitEvent(c->stream, b.ready, 0);
   if (he != hipSuccess) return (int)he;
-  int e = ddpx_comm_allreduce(c, b.ptr, b.ptr, b.count, b.dtype, r->op, c->stream);
+  int e;
+  if (b.mode == 1) {
+    size_t shard = b.count / (size_t)c->nranks;
+    char* recv = static_cast<char*>(b.ptr) + (size_t)c->rank * shard * dtype_size(b.dtype);
+    e = ddpx_comm_reduce_scatter(c, b.ptr, recv, shard, b.dtype, r->op, c->stream);
+  } else {
+    e = ddpx_comm_allreduce(c, b.ptr, b.ptr, b.count, b.dtype, r->op, c->stream);
+  }
   if (e) return e;
   he = hipEventRecord(b.done, c->stream);
   if (he != hipSuccess) return (int)he;
@@ -341,11 +387,46 @@ DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
   return forced;
 }
 
+// Sharded optimizer: after `compute` wrote this rank's shard of bucket i's parameter copy,
+// all-gather the copy in place on the comm stream (ordered after the reduce-scatters already
+// queued there).  wait_gather() joins it into a stream that is about to read the parameters.
+DDPX_API int ddpx_reducer_gather(void* h, int i, hipStream_t compute) {
+  Reducer* r = static_cast<Reducer*>(h);
+  if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  Bucket& b = r->buckets[i];
+  if (!b.gptr) return -2;
+  Comm* c = r->comm;
+  hipError_t he = hipEventRecord(b.gready, compute);
+  if (he != hipSuccess) return (int)he;
+  he = hipStreamWaitEvent(c->stream, b.gready, 0);
+  if (he != hipSuccess) return (int)he;
+  size_t shard = b.gcount / (size_t)c->nranks;
+  const char* send = static_cast<const char*>(b.gptr) + (size_t)c->rank * shard * dtype_size(b.gdtype);
+  int e = ddpx_comm_allgather(c, send, b.gptr, shard, b.gdtype, c->stream);
+  if (e) return e;
+  he = hipEventRecord(b.gdone, c->stream);
+  if (he != hipSuccess) return (int)he;
+  b.gathering = true;
+  return 0;
+}
+
+DDPX_API int ddpx_reducer_wait_gather(void* h, int i, hipStream_t s) {
+  Reducer* r = static_cast<Reducer*>(h);
+  if (i < 0 || i >= (int)r->buckets.size()) return -1;
+  Bucket& b = r->buckets[i];
+  if (!b.gathering) return 0;
+  hipError_t he = hipStreamWaitEvent(s, b.gdone, 0);
+  b.gathering = false;
+  return (int)he;
+}
+
 DDPX_API int ddpx_reducer_destroy(void* h) {
   Reducer* r = static_cast<Reducer*>(h);
   for (auto& b : r->buckets) {
     hipEventDestroy(b.ready);
     hipEventDestroy(b.done);
+    hipEventDestroy(b.gready);
+    hipEventDestroy(b.gdone);
   }
   delete r;
   return 0;

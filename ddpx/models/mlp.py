@@ -88,7 +88,9 @@ class MLP(nn.Module):
         if self.native_active(device):
             from ..runtime import native
             native.kernels()  # fail loudly if the extension is missing on a GPU
-            return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters())}
+            # weights are read by the kernels only through the bf16 shadow; biases in fp32
+            return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters()),
+                    "shadow_only_params": [m.weight for m in self.modules() if isinstance(m, nn.Linear)]}
         return {}
 
     def input_layout(self, device) -> str:

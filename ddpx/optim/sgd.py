@@ -43,7 +43,9 @@ class SGD(Optimizer):
         if ids != {id(p) for p in flat.params}:
             raise ValueError("SGD must own exactly the parameters of one FlatParams store")
         self.flat: FlatParams = flat
-        self.momentum_buffer = torch.zeros_like(flat.master) if momentum else None
+        if momentum:
+            # registered with the store so a re-layout (sharded DDP) carries it along
+            flat.state_tensors["momentum"] = torch.zeros_like(flat.master)
         self.capturable = capturable
         # fused_backward: single-process training applies each parameter's update inside the kernel
         # that produces its gradient (no gradient round trip through HBM, no separate SGD pass).
@@ -52,8 +54,15 @@ class SGD(Optimizer):
         self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if need_dev_lr else None
         if self.fused_backward:
             flat.fused_opt = self
-        self.bucket_source = None  # set by DDP when the optimizer overlaps the all-reduce
+        self.bucket_source = None  # set by DDP when the optimizer overlaps the all-reduce or is sharded
+        flat.optimizer = self
+        if getattr(flat.sink, "sharded", False):
+            flat.sink.attach_optimizer(self)
         self.step_count = 0
+
+    @property
+    def momentum_buffer(self):
+        return self.flat.state_tensors.get("momentum")
 
     # ------------------------------------------------------------------ API
     def zero_grad(self, set_to_none: bool = True):  # noqa: D401 - torch signature
@@ -92,7 +101,16 @@ class SGD(Optimizer):
         if not (self.flat.master.is_cuda and torch.cuda.is_current_stream_capturing()):
             self.flat.fix_unwritten()
         src = self.bucket_source
-        if any(self.flat.updated):
+        if src is not None and getattr(src, "sharded", False):
+            # ZeRO-1: each rank updates only its shard of every sharded bucket (gradients were
+            # reduce-scattered), then the bucket's parameter copy is all-gathered in place
+            for b in src.bucket_order():
+                src.wait_bucket(b)
+                for (start, end) in src.update_ranges(b):
+                    self._update(start, end, g)
+                src.gather_bucket(b)
+            src.optimizer_done()
+        elif any(self.flat.updated):
             # fused-backward parameters are already stepped; update the rest range by range
             f = self.flat
             i, n = 0, len(f.params)

@@ -123,8 +123,10 @@ class TorchComm(Comm):
         if self.world_size == 1:
             out.copy_(inp)
             return
-        dist.all_gather_into_tensor(out, inp, group=self.group) if inp.is_cuda else dist.all_gather(
-            list(out.chunk(self.world_size)), inp, group=self.group)
+        if inp.is_cuda:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        else:  # inp may alias its own chunk of out (in-place gather): send a copy
+            dist.all_gather(list(out.chunk(self.world_size)), inp.clone(), group=self.group)
 
 
 class _ScaleOnWait:

@@ -27,6 +27,15 @@ MI355X-specific design:
 * ``overlap_optimizer=True`` leaves the buckets un-joined at the end of
   backward; ``ddpx.optim.SGD`` then updates each bucket's slice as soon as its
   collective lands, overlapping the optimizer with the remaining traffic.
+* ``shard_optimizer=True`` (ZeRO-1, not in the reference — SURVEY §2.5 lists it as absent):
+  the flat store is re-packed so every bucket splits into ``world_size`` equal 256-B-aligned
+  shards; backward reduce-scatters each bucket in place (same bytes on the wire as the
+  all-reduce's first half), every rank runs SGD on its own shard only (1/N of the optimizer's
+  HBM traffic), and the updated parameters are all-gathered in place.  For models whose
+  kernels read weights only through the bf16 compute shadow (the native MLP) just the shadow
+  is gathered — half the bytes of an fp32 all-gather — and the few fp32-read parameters
+  (biases) stay replicated in one all-reduced bucket.  ``consolidate()`` gathers fp32 master
+  weights and momentum on every rank before a checkpoint.
 """
 from __future__ import annotations
 
@@ -37,7 +46,7 @@ import torch.distributed as dist
 from torch import nn
 
 from ..runtime import native
-from ..runtime.flat_params import FlatParams, flat_of
+from ..runtime.flat_params import ALIGN, FlatParams, flat_of
 from .comm import NCCL_DTYPE, NCCL_OP, Comm, RcclComm, TorchComm
 
 DEFAULT_FIRST_BUCKET_MB = 1.0   # dist._DEFAULT_FIRST_BUCKET_BYTES
@@ -86,13 +95,26 @@ class FlatBuffers:
 class _PyReducer:
     """Bucket state machine over torch.distributed async collectives (CPU / gloo)."""
 
-    def __init__(self, comm: TorchComm, ranges):
+    def __init__(self, comm: TorchComm, ranges, modes=None):
         self.comm = comm
         self.ranges = ranges
+        self.modes = modes or [0] * len(ranges)
         self.tensors = None
         self.expected = None
         self.pending = None
         self.works = None
+        self.gather_targets = [None] * len(ranges)
+
+    def set_gather(self, b, t):
+        self.gather_targets[b] = t
+
+    def gather(self, b):
+        """In-place all-gather of bucket b's parameter copy (synchronous on gloo)."""
+        t = self.gather_targets[b]
+        self.comm.allgather(t, t.chunk(self.comm.world_size)[self.comm.rank])
+
+    def wait_gather(self, b, stream=None):
+        pass
 
     def setup(self, grad_flat, expected):
         self.tensors = [grad_flat[s:e] for s, e in self.ranges]
@@ -105,6 +127,8 @@ class _PyReducer:
         self.launched = [False] * len(self.ranges)
 
     def _launch(self, b):
+        # gloo has no reduce-scatter: a sharded bucket is all-reduced (its own shard is what the
+        # optimizer reads, exactly as after an in-place reduce-scatter)
         self.works[b] = self.comm.allreduce_(self.tensors[b], op="avg", async_op=True)
         self.launched[b] = True
 
@@ -136,19 +160,33 @@ class _PyReducer:
 class _NativeReducer:
     """ctypes front-end of the C++ reducer (csrc/runtime/rccl_comm.cpp)."""
 
-    def __init__(self, comm: RcclComm, ranges):
+    def __init__(self, comm: RcclComm, ranges, modes=None):
         self.comm = comm
         self.ranges = ranges
+        self.modes = modes or [0] * len(ranges)
         self.rt = native.runtime()
         self.h = self.rt.ddpx_reducer_create(comm.handle, len(ranges), NCCL_OP["avg"])
+        self._gkeep = {}
 
     def setup(self, grad_flat, expected):
         dt = NCCL_DTYPE[grad_flat.dtype]
         self._keep = grad_flat
         for b, (s, e) in enumerate(self.ranges):
             t = grad_flat[s:e]
-            native.check(self.rt.ddpx_reducer_set_bucket(self.h, b, t.data_ptr(), t.numel(), dt, expected[b]),
-                         "reducer_set_bucket")
+            native.check(self.rt.ddpx_reducer_set_bucket(self.h, b, t.data_ptr(), t.numel(), dt, expected[b],
+                                                         self.modes[b]), "reducer_set_bucket")
+
+    def set_gather(self, b, t):
+        self._gkeep[b] = t
+        native.check(self.rt.ddpx_reducer_set_gather(self.h, b, t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype]),
+                     "reducer_set_gather")
+
+    def gather(self, b):
+        native.check(self.rt.ddpx_reducer_gather(self.h, b, native.stream_handle()), "reducer_gather")
+
+    def wait_gather(self, b, stream=None):
+        native.check(self.rt.ddpx_reducer_wait_gather(self.h, b, native.stream_handle(stream)),
+                     "reducer_wait_gather")
 
     def prepare(self):
         self.rt.ddpx_reducer_prepare(self.h)
@@ -181,7 +219,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, comm: Comm | None = None,
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
-                 reduce_single: bool = False):
+                 reduce_single: bool = False, shard_optimizer: bool = False):
         super().__init__()
         self.module = module
         dev = next(module.parameters()).device
@@ -217,11 +255,18 @@ class DistributedDataParallel(nn.Module):
         self._broadcast_state()
 
         # Buckets: contiguous flat ranges over grad-ready order.
+        active = self.world_size > 1 or reduce_single  # reduce_single: exercise the reducer at ws=1 (tests)
+        self.sharded = bool(shard_optimizer and active)
         esz = self.flat.grad.element_size()
-        sizes = [n * esz for n in self.flat.numels]
         limits = [int(first_bucket_mb * 1024 * 1024), int(bucket_cap_mb * 1024 * 1024)]
-        assign = compute_bucket_assignment(sizes, limits)
+        if self.sharded:
+            assign, modes = self._shard_layout(limits, esz)
+        else:
+            sizes = [n * esz for n in self.flat.numels]
+            assign = compute_bucket_assignment(sizes, limits)
+            modes = [0] * len(assign)
         self.bucket_params = assign
+        self.bucket_modes = modes
         self.bucket_of = [0] * len(self.flat.params)
         ranges, expected = [], []
         for b, idxs in enumerate(assign):
@@ -230,13 +275,93 @@ class DistributedDataParallel(nn.Module):
             ranges.append(self.flat.span(idxs[0], idxs[-1]))
             expected.append(len(idxs))
         self.bucket_ranges = ranges
-        if self.world_size > 1 or reduce_single:  # reduce_single: exercise the reducer at ws=1 (tests)
-            self.reducer = _NativeReducer(comm, ranges) if isinstance(comm, RcclComm) else _PyReducer(comm, ranges)
+        if active:
+            cls = _NativeReducer if isinstance(comm, RcclComm) else _PyReducer
+            self.reducer = cls(comm, ranges, modes)
             self.reducer.setup(self.flat.grad, expected)
+            if self.sharded:
+                for b, (s0, e0) in enumerate(ranges):
+                    if modes[b] == 1:
+                        self.reducer.set_gather(b, self._gather_src[s0:e0])
         else:
             self.reducer = None
+        opt = getattr(self.flat, "optimizer", None)
+        if self.sharded and opt is not None:
+            self.attach_optimizer(opt)
         self.flat.sink = self
         self._completion_order = []
+
+    def _shard_layout(self, limits, esz):
+        """Re-pack the flat store for ZeRO-1 (see module docstring); returns (bucket params, modes)."""
+        f = self.flat
+        if f.shadow is not None and f.shadow_only:
+            S = [i for i, p in enumerate(f.params) if id(p) in f.shadow_only]
+            self.gather_what = "shadow"
+        else:
+            S = list(range(len(f.params)))
+            self.gather_what = "master"
+        R = [i for i in range(len(f.params)) if i not in set(S)]
+        groups = [[S[j] for j in g] for g in compute_bucket_assignment([f.numels[i] * esz for i in S], limits)]
+        modes = [1] * len(groups)
+        if R:
+            groups.append(R)  # fp32-read params: one replicated (all-reduced) bucket, produced last
+            modes.append(0)
+        f.relayout(groups, pad_to=self.world_size * ALIGN)
+        self._gather_src = f.shadow if self.gather_what == "shadow" else f.master
+        assign, k = [], 0
+        for g in groups:
+            assign.append(list(range(k, k + len(g))))
+            k += len(g)
+        return assign, modes
+
+    # ------------------------------------------------------- sharded optimizer
+    def bucket_order(self):
+        if self._overlap_pending:
+            order = list(self._completion_order)
+            return order + [b for b in range(len(self.bucket_ranges)) if b not in order]
+        return list(range(len(self.bucket_ranges)))
+
+    def wait_bucket(self, b):
+        self.reducer.wait_bucket(b)
+
+    def update_ranges(self, b):
+        s, e = self.bucket_ranges[b]
+        if self.bucket_modes[b] == 1:
+            c = (e - s) // self.world_size
+            return [(s + self.rank * c, s + (self.rank + 1) * c)]
+        return [(s, e)]
+
+    def gather_bucket(self, b):
+        if self.bucket_modes[b] == 1:
+            self.reducer.gather(b)
+
+    def _join_gathers(self):
+        for b, m in enumerate(self.bucket_modes):
+            if m == 1:
+                self.reducer.wait_gather(b)
+                if self.gather_what == "master" and self.flat.shadow is not None:
+                    from ..ops.elementwise import cast_bf16_
+                    s, e = self.bucket_ranges[b]
+                    cast_bf16_(self.flat.master[s:e], self.flat.shadow[s:e])
+
+    @torch.no_grad()
+    def consolidate(self):
+        """Collective: make fp32 master weights and optimizer state complete on every rank.
+
+        Needed before ``state_dict()`` / checkpointing when the optimizer is sharded (each rank
+        only keeps its own shards of master/momentum current).  No-op otherwise.
+        """
+        if not self.sharded:
+            return
+        tensors = [self.flat.master] + list(self.flat.state_tensors.values())
+        for b, (s, e) in enumerate(self.bucket_ranges):
+            if self.bucket_modes[b] != 1:
+                continue
+            for t in tensors:
+                full = t[s:e]
+                self.comm.allgather(full, full.chunk(self.world_size)[self.rank])
+        if self.flat.master.is_cuda:
+            torch.cuda.current_stream().synchronize()
 
     # ------------------------------------------------------------- state sync
     @torch.no_grad()
@@ -338,6 +463,8 @@ class DistributedDataParallel(nn.Module):
         self.reducer.wait_bucket(b)
 
     def optimizer_done(self):
+        if self.sharded:
+            self._join_gathers()
         self._overlap_pending = False
 
     def attach_optimizer(self, opt):

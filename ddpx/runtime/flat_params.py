@@ -81,6 +81,14 @@ class FlatParams:
         self.updated = [False] * len(self.params)  # parameter already stepped by a fused-optimizer epilogue
         self.fused_opt = None  # set by ddpx.optim.SGD(fused_backward=True)
         self.sink = None
+        self.optimizer = None  # the ddpx SGD that owns this store (set by SGD)
+        # params whose forward/backward read ONLY the bf16 shadow (never the fp32 master) —
+        # a sharded optimizer may then all-gather just the shadow for them
+        self.shadow_only = set()
+        # per-parameter optimizer state laid out like master (e.g. momentum), remapped by relayout()
+        self.state_tensors = {}
+        self.layout_version = 0
+        self.group_spans = None
         self._warned_unused = False
         self._hooks = []
         for p in self.params:
@@ -106,6 +114,62 @@ class FlatParams:
             return
         from ..ops.elementwise import cast_bf16_
         cast_bf16_(self.master, self.shadow)
+
+    def relayout(self, groups, pad_to: int = ALIGN):
+        """Re-pack the store as ``groups`` (lists of current param indices) in the given order.
+
+        Each group starts 64-element aligned and its length is padded to a multiple of ``pad_to``
+        (a sharded optimizer needs every bucket divisible into equal, aligned shards).  Values of
+        master, shadow and registered state tensors move with their parameters; gradients reset.
+        Returns the new [start, end) span of every group.
+        """
+        order = [i for g in groups for i in g]
+        if sorted(order) != list(range(len(self.params))):
+            raise ValueError("relayout groups must cover every parameter exactly once")
+        if pad_to % ALIGN:
+            raise ValueError("pad_to must be a multiple of the alignment")
+        new_params = [self.params[i] for i in order]
+        offsets, spans, off, k = [], [], 0, 0
+        for g in groups:
+            start = off
+            for _ in g:
+                p = new_params[k]
+                offsets.append(off)
+                off = _round_up(off + p.numel(), ALIGN)
+                k += 1
+            off = start + _round_up(max(off - start, pad_to), pad_to)
+            spans.append((start, off))
+        total = off
+        dev = self.device
+        master = torch.zeros(total, dtype=torch.float32, device=dev)
+        grad = torch.zeros(total, dtype=self.grad.dtype, device=dev)
+        shadow = torch.zeros(total, dtype=self.shadow.dtype, device=dev) if self.shadow is not None else None
+        states = {k_: torch.zeros(total, dtype=t.dtype, device=dev) for k_, t in self.state_tensors.items()}
+        with torch.no_grad():
+            for p, o in zip(new_params, offsets):
+                i_old = self.index[id(p)]
+                so, n = self.offsets[i_old], self.numels[i_old]
+                master[o:o + n].copy_(self.master[so:so + n])
+                for k_, t in self.state_tensors.items():
+                    states[k_][o:o + n].copy_(t[so:so + n])
+                view = master[o:o + n].view_as(p)
+                p.data = view
+                p.main_grad = grad[o:o + n].view(p.shape)
+                if shadow is not None:
+                    p._ddpx_shadow = shadow[o:o + n].view(p.shape)
+        self.params = new_params
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.offsets = offsets
+        self.numels = [p.numel() for p in self.params]
+        self.total = total
+        self.master, self.grad, self.shadow = master, grad, shadow
+        self.state_tensors = states
+        self.refresh_shadow()
+        self.written = [False] * len(self.params)
+        self.updated = [False] * len(self.params)
+        self.group_spans = spans
+        self.layout_version += 1
+        return spans
 
     # -- gradient protocol -----------------------------------------------------
     def grad_target(self, p):

@@ -105,7 +105,10 @@ def _declare_rt(lib):
     _sig(lib, "ddpx_comm_group_start", I)
     _sig(lib, "ddpx_comm_group_end", I)
     _sig(lib, "ddpx_reducer_create", P, P, I, I)
-    _sig(lib, "ddpx_reducer_set_bucket", I, P, I, P, S, I, I)
+    _sig(lib, "ddpx_reducer_set_bucket", I, P, I, P, S, I, I, I)
+    _sig(lib, "ddpx_reducer_set_gather", I, P, I, P, S, I)
+    _sig(lib, "ddpx_reducer_gather", I, P, I, P)
+    _sig(lib, "ddpx_reducer_wait_gather", I, P, I, P)
     _sig(lib, "ddpx_reducer_prepare", I, P)
     _sig(lib, "ddpx_reducer_mark_ready", I, P, I, I, P)
     _sig(lib, "ddpx_reducer_wait_bucket", I, P, I, P)

@@ -15,5 +15,7 @@ def prepare_model(model: nn.Module, device, grad_dtype=torch.float32) -> FlatPar
     if f is not None:
         return f
     spec = model.ddpx_spec(device) if hasattr(model, "ddpx_spec") else {}
-    return FlatParams(model, grad_dtype=grad_dtype, shadow_dtype=spec.get("shadow_dtype"),
-                      native_params=spec.get("native_params", ()))
+    f = FlatParams(model, grad_dtype=grad_dtype, shadow_dtype=spec.get("shadow_dtype"),
+                   native_params=spec.get("native_params", ()))
+    f.shadow_only = {id(p) for p in spec.get("shadow_only_params", ())}
+    return f

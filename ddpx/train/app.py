@@ -62,6 +62,8 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--no_fused_optimizer", action="store_true",
                    help="single GPU: run SGD as its own pass instead of inside the backward kernels")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
+    p.add_argument("--shard_optimizer", action="store_true",
+                   help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
     p.add_argument("--resume", action="store_true", help=f"resume from {FULL_CKPT_PATH}")
     p.add_argument("--full_checkpoint", action="store_true", help=f"also write {FULL_CKPT_PATH}")
@@ -149,7 +151,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
     if distributed:
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       first_bucket_mb=args.first_bucket_mb,
-                                      overlap_optimizer=args.overlap_optimizer)
+                                      overlap_optimizer=args.overlap_optimizer,
+                                      shard_optimizer=args.shard_optimizer)
         if args.overlap_optimizer:
             net.attach_optimizer(optimizer)
     metrics = MetricsWriter(args.metrics, rank) if args.metrics else None
@@ -164,6 +167,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
 
     start_time = time.time()
     trainer.train(args.total_epochs)
+    if isinstance(net, DistributedDataParallel):
+        net.consolidate()  # sharded optimizer: complete fp32 weights for eval / final state
     end_time = time.time()
     training_time = end_time - start_time
     print(f"Total training time: {training_time:.2f} seconds")

@@ -132,6 +132,8 @@ class Trainer:
     def train(self, max_epochs: int):
         for epoch in range(self.start_epoch, max_epochs):
             self._run_epoch(epoch)
+            if self.distributed and epoch % self.save_every == 0 and hasattr(self.model, "consolidate"):
+                self.model.consolidate()  # collective: sharded optimizer -> complete fp32 state on every rank
             if (not self.distributed or self.rank == 0) and epoch % self.save_every == 0:
                 self._save_checkpoint(epoch)
         if torch.cuda.is_available() and next(self.model.parameters()).is_cuda:

@@ -8,7 +8,7 @@ import torch.nn.functional as F
 from tests._dist_util import free_port, init_gloo
 
 
-def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps):
+def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False):
     import ddpx
     from ddpx.models import VGG, DeepNN
     from ddpx.optim.sgd import SGD
@@ -27,8 +27,10 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps):
         ref.load_state_dict(ours.state_dict())
         ddpx.prepare_model(ours, "cpu")
         d_ours = DistributedDataParallel(ours, comm=TorchComm(), bucket_cap_mb=bucket_mb, first_bucket_mb=0.25,
-                                         overlap_optimizer=overlap)
+                                         overlap_optimizer=overlap, shard_optimizer=shard)
         d_ref = TorchDDP(ref, bucket_cap_mb=bucket_mb)
+        if shard:
+            assert d_ours.sharded and all((e - s) % (ws * 64) == 0 for s, e in d_ours.bucket_ranges)
         o_ours = SGD(ours.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
         if overlap:
             d_ours.attach_optimizer(o_ours)
@@ -44,8 +46,13 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps):
                 opt.zero_grad()
                 F.cross_entropy(net(x), t).backward()
                 opt.step()
+        d_ours.consolidate()
         for (n, p), (_, q) in zip(ours.named_parameters(), ref.named_parameters()):
             assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), (rank, n, (p - q).abs().max().item())
+        # optimizer state (momentum) matches torch's after consolidation
+        so, sr = o_ours.state_dict()["state"], o_ref.state_dict()["state"]
+        for i in sr:
+            assert torch.allclose(so[i]["momentum_buffer"], sr[i]["momentum_buffer"], atol=2e-5, rtol=1e-4), i
         for (n, b), (_, c) in zip(ours.named_buffers(), ref.named_buffers()):
             assert torch.allclose(b.float(), c.float(), atol=2e-5, rtol=1e-4), (rank, n)
         # replicas identical across ranks
@@ -58,14 +65,16 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,model,overlap,bucket", [
-    (2, "deepnn", False, 25.0),
-    (2, "vgg", False, 25.0),
-    (2, "vgg", True, 4.0),
-    (4, "deepnn", True, 1.0),
+@pytest.mark.parametrize("ws,model,overlap,bucket,shard", [
+    (2, "deepnn", False, 25.0, False),
+    (2, "vgg", False, 25.0, False),
+    (2, "vgg", True, 4.0, False),
+    (4, "deepnn", True, 1.0, False),
+    (2, "vgg", False, 4.0, True),   # ZeRO-1: reduce-scatter + shard update + in-place all-gather
+    (4, "deepnn", True, 1.0, True),
 ])
-def test_ddp_matches_torch_ddp(ws, model, overlap, bucket):
-    mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3), nprocs=ws, join=True)
+def test_ddp_matches_torch_ddp(ws, model, overlap, bucket, shard):
+    mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3, shard), nprocs=ws, join=True)
 
 
 def _no_sync_worker(rank, ws, port):

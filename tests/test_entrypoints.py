@@ -42,7 +42,8 @@ def test_singlegpu_cpu_vgg_prints_and_checkpoint(tmp_path):
 def test_singlegpu_cpu_mlp_learns(tmp_path):
     out = _run([os.path.join(ROOT, "singlegpu.py"), "3", "5", "--model", "mlp", "--hidden", "128",
                 "--batch_size", "128", "--device", "cpu", "--data", "synthetic", "--train_size", "2048",
-                "--test_size", "512", "--steps_per_epoch", "auto", "--metrics", "m.jsonl", "--lr", "0.02"], tmp_path)
+                "--test_size", "512", "--steps_per_epoch", "auto", "--metrics", "m.jsonl", "--lr", "0.02",
+                "--seed", "0"], tmp_path)
     acc = float(re.search(r"accuracy=(\d+\.\d\d)%", out).group(1))
     assert acc > 30.0, out  # learnable synthetic data: well above chance (10%)
     assert (tmp_path / "m.jsonl").exists()
@@ -59,6 +60,19 @@ def test_multigpu_cpu_spawn(tmp_path):
     assert out.count("Total training time:") == 2  # every rank
     sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
     assert not any(k.startswith("module.") for k in sd)
+
+
+def test_multigpu_sharded_optimizer(tmp_path):
+    out = _run([os.path.join(ROOT, "multigpu.py"), "2", "1", "--batch_size", "32", "--device", "cpu",
+                "--nprocs", "2", "--model", "mlp", "--hidden", "64", "--data", "synthetic", "--train_size", "256",
+                "--test_size", "64", "--shard_optimizer", "--full_checkpoint", "--lr", "0.02"], tmp_path,
+               extra_env={"MASTER_PORT": str(free_port())})
+    assert "[GPU1] Epoch 1 | Batchsize: 32 | Steps: 4" in out
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    full = torch.load(tmp_path / "checkpoint_full.pt", weights_only=True)
+    for k, v in sd.items():
+        assert torch.isfinite(v.float()).all(), k
+    assert len(full["optimizer"]["state"]) == len(sd)
 
 
 def test_multigpu_torchrun(tmp_path):

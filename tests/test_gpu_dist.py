@@ -48,8 +48,8 @@ def test_rccl_collectives(gpu, pg):
     c.close()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_native_reducer_ddp_matches_plain(gpu, pg, overlap):
+@pytest.mark.parametrize("overlap,shard", [(False, False), (True, False), (False, True), (True, True)])
+def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard):
     import ddpx
     from ddpx.models import MLP
     from ddpx.optim.sgd import SGD
@@ -61,10 +61,13 @@ def test_native_reducer_ddp_matches_plain(gpu, pg, overlap):
     ddpx.prepare_model(a, gpu)
     ddpx.prepare_model(b, gpu)
     comm = RcclComm(gpu)
-    da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
-                                 overlap_optimizer=overlap)
-    assert len(da.bucket_ranges) >= 2
     oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
+                                 overlap_optimizer=overlap, shard_optimizer=shard)
+    assert len(da.bucket_ranges) >= 2
+    if shard:  # native MLP weights are shadow-only: reduce-scatter + bf16 shadow gather, biases replicated
+        assert da.sharded and da.gather_what == "shadow" and da.bucket_modes[-1] == 0
+        assert oa.bucket_source is da
     if overlap:
         da.attach_optimizer(oa)
     ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
@@ -83,7 +86,8 @@ def test_native_reducer_ddp_matches_plain(gpu, pg, overlap):
     comm.close()
 
 
-def test_graph_capture_with_rccl(gpu, pg):
+@pytest.mark.parametrize("shard", [False, True])
+def test_graph_capture_with_rccl(gpu, pg, shard):
     """Whole step (fwd, bwd with bucketed all-reduce on the comm stream, SGD) in one HIP graph."""
     import ddpx
     from ddpx.models import MLP
@@ -97,7 +101,8 @@ def test_graph_capture_with_rccl(gpu, pg):
     for m in (a, b):
         ddpx.prepare_model(m, gpu)
     comm = RcclComm(gpu)
-    da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True)
+    da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
+                                 shard_optimizer=shard)
     oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True)
     ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
     xs = [torch.rand(128, 3072, device=gpu).to(torch.bfloat16) for _ in range(4)]
