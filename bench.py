@@ -37,10 +37,12 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch_size", type=int, default=512, help="per-GPU batch")
-    p.add_argument("--hidden", type=int, default=4096)
+    p.add_argument("--hidden", type=int, default=None, help="MLP hidden width (default 4096 toy, 16384 wide)")
     p.add_argument("--layers", type=int, default=3)
     p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg"])
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
+    p.add_argument("--fp8", type=int, default=None,
+                   help="1: MX-FP8 hidden-layer forward/wgrad GEMMs (default 1 for --model mlp_wide)")
     p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--overlap_optimizer", type=int, default=None,
@@ -82,6 +84,11 @@ def setup_dist(n, impl):
     torch.cuda.set_device(local)
     if world > 1 or (n == 1 and "--ddp_single" in sys.argv):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         # ddpx: GPU collectives go through its own RCCL communicator; the c10d group only
         # bootstraps it (TCPStore) and carries CPU barriers/timing -> gloo.  torch: stock RCCL PG.
         dist.init_process_group(backend="gloo" if impl == "ddpx" else "nccl", rank=rank, world_size=world)
@@ -102,6 +109,10 @@ def make_data(args, device, rank, world, layout=None):
 
 
 def resolve_defaults(args, world):
+    if args.hidden is None:
+        args.hidden = 16384 if args.model == "mlp_wide" else 4096
+    if args.fp8 is None:
+        args.fp8 = int(args.model == "mlp_wide" and args.impl == "ddpx")
     multi = world > 1 or args.ddp_single
     if args.grad_dtype == "auto":
         args.grad_dtype = "bf16" if multi else "fp32"
@@ -119,7 +130,8 @@ def build_ddpx(args, device, world):
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
-    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16", device=device)
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16", device=device,
+                        fp8=bool(args.fp8))
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update is fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
@@ -250,13 +262,13 @@ def main():
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
-    model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}", "mlp_wide": f"wide-mlp-3072x{args.hidden}",
+    model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}", "mlp_wide": f"wide-mlp-3072x{args.hidden}x{args.layers}",
                   "vgg": "vgg11-cifar"}[args.model]
     base = baseline_value(f"{args.model}_x{world}") if args.impl == "ddpx" else None
     rec = {
         "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16" if (args.model != "vgg" or args.impl == "ddpx" or args.torch_amp) else "fp32",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": ("mxfp8/bf16" if args.fp8 else "bf16") if (args.model != "vgg" or args.impl == "ddpx" or args.torch_amp) else "fp32",
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),

@@ -178,12 +178,12 @@ __device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t of
     stored = v * p.alpha + cin;
   } else if constexpr (E == EPI_BF16 || E == EPI_BNSTAT_BF16) {
     stored = bf2f(f2bf(v * p.alpha + cin));
-  } else if constexpr (E == EPI_BIAS_BF16) {
-    stored = bf2f(f2bf(v + p.bias[n]));
+  } else if constexpr (E == EPI_BIAS_BF16) {  // alpha: dequant scale of the fp8 GEMMs (1 for bf16)
+    stored = bf2f(f2bf(fmaf(v, p.alpha, p.bias[n])));
   } else if constexpr (E == EPI_BIAS_RELU_BF16) {
-    stored = bf2f(f2bf(fmaxf(v + p.bias[n], 0.f)));
+    stored = bf2f(f2bf(fmaxf(fmaf(v, p.alpha, p.bias[n]), 0.f)));
   } else if constexpr (E == EPI_BIAS_F32) {
-    stored = v + p.bias[n];
+    stored = fmaf(v, p.alpha, p.bias[n]);
   } else if constexpr (E == EPI_SGD) {
     stored = v * p.alpha;
     float d = fmaf(p.sgd.wd, pv, stored);
@@ -194,7 +194,7 @@ __device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t of
     *p_out = fmaf(-lr, d, pv);
   } else {  // EPI_RELUMASK_BF16
     const bool pos = (auxv & 0x8000u) == 0 && (auxv & 0x7fffu) != 0;
-    stored = pos ? bf2f(f2bf(v)) : 0.f;
+    stored = pos ? bf2f(f2bf(v * p.alpha)) : 0.f;
   }
   return stored;
 }

@@ -10,7 +10,8 @@ from .vgg import VGG
 __all__ = ["VGG", "DeepNN", "MLP", "build_model"]
 
 
-def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "native"):
+def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "native",
+                fp8: bool = False):
     dev = torch.device(device) if device is not None else torch.device("cpu")
     if dtype == "auto":
         dtype = "bf16" if dev.type == "cuda" else "fp32"
@@ -25,6 +26,7 @@ def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", de
         h = hidden or (16384 if name == "mlp_wide" else 4096)
         m = MLP(hidden=h, layers=layers, compute_dtype=cdt)
         m.use_native = kernels == "native"
+        m.fp8 = bool(fp8)  # MX-FP8 forward / weight-gradient GEMMs on the native path
     else:
         raise ValueError(f"unknown model {name!r}")
     return m

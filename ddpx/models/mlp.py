@@ -38,6 +38,7 @@ class MLP(nn.Module):
         self.num_classes = num_classes
         self.compute_dtype = compute_dtype
         self.use_native = True
+        self.fp8 = False  # MX-FP8 hidden-layer GEMMs (ddpx.ops.mlp), wide-MLP config
 
     def linears(self):
         return [getattr(self, f"fc{i}") for i in range(self.num_layers)]

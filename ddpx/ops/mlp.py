@@ -11,6 +11,12 @@ its DDP bucket slice, then announced to the reducer):
       (db_{l-1} = Σ_m dpre_{l-1} from the dgrad epilogue's per-tile column sums)
 The weight gradient of a layer is issued BEFORE its data gradient so the
 bucket holding it starts its all-reduce while the next GEMMs run.
+
+``model.fp8`` (the wide-MLP config, BASELINE.json configs[4]): the hidden layers' forward and
+weight-gradient GEMMs run on MX-FP8 (``ddpx.ops.fp8``: e4m3 activations/weights, e5m2 output
+gradients, E8M0 block-32 scales applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4``); the
+forward quantises each input both row-wise (its GEMM) and transposed (the later wgrad's B operand).
+The data-gradient GEMM stays bf16.  Master weights, gradients and SGD are unchanged (fp32).
 """
 from __future__ import annotations
 
@@ -33,19 +39,54 @@ def _params(model):
     return [(lin.weight, lin.bias) for lin in lins]
 
 
-def _forward(model, x, targets, want_logits, want_grad):
+def _fp8_ok(model, x):
+    if not getattr(model, "fp8", False):
+        return False
+    B = x.shape[0]
+    return B % 128 == 0 and all(w.shape[1] % 128 == 0 for w, _ in _params(model)[:-1])
+
+
+def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
     flat = model.fc0.weight._ddpx_flat
     ps = _params(model)
     hs = [x]
+    fp8 = _fp8_ok(model, x)
+    if for_backward is None:
+        for_backward = want_grad
+    saved8 = [] if (fp8 and for_backward) else None
     for (w, b) in ps[:-1]:
-        hs.append(G.linear_fwd(hs[-1], flat.shadow_of(w), b, relu=True))
+        if fp8:
+            from . import fp8 as F8
+            if for_backward:
+                hq, hqt = F8.quant(hs[-1], F8.E4M3, rows=True, cols=True)
+                saved8.append(hqt)
+            else:
+                hq = F8.quant(hs[-1], F8.E4M3)
+            wq = F8.quant(flat.shadow_of(w), F8.E4M3)
+            hs.append(F8.gemm(hq, wq, epi=G.EPI_BIAS_RELU_BF16, bias=b))
+        else:
+            hs.append(G.linear_fwd(hs[-1], flat.shadow_of(w), b, relu=True))
     wl, bl = ps[-1]
     loss, logits, dl = head_forward(hs[-1], flat.shadow_of(wl), bl, targets, want_logits=want_logits,
                                     want_grad=want_grad)
-    return hs, loss, logits, dl
+    return hs, loss, logits, dl, saved8
 
 
-def _backward(model, hs, dl, grad_out):
+def _wgrad(saved, l, dpre, h, out, accumulate=False, sgd=None):
+    """dW_l = dpreᵀ h — MX-FP8 when the forward saved hᵀ in fp8, else the bf16 pipe."""
+    if saved:
+        from . import fp8 as F8
+        dq = F8.quant(dpre, F8.E5M2, rows=False, cols=True)  # dpreᵀ [out][batch]
+        if sgd is not None:
+            return F8.gemm(dq, saved[l], epi=G.EPI_SGD, sgd=sgd)
+        epi = G.EPI_F32 if out.dtype == torch.float32 else G.EPI_BF16
+        return F8.gemm(dq, saved[l], out=out, epi=epi, accumulate=accumulate)
+    if sgd is not None:
+        return G.linear_wgrad(dpre, h, None, sgd=sgd)
+    return G.linear_wgrad(dpre, h, out, accumulate=accumulate)
+
+
+def _backward(model, hs, dl, grad_out, saved8=None):
     flat = model.fc0.weight._ddpx_flat
     ps = _params(model)
     L = len(ps) - 1  # number of hidden layers
@@ -67,7 +108,7 @@ def _backward(model, hs, dl, grad_out):
                 bp = ps[l - 1][1]
                 dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
                 flat.mark_updated(bp)
-            G.linear_wgrad(dpre, hs[l], None, sgd=flat.fused_spec(w))
+            _wgrad(saved8, l, dpre, hs[l], None, sgd=flat.fused_spec(w))
             flat.mark_updated(w)
             dpre = dnext
         return
@@ -84,7 +125,7 @@ def _backward(model, hs, dl, grad_out):
     for l in range(L - 1, -1, -1):
         w, _ = ps[l]
         dWl, accw = flat.grad_target(w)
-        G.linear_wgrad(dpre, hs[l], dWl, accumulate=accw)
+        _wgrad(saved8, l, dpre, hs[l], dWl, accumulate=accw)
         flat.grad_done(w)
         if l > 0:
             bp = ps[l - 1][1]
@@ -99,33 +140,35 @@ def _backward(model, hs, dl, grad_out):
 class _MLPLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, targets, model, *weights):
-        hs, loss, _, dl = _forward(model, x, targets, want_logits=False, want_grad=True)
+        hs, loss, _, dl, saved8 = _forward(model, x, targets, want_logits=False, want_grad=True)
         ctx.model = model
         ctx.hs = hs
         ctx.dl = dl
+        ctx.saved8 = saved8
         ctx.n_in = len(weights)
         return loss
 
     @staticmethod
     def backward(ctx, grad_loss):
-        _backward(ctx.model, ctx.hs, ctx.dl, grad_loss)
-        ctx.hs = ctx.dl = None
+        _backward(ctx.model, ctx.hs, ctx.dl, grad_loss, ctx.saved8)
+        ctx.hs = ctx.dl = ctx.saved8 = None
         return (None, None, None) + (None,) * ctx.n_in
 
 
 class _MLPLogits(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, model, *weights):
-        hs, _, logits, _ = _forward(model, x, None, want_logits=True, want_grad=False)
+        hs, _, logits, _, saved8 = _forward(model, x, None, want_logits=True, want_grad=False, for_backward=True)
         ctx.model = model
         ctx.hs = hs
+        ctx.saved8 = saved8
         ctx.n_in = len(weights)
         return logits
 
     @staticmethod
     def backward(ctx, grad_logits):
-        _backward(ctx.model, ctx.hs, grad_logits.float().contiguous(), None)
-        ctx.hs = None
+        _backward(ctx.model, ctx.hs, grad_logits.float().contiguous(), None, ctx.saved8)
+        ctx.hs = ctx.saved8 = None
         return (None, None) + (None,) * ctx.n_in
 
 
@@ -143,6 +186,6 @@ def mlp_loss(model, x, targets):
 def mlp_logits(model, x):
     x = _to_bf16_2d(x)
     if not torch.is_grad_enabled():
-        _, _, logits, _ = _forward(model, x, None, want_logits=True, want_grad=False)
+        _, _, logits, _, _ = _forward(model, x, None, want_logits=True, want_grad=False)
         return logits
     return _MLPLogits.apply(x, model, *_weights(model))
