@@ -20,17 +20,20 @@ from ddpx.ops import gemm as G
 from ddpx.ops.elementwise import sgd_flat_
 
 
-def timeit(fn, reps=20):
+def timeit(fn, reps=20, inner=10):
+    """Median over reps of (time of `inner` back-to-back calls) / inner, in µs: back-to-back launches
+    keep the GPU busy, so host launch overhead does not inflate short kernels."""
     for _ in range(3):
         fn()
     ts = []
     for _ in range(reps):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        fn()
+        for _ in range(inner):
+            fn()
         e.record()
         e.synchronize()
-        ts.append(s.elapsed_time(e) * 1000)
+        ts.append(s.elapsed_time(e) * 1000 / inner)
     ts.sort()
     return round(ts[len(ts) // 2], 2)
 
@@ -66,7 +69,7 @@ def main():
         o32 = torch.empty(N, K, device=dev)
         o16 = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
         row = {}
-        for tile in range(8):
+        for tile in range(9):
             try:
                 row[f"f32_t{tile}"] = timeit(lambda: G.linear_wgrad(dy, x, o32, tile=tile))
                 row[f"bf16_t{tile}"] = timeit(lambda: G.linear_wgrad(dy, x, o16, tile=tile))

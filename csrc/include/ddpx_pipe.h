@@ -106,14 +106,16 @@ __device__ __forceinline__ unsigned src_off(const ConvGeom& g, int ld, int row, 
   }
 }
 
-// Stage one ROWS x 64 operand tile into an LDS slot with LDS-DMA.
-template <int ROWS, bool KC, int MODE>
+// Stage one ROWS x 64 operand tile into an LDS slot with LDS-DMA (ROWS/8 wave-instructions of 1 KiB,
+// spread over NW waves).
+template <int ROWS, bool KC, int MODE, int NW = 4>
 __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rs, char* slot, const ConvGeom& g, int ld, int row0,
                                            int nrows, int k0, int kend, int wave, int lane) {
-  constexpr int NI = ROWS / 32;
+  constexpr int NI = ROWS / (8 * NW);
+  static_assert(NI * 8 * NW == ROWS, "tile rows must split evenly over the waves");
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int inst = j * 4 + wave;
+    const int inst = j * NW + wave;
     if constexpr (KC) {
       const int r = inst * 8 + (lane >> 3);
       const int pch = lane & 7;
@@ -199,11 +201,11 @@ __device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t of
   return stored;
 }
 
-template <int E, int BM, int BN>
+template <int E, int BM, int BN, int NT = 256>
 __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const float* T, int m0, int n0, int tid,
                                              float (&csum)[4]) {
   constexpr int Q = BN / 4;           // column quads per row
-  constexpr int RSTEP = 256 / Q;      // rows between a thread's consecutive vectors
+  constexpr int RSTEP = NT / Q;       // rows between a thread's consecutive vectors
   constexpr int NV = BM / RSTEP;      // vectors per thread
   constexpr int TLD = BN + 4;
   const int cq = tid % Q, r0 = tid / Q;
@@ -302,9 +304,9 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
 }
 
 // Column reductions of the stored tile: thread (cq, r0) holds partial sums of 4 columns.
-template <int BN>
+template <int BN, int NT = 256>
 __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], int tid, float* out /* BN */) {
-  constexpr int Q = BN / 4, RG = 256 / Q;
+  constexpr int Q = BN / 4, RG = NT / Q;
   const int cq = tid % Q, rg = tid / Q;
 #pragma unroll
   for (int q = 0; q < 4; ++q) red[rg * BN + 4 * cq + q] = cs[q];
@@ -317,19 +319,22 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
   __syncthreads();
 }
 
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE>
-__global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
+// NW = 4: 2x2 waves; NW = 8: 4 (M) x 2 (N) waves.  Wave tile (BM/WGM) x (BN/2).
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
+  constexpr int NT = NW * 64;
+  constexpr int WGM = NW / 2;
   constexpr int BK = 64;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int SLOT = A_BYTES + B_BYTES;
-  constexpr int FM = BM / 32, FN = BN / 32;
-  constexpr int LPW = BM / 32 + BN / 32;  // DMA instructions per wave per stage
+  constexpr int FM = BM / WGM / 16, FN = BN / 32;
+  constexpr int LPW = (BM + BN) / (8 * NW);  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave >> 1, wn = wave & 1;  // wm in [0, WGM)
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -357,8 +362,8 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
   auto issue = [&](int t) {
     char* slot = smem + (t % STAGES) * SLOT;
     const int k0 = kbeg + t * BK;
-    stage_tile<BM, AK, AMODE>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
-    stage_tile<BN, BKc, BMODE>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+    stage_tile<BM, AK, AMODE, NW>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+    stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
   };
 
 #pragma unroll
@@ -380,7 +385,7 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / 2) + i * 16, kk, lane);
+      for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / WGM) + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) b[j] = frag<BN, BKc>(sb, wn * (BN / 2) + j * 16, kk, lane);
 #pragma unroll
@@ -394,10 +399,10 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
   // ---- stage the accumulator tile through LDS (all DMA has landed: last wait was vmcnt(0)) ----
   constexpr int TLD = BN + 4;
   float* T = reinterpret_cast<float*>(smem);
-  static_assert(BM * TLD * 4 + (256 / (BN / 4) + 2) * BN * 4 <= STAGES * SLOT, "epilogue LDS overflow");
+  static_assert(BM * TLD * 4 + (NT / (BN / 4) + 2) * BN * 4 <= STAGES * SLOT, "epilogue LDS overflow");
   __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
   {
-    const int mr = wm * (BM / 2) + 4 * (lane >> 4);
+    const int mr = wm * (BM / WGM) + 4 * (lane >> 4);
     const int nc = wn * (BN / 2) + (lane & 15);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -409,23 +414,23 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
   __syncthreads();
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   switch (p.epi) {
-    case EPI_F32: epilogue_vec<EPI_F32, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BF16: epilogue_vec<EPI_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_SGD: epilogue_vec<EPI_SGD, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
-    default: epilogue_vec<EPI_RELUMASK_BF16, BM, BN>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_F32: epilogue_vec<EPI_F32, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BF16: epilogue_vec<EPI_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_SGD: epilogue_vec<EPI_SGD, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    default: epilogue_vec<EPI_RELUMASK_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
   }
   if (!p.colsum) return;
 
   // ---- per-tile column reductions (bias gradient / BatchNorm statistics) ----
-  // scratch after the tile image: [256/(BN/4)][BN] partials + [BN] results
+  // scratch after the tile image: [NT/(BN/4)][BN] partials + [BN] results
   float* red = T + BM * TLD;
-  float* colres = red + (256 / (BN / 4)) * BN;
+  float* colres = red + (NT / (BN / 4)) * BN;
   __syncthreads();
-  quad_colsum<BN>(red, cs, tid, colres);
+  quad_colsum<BN, NT>(red, cs, tid, colres);
   if (p.epi != EPI_BNSTAT_BF16) {
     if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
     return;
@@ -436,7 +441,7 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
   if (tid < BN) tmean[tid] = colres[tid] / (float)rows_valid;
   __syncthreads();
   {
-    constexpr int Q = BN / 4, RSTEP = 256 / Q, NV = BM / RSTEP;
+    constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BM / RSTEP;
     const int cq = tid % Q, r0 = tid / Q;
     float m2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -450,7 +455,7 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
         m2[q] += d * d;
       }
     }
-    quad_colsum<BN>(red, m2, tid, colres);
+    quad_colsum<BN, NT>(red, m2, tid, colres);
   }
   if (tid < BN && n0 + tid < p.N) {
     p.colsum[((size_t)tm * 2) * p.N + n0 + tid] = tmean[tid];
@@ -458,23 +463,26 @@ __global__ void __launch_bounds__(256) gemm_pipe_kernel(Params p) {
   }
 }
 
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE>
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4>
 static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE>), dim3(tiles, splits), dim3(256), 0, s,
-                     p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW>), dim3(tiles, splits),
+                     dim3(NW * 64), 0, s, p);
   return hipGetLastError();
 }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {
-  static const int t[8][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64}, {64, 64}};
-  *bm = t[cfg & 7][0];
-  *bn = t[cfg & 7][1];
+  static const int t[9][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128},
+                              {64, 128},  {128, 64}, {64, 64},  {256, 128}};
+  const int c = (cfg >= 0 && cfg <= 8) ? cfg : 7;
+  *bm = t[c][0];
+  *bn = t[c][1];
 }
 
 template <bool AK, bool BKc, int AMODE, int BMODE>
 static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) {
   switch (cfg) {
+    case 8: return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8>(p, splits, s);  // 8 waves, 144 KiB LDS
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
     case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB

@@ -16,9 +16,11 @@
 // STAGES-deep LDS-DMA ring with counted vmcnt waits; one stage = 128 K-bytes = one MFMA K-step.
 // The fp8 tile rows are 128 B, byte-identical to the bf16 pipe's [row][64 x bf16] images, so the
 // same staging code and XOR swizzle serve both.  Each wave additionally DMAs 256 B of scales per
-// stage (waves 0/1: A rows, 2/3: B rows; 4 E8M0 bytes per row per stage).  Lane l of an MFMA holds
-// row l&15, K-bytes [32(l>>4), 32(l>>4)+32) of the stage, i.e. exactly one scale block, and feeds
-// that block's scale byte (opsel 0).  Epilogues are the bf16 pipe's (bias/ReLU/bf16/f32/SGD).
+// stage (waves 0/1: A rows, 2/3: B rows; 4 E8M0 bytes per row per stage).  Operand map of the
+// scaled MFMA (measured on MI355X with per-block scales, tools/mx_probe.py): lane l holds row l&15,
+// its bytes 0-15 are K [16g, 16g+16) and bytes 16-31 are K [64+16g, 64+16g+16) (g = l>>4), and the
+// scale byte lane-group g supplies (opsel 0) applies to K-block g = [32g, 32g+32) — so a block's
+// data sits in two lane groups.  Epilogues are the bf16 pipe's (bias/ReLU/bf16/f32/SGD).
 #include "ddpx_pipe.h"
 
 namespace ddpx {
@@ -136,8 +138,12 @@ __global__ void probe_kernel(const unsigned char* A, const unsigned char* B, con
                              const unsigned char* sb, float* C) {
   const int l = threadIdx.x;
   const int row = l & 15, g = l >> 4;
-  const i32x8 a = *reinterpret_cast<const i32x8*>(A + row * 128 + 32 * g);
-  const i32x8 b = *reinterpret_cast<const i32x8*>(B + row * 128 + 32 * g);
+  const u32x4 alo = *reinterpret_cast<const u32x4*>(A + row * 128 + 16 * g);
+  const u32x4 ahi = *reinterpret_cast<const u32x4*>(A + row * 128 + 64 + 16 * g);
+  const u32x4 blo = *reinterpret_cast<const u32x4*>(B + row * 128 + 16 * g);
+  const u32x4 bhi = *reinterpret_cast<const u32x4*>(B + row * 128 + 64 + 16 * g);
+  const i32x8 a = {(int)alo[0], (int)alo[1], (int)alo[2], (int)alo[3], (int)ahi[0], (int)ahi[1], (int)ahi[2], (int)ahi[3]};
+  const i32x8 b = {(int)blo[0], (int)blo[1], (int)blo[2], (int)blo[3], (int)bhi[0], (int)bhi[1], (int)bhi[2], (int)bhi[3]};
   const int xa = sa[row * 4 + g], xb = sb[row * 4 + g];
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, FA, FB, 0, xa, 0, xb);
@@ -226,8 +232,8 @@ __global__ void __launch_bounds__(256) gemm_mx8_kernel(MxParams mp) {
     for (int i = 0; i < FM; ++i) {
       const int row = wm * 64 + i * 16 + (lane & 15);
       const int sw = (row >> 1) & 7;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(sa + row * 128 + (((2 * g) ^ sw) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(sa + row * 128 + (((2 * g + 1) ^ sw) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(sa + row * 128 + ((g ^ sw) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(sa + row * 128 + (((g + 4) ^ sw) << 4));
       a[i] = (i32x8){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
       xa[i] = ss[row * 4 + g];
     }
@@ -235,8 +241,8 @@ __global__ void __launch_bounds__(256) gemm_mx8_kernel(MxParams mp) {
     for (int j = 0; j < FN; ++j) {
       const int row = wn * 64 + j * 16 + (lane & 15);
       const int sw = (row >> 1) & 7;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(sb + row * 128 + (((2 * g) ^ sw) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(sb + row * 128 + (((2 * g + 1) ^ sw) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(sb + row * 128 + ((g ^ sw) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(sb + row * 128 + (((g + 4) ^ sw) << 4));
       b[j] = (i32x8){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
       xb[j] = ss[BM * 4 + row * 4 + g];
     }

@@ -23,6 +23,10 @@ from ..runtime import native
 
 # "pipe" (LDS-DMA multi-stage ring, default) or "v1" (register-staged, 2 LDS buffers)
 GEMM_IMPL = os.environ.get("DDPX_GEMM", "pipe")
+# split-K on the 8-wave 256x128 tile for the M=512-row products (forward / dgrad).  Off by default:
+# on MI355X the partial-slab round trip (S x 8 MiB fp32) costs more than the larger tile saves for the
+# toy MLP (bench: 0.352 vs 0.295 ms/step, profiles/r1_gemm); DDPX_SPLITK=1 enables it.
+SPLITK = os.environ.get("DDPX_SPLITK", "0") == "1"
 
 EPI_F32 = 0
 EPI_BF16 = 1
@@ -56,11 +60,31 @@ def _check_bf16_2d(t, name):
     _req(t.data_ptr() % 16 == 0, f"{name} must be 16-byte aligned")
 
 
+def splitk_plan(M, N, K, a_kcontig, b_kcontig, tile=-1, impl=None, epi=None):
+    """(splits, scratch_floats, colsum_rows) — splits == 1 means the regular single-pass kernel."""
+    if not SPLITK or tile != -1 or (impl or GEMM_IMPL) != "pipe" or epi == EPI_SGD or N % 4:
+        return 1, 0, 0
+    sf = native.c_int64(0)
+    rows = native.c_int(0)
+    s = native.kernels().ddpx_gemm_splitk_plan(M, N, K, int(a_kcontig), int(b_kcontig), native.ctypes.byref(sf),
+                                               native.ctypes.byref(rows))
+    return s, sf.value, rows.value
+
+
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
              accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None):
     lib = native.kernels()
     impl = impl or GEMM_IMPL
     s = native.stream_handle(stream)
+    splits, sfl, _ = splitk_plan(M, N, K, a_kcontig, b_kcontig, tile, impl, epi) if sgd is None else (1, 0, 0)
+    if splits > 1 and ldc % 4 == 0:
+        scratch = torch.empty(sfl, dtype=torch.float32, device=a.device)
+        rc = lib.ddpx_gemm_pipe_splitk(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
+                                       native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig),
+                                       int(b_kcontig), epi, int(accumulate), float(alpha), splits, scratch.data_ptr(),
+                                       s)
+        native.check(rc, f"ddpx_gemm_pipe_splitk(M={M},N={N},K={K},epi={epi},splits={splits})")
+        return c
     if impl == "v1":
         if colsum is not None or sgd is not None:
             raise ValueError("v1 GEMM has no fused column sum / optimizer epilogue")
@@ -76,6 +100,10 @@ def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias
 
 
 def tiles_m(M, N, K, a_kcontig, b_kcontig, tile=-1):
+    """Rows of per-tile column-sum partials the kernel chosen for this shape writes."""
+    splits, _, rows = splitk_plan(M, N, K, a_kcontig, b_kcontig, tile)
+    if splits > 1:
+        return rows
     return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, K, int(a_kcontig), int(b_kcontig), tile)
 
 

@@ -13,7 +13,7 @@ The weight gradient of a layer is issued BEFORE its data gradient so the
 bucket holding it starts its all-reduce while the next GEMMs run.
 
 ``model.fp8`` (the wide-MLP config, BASELINE.json configs[4]): the hidden layers' forward and
-weight-gradient GEMMs run on MX-FP8 (``ddpx.ops.fp8``: e4m3 activations/weights, e5m2 output
+weight-gradient GEMMs run on MX-FP8 (``ddpx.ops.fp8``: e4m3 activations, weights and output
 gradients, E8M0 block-32 scales applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4``); the
 forward quantises each input both row-wise (its GEMM) and transposed (the later wgrad's B operand).
 The data-gradient GEMM stays bf16.  Master weights, gradients and SGD are unchanged (fp32).
@@ -76,7 +76,9 @@ def _wgrad(saved, l, dpre, h, out, accumulate=False, sgd=None):
     """dW_l = dpreᵀ h — MX-FP8 when the forward saved hᵀ in fp8, else the bf16 pipe."""
     if saved:
         from . import fp8 as F8
-        dq = F8.quant(dpre, F8.E5M2, rows=False, cols=True)  # dpreᵀ [out][batch]
+        # output gradients in e4m3 too: with per-32-element E8M0 block scales the range is covered
+        # by the scale, and e4m3's extra mantissa bit halves the wgrad error vs e5m2
+        dq = F8.quant(dpre, F8.E4M3, rows=False, cols=True)  # dpreᵀ [out][batch]
         if sgd is not None:
             return F8.gemm(dq, saved[l], epi=G.EPI_SGD, sgd=sgd)
         epi = G.EPI_F32 if out.dtype == torch.float32 else G.EPI_BF16

@@ -40,6 +40,7 @@ MI355X-specific design:
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -288,6 +289,13 @@ class DistributedDataParallel(nn.Module):
         opt = getattr(self.flat, "optimizer", None)
         if self.sharded and opt is not None:
             self.attach_optimizer(opt)
+        # every rank must agree on the bucket layout (a mismatch would pair wrong slices in RCCL)
+        if verify and self.world_size > 1:
+            layout = [tuple(r) for r in self.bucket_ranges], list(self.bucket_modes)
+            for r, other in enumerate(comm.all_gather_object(layout)):
+                if other != layout:
+                    raise RuntimeError(f"DDP: bucket layout differs between rank {self.rank} and rank {r}")
+        self.debug = os.environ.get("DDPX_DEBUG", "0") == "1"
         self.flat.sink = self
         self._completion_order = []
 
@@ -435,6 +443,13 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         if self.reducer is None:
             return
+        if self.debug and self.world_size > 1:
+            # TORCH_DISTRIBUTED_DEBUG=DETAIL-style check: identical bucket completion order on every rank
+            order = list(self._completion_order)
+            for r, other in enumerate(self.comm.all_gather_object(order)):
+                if other != order:
+                    raise RuntimeError(f"DDP debug: bucket completion order {order} on rank {self.rank} "
+                                       f"!= {other} on rank {r}")
         if self.overlap_optimizer:
             self._overlap_pending = True
             # launch stragglers but do not join: the optimizer waits per bucket

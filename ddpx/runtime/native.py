@@ -52,6 +52,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_scale_f32", I, P, I64, F, P)
     _sig(lib, "ddpx_gemm_pipe", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_gemm_pipe_tiles_m", I, I, I, I, I, I, I)
+    _sig(lib, "ddpx_gemm_splitk_plan", I, I, I, I, I, I, ctypes.POINTER(c_int64), ctypes.POINTER(c_int))
+    _sig(lib, "ddpx_gemm_pipe_splitk", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P)
     _sig(lib, "ddpx_mx8_quant", I, P, I, I, I, P, I, P, P, I, P, I, P)
     _sig(lib, "ddpx_mx8_probe", I, P, P, P, P, P, I, I, P)
     _sig(lib, "ddpx_gemm_mx8", I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, P, P, P, P, F, F, P)

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import argparse
 import os
+import subprocess
+import sys
 import time
 
 import torch
@@ -71,7 +73,54 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--eval_batch", type=int, default=512)
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--nprocs", type=int, default=None, help="multigpu: processes to spawn (default: #GPUs)")
+    p.add_argument("--fp8", action="store_true", help="MLP: MX-FP8 hidden-layer forward / weight-gradient GEMMs")
+    p.add_argument("--profile", default=None, metavar="DIR",
+                   help="re-run this command under rocprofv3 --kernel-trace --stats, output in DIR")
+    p.add_argument("--debug", action="store_true",
+                   help="serialised kernels (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1) and DDP "
+                        "bucket-order validation across ranks on every step")
+    p.add_argument("--fault_step", type=int, default=None,
+                   help="fault injection: rank --fault_rank raises at this global step")
+    p.add_argument("--fault_rank", type=int, default=0)
     return p
+
+
+def maybe_profile(args, argv=None) -> None:
+    """``--profile DIR``: run this same command as a CHILD under rocprofv3 and exit with its code.
+
+    Done before anything touches the GPU (rocprofv3's library initialises it in the child; this
+    process never does), per SURVEY §5.1.  Output: DIR/<pid>/..._kernel_stats.csv etc.
+    """
+    if not getattr(args, "profile", None):
+        return
+    argv = list(sys.argv if argv is None else argv)
+    rest, skip = [], False
+    for a in argv[1:]:
+        if skip:
+            skip = False
+            continue
+        if a == "--profile":
+            skip = True
+            continue
+        if a.startswith("--profile="):
+            continue
+        rest.append(a)
+    out = os.path.abspath(args.profile)
+    os.makedirs(out, exist_ok=True)
+    cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", out, "--", sys.executable,
+           os.path.abspath(argv[0]), *rest]
+    env = dict(os.environ, TMPDIR="/tmp")
+    print("profiling:", " ".join(cmd), flush=True)
+    rc = subprocess.run(cmd, env=env).returncode
+    sys.exit(rc)
+
+
+def apply_debug_env(args) -> None:
+    """``--debug``: kernel serialisation for fault localisation (must precede GPU initialisation)."""
+    if getattr(args, "debug", False):
+        os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+        os.environ.setdefault("HIP_LAUNCH_BLOCKING", "1")
+        os.environ.setdefault("DDPX_DEBUG", "1")
 
 
 def resolve_device(args, local_rank: int = 0) -> torch.device:
@@ -108,7 +157,7 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
     if args.seed is not None:
         torch.manual_seed(args.seed)
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
-                        kernels=args.kernels)
+                        kernels=args.kernels, fp8=getattr(args, "fp8", False))
     if getattr(args, "sync_bn", False) and distributed:
         if hasattr(model, "use_native"):
             model.use_native = False
@@ -159,6 +208,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
     trainer = Trainer(net, train_data, optimizer, local_rank if device.type == "cuda" else rank, args.save_every,
                       scheduler, distributed=distributed, rank=rank, graph=args.graph, metrics=metrics,
                       full_checkpoint=args.full_checkpoint)
+    if args.fault_step is not None and rank == args.fault_rank:
+        trainer.fault_step = args.fault_step
     if args.resume and os.path.exists(FULL_CKPT_PATH):
         trainer.start_epoch = load_full_checkpoint(FULL_CKPT_PATH, model, optimizer, scheduler,
                                                    map_location=device)

@@ -41,6 +41,7 @@ class Trainer:
         self.train_data = train_data
         self.optimizer = optimizer
         self.save_every = save_every
+        self.fault_step = None  # fault injection
         self.scheduler = scheduler
         self.distributed = distributed
         self.rank = rank
@@ -74,6 +75,8 @@ class Trainer:
         return loss
 
     def _run_batch(self, source, targets):
+        if self.fault_step is not None and self.global_step == self.fault_step:
+            raise RuntimeError(f"injected fault at step {self.global_step} (--fault_step)")
         bs = source.shape[0]
         if self.use_graph and self._graph is None and self.global_step >= self.graph_warmup \
                 and self._graph_batch is None:

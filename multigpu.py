@@ -20,7 +20,8 @@ import torch.multiprocessing as mp
 
 from ddpx.data.datasets import get_datasets as getTrainingData  # noqa: F401  (reference name)
 from ddpx.models import VGG, DeepNN, MLP  # noqa: F401
-from ddpx.train.app import build_parser, ddp_setup, load_train_objs, main_multi, prepare_dataloader  # noqa: F401
+from ddpx.train.app import (apply_debug_env, build_parser, ddp_setup, load_train_objs, main_multi,  # noqa: F401
+                            maybe_profile, prepare_dataloader)
 from ddpx.train.evaluate import evaluate  # noqa: F401
 from ddpx.train.trainer import Trainer  # noqa: F401
 from ddpx.utils.size import Byte, GiB, KiB, MiB, get_model_size  # noqa: F401
@@ -37,15 +38,18 @@ def main(rank: int, world_size: int, save_every: int, total_epochs: int, batch_s
 if __name__ == "__main__":
     parser = build_parser("simple distributed training job")
     args = parser.parse_args()
+    maybe_profile(args)  # --profile: re-run as a child under rocprofv3 (before any GPU use)
+    apply_debug_env(args)
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:  # torchrun / elastic launch
         main(int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), args.save_every, args.total_epochs,
              args.batch_size, args)
     else:
         if args.nprocs:
             world_size = args.nprocs
-        elif args.device == "cpu" or not torch.cuda.is_available():
-            world_size = 2
         else:
-            world_size = torch.cuda.device_count()
+            # device_count() does not initialise HIP in this process: the spawned children are
+            # forked+exec'd, which must not happen from a process that touched the GPU
+            n = 0 if args.device == "cpu" else torch.cuda.device_count()
+            world_size = n if n > 0 else 2
         mp.spawn(main, args=(world_size, args.save_every, args.total_epochs, args.batch_size, args),
                  nprocs=world_size)

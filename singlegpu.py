@@ -11,7 +11,8 @@ from __future__ import annotations
 
 from ddpx.data.datasets import get_datasets as getTrainingData  # noqa: F401  (reference name)
 from ddpx.models import VGG, DeepNN, MLP  # noqa: F401
-from ddpx.train.app import build_parser, load_train_objs, prepare_dataloader, run  # noqa: F401
+from ddpx.train.app import (apply_debug_env, build_parser, load_train_objs, maybe_profile,  # noqa: F401
+                            prepare_dataloader, run)
 from ddpx.train.evaluate import evaluate  # noqa: F401
 from ddpx.train.trainer import Trainer  # noqa: F401
 from ddpx.utils.size import Byte, GiB, KiB, MiB, get_model_size  # noqa: F401
@@ -28,5 +29,7 @@ def main(device, total_epochs: int, save_every: int, batch_size: int, args=None)
 if __name__ == "__main__":
     parser = build_parser("simple single-device training job")
     args = parser.parse_args()
+    maybe_profile(args)  # --profile: re-run as a child under rocprofv3 (before any GPU use)
+    apply_debug_env(args)
     device = 0
     main(device, args.total_epochs, args.save_every, args.batch_size, args)

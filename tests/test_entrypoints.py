@@ -93,3 +93,24 @@ def test_resume_full_checkpoint(tmp_path):
     assert "[GPU0] Epoch 0" not in out and "[GPU0] Epoch 2 | Batchsize: 64 | Steps: 4" in out
     st = torch.load(tmp_path / "checkpoint_full.pt", weights_only=True)
     assert st["epoch"] == 2 and st["optimizer"]["state"]
+
+
+def test_fault_injection_all_ranks_exit_nonzero(tmp_path):
+    """a rank failing mid-training takes the whole job down with a non-zero exit."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "multigpu.py"), "2", "1", "--batch_size", "32",
+                        "--device", "cpu", "--nprocs", "2", "--model", "mlp", "--hidden", "64", "--data",
+                        "synthetic", "--train_size", "256", "--test_size", "64", "--fault_step", "5",
+                        "--fault_rank", "1"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert "injected fault at step 5" in (p.stdout + p.stderr)
+
+
+def test_ddpx_launch_wrapper(tmp_path):
+    """python -m ddpx.launch == torchrun with single-node 127.0.0.1 defaults."""
+    out = _run(["-m", "ddpx.launch", "--nproc-per-node", "2", os.path.join(ROOT, "multigpu.py"), "1", "1",
+                "--batch_size", "64", "--device", "cpu", "--model", "mlp", "--hidden", "64", "--data", "synthetic",
+                "--train_size", "256", "--test_size", "64", "--no_eval"], tmp_path)
+    assert "[GPU1] Epoch 0 | Batchsize: 64 | Steps: 2" in out

@@ -302,3 +302,33 @@ def test_native_libs_loaded(gpu):
     from ddpx.runtime import native
     libs = native.loaded_libraries()
     assert any("libddpx_kernels.so" in p for p in libs), libs
+
+
+@pytest.mark.parametrize("splitk", [True, False])
+def test_linear_mlp_shapes_splitk(gpu, splitk, monkeypatch):
+    """The toy-MLP products at M=512 (split-K 256x128 8-wave path vs single-pass tiles)."""
+    from ddpx.ops import gemm as G
+    monkeypatch.setattr(G, "SPLITK", splitk)
+    torch.manual_seed(7)
+    M, K, N = 512, 4096, 4096
+    x = _rand_bf16(M, K, dev=gpu)
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=gpu)
+    if splitk:
+        assert G.splitk_plan(M, N, K, True, True)[0] > 1
+        assert G.splitk_plan(M, K, N, True, False)[0] > 1
+    y = G.linear_fwd(x, w, b, relu=True)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    assert _rel(y, ref) < 5e-3
+    y2 = G.linear_fwd(x, w, b, relu=True)
+    assert torch.equal(y, y2)  # fixed-order split reduction: deterministic
+    dy = _rand_bf16(M, N, dev=gpu)
+    db = torch.empty(K, device=gpu)
+    dx = G.linear_dgrad(dy, w, relu_mask_of=x, bias_grad=db)
+    refdx = (dy.float() @ w.float()) * (x.float() > 0)
+    assert _rel(dx, refdx) < 5e-3
+    assert _rel(db, dx.float().sum(0)) < 1e-4
+    xs = x[:, :3072].contiguous()
+    ws = w[:, :3072].contiguous()
+    y3 = G.linear_fwd(xs, ws, b, relu=True)
+    assert _rel(y3, torch.relu(xs.float() @ ws.float().t() + b)) < 5e-3
