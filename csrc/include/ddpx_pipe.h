@@ -320,15 +320,17 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 }
 
 // NW = 4: 2x2 waves; NW = 8: 4 (M) x 2 (N) waves.  Wave tile (BM/WGM) x (BN/2).
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4>
+// KSUB: 64-wide K sub-tiles per stage (one barrier per 64*KSUB of K).
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1>
 __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
-  constexpr int BK = 64;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int BK = 64 * KSUB;
+  constexpr int A_SUB = BM * 64 * 2, B_SUB = BN * 64 * 2;
+  constexpr int A_BYTES = A_SUB * KSUB, B_BYTES = B_SUB * KSUB;
   constexpr int SLOT = A_BYTES + B_BYTES;
   constexpr int FM = BM / WGM / 16, FN = BN / 32;
-  constexpr int LPW = (BM + BN) / (8 * NW);  // DMA instructions per wave per stage
+  constexpr int LPW = KSUB * (BM + BN) / (8 * NW);  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
 
   const int tid = threadIdx.x;
@@ -361,9 +363,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
 
   auto issue = [&](int t) {
     char* slot = smem + (t % STAGES) * SLOT;
-    const int k0 = kbeg + t * BK;
-    stage_tile<BM, AK, AMODE, NW>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
-    stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+#pragma unroll
+    for (int u = 0; u < KSUB; ++u) {
+      const int k0 = kbeg + t * BK + u * 64;
+      stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+      stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+    }
   };
 
 #pragma unroll
@@ -379,10 +384,13 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     asm volatile("" ::: "memory");
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
 
-    const char* sa = smem + (t % STAGES) * SLOT;
-    const char* sb = sa + A_BYTES;
+    const char* sa0 = smem + (t % STAGES) * SLOT;
+    const char* sb0 = sa0 + A_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
+    for (int k2 = 0; k2 < BK; k2 += 32) {
+      const int u = k2 >> 6, kk = k2 & 63;
+      const char* sa = sa0 + u * A_SUB;
+      const char* sb = sb0 + u * B_SUB;
       bf16x8 a[FM], b[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / WGM) + i * 16, kk, lane);
@@ -463,18 +471,18 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   }
 }
 
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4>
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1>
 static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW>), dim3(tiles, splits),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB>), dim3(tiles, splits),
                      dim3(NW * 64), 0, s, p);
   return hipGetLastError();
 }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {
-  static const int t[9][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128},
-                              {64, 128},  {128, 64}, {64, 64},  {256, 128}};
-  const int c = (cfg >= 0 && cfg <= 8) ? cfg : 7;
+  static const int t[13][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
+                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64}};
+  const int c = (cfg >= 0 && cfg <= 12) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
 }
@@ -483,6 +491,10 @@ template <bool AK, bool BKc, int AMODE, int BMODE>
 static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) {
   switch (cfg) {
     case 8: return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8>(p, splits, s);  // 8 waves, 144 KiB LDS
+    case 9: return launch<64, 64, 3, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s);  // BK 128, 96 KiB
+    case 10: return launch<64, 128, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s); // BK 128, 96 KiB
+    case 11: return launch<128, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s); // BK 128, 96 KiB
+    case 12: return launch<64, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s);  // BK 128, 64 KiB (2 WG/CU)
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
     case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB

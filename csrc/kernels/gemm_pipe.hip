@@ -117,14 +117,14 @@ static int splitk_plan(int M, int N, int K, bool ak, bool bk) {
 }
 
 // Default tile per operand-layout class, from the MI355X sweep of the MLP shapes
-// (benchmarks/gemm_sweep.py; profiles/): M=512-row products want many small
-// tiles (64x64, 2-3 WG/CU), the K=512 weight-gradient products 64x128/3 stages.
+// (benchmarks/mlp_gemm_bench.py, benchmarks/sgd_bw.py; profiles/r1_gemm2): the M=512-row products
+// want 64x64 tiles with 128-wide K stages (fwd 27.1 vs 29.1 us, dgrad 36.5 vs 45.1 us at H=4096),
+// the K=512 weight-gradient products 64x128/3 stages.
 static int pick(int M, int N, int K, bool ak, bool bk) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   if (!ak && !bk) return tiles(64, 128) >= 512 ? 5 : 7;      // wgrad-shaped (reduction over batch)
-  if (ak && !bk) return 3;                                   // dgrad-shaped
-  if (tiles(128, 128) >= 1024 && K >= 2048) return 0;        // big forward GEMMs
-  return 7;                                                  // forward, small M
+  if (tiles(128, 128) >= 512 && K >= 2048) return 0;         // wide layers: 128x128 halves L2 traffic
+  return 12;  // M=512-row forward / dgrad: 64x64, BK=128 (one barrier per 128 of K), 2 WG/CU
 }
 
 }  // namespace pipe
