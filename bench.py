@@ -251,6 +251,7 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     multi = world > 1 or args.ddp_single
+    comm = net.comm_stats() if (multi and args.impl == "ddpx" and hasattr(net, "comm_stats")) else None
     consistent = None
     if multi and args.impl == "ddpx":
         # outside the timed region: replicas must hold identical weights after K steps
@@ -278,7 +279,9 @@ def main():
                    "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4),
                    "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
                    "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
-                   "replicas_consistent": consistent},
+                   "replicas_consistent": consistent,
+                   "comm_ms_per_step": round(comm["comm_ms"], 4) if comm else None,
+                   "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None},
     }
     if rank == 0:
         line = json.dumps(rec)

@@ -135,6 +135,11 @@ struct Reducer {
   int op = ncclAvg;
   std::vector<Bucket> buckets;
   int launched = 0;
+  // per-iteration communication timing (timing-enabled events; also valid inside HIP graphs):
+  // t_first before the first collective, t_last after the latest one (comm stream), t_bwd on the
+  // compute stream when backward ended (finalize) -> comm time and the part not hidden by backward
+  hipEvent_t t_first = nullptr, t_last = nullptr, t_bwd = nullptr;
+  bool timed = false, bwd_marked = false;
 };
 
 }  // namespace
@@ -272,6 +277,9 @@ DDPX_API void* ddpx_reducer_create(void* comm, int nbuckets, int op) {
   r->comm = static_cast<Comm*>(comm);
   r->op = op;
   r->buckets.resize(nbuckets);
+  hipEventCreate(&r->t_first);
+  hipEventCreate(&r->t_last);
+  hipEventCreate(&r->t_bwd);
   for (auto& b : r->buckets) {
     hipEventCreateWithFlags(&b.ready, hipEventDisableTiming);
     hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
@@ -327,6 +335,7 @@ static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
   if (he != hipSuccess) return (int)he;
   he = hipStreamWaitEvent(c->stream, b.ready, 0);
   if (he != hipSuccess) return (int)he;
+  if (r->launched == 0) hipEventRecord(r->t_first, c->stream);
   int e;
   if (b.mode == 1) {
     size_t shard = b.count / (size_t)c->nranks;
@@ -338,6 +347,8 @@ static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
   if (e) return e;
   he = hipEventRecord(b.done, c->stream);
   if (he != hipSuccess) return (int)he;
+  hipEventRecord(r->t_last, c->stream);
+  r->timed = true;
   b.launched = true;
   r->launched++;
   return 0;
@@ -372,6 +383,8 @@ DDPX_API int ddpx_reducer_wait_bucket(void* h, int i, hipStream_t s) {
 // to be force-launched.
 DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
   Reducer* r = static_cast<Reducer*>(h);
+  hipEventRecord(r->t_bwd, compute);
+  r->bwd_marked = true;
   int forced = 0;
   for (auto& b : r->buckets) {
     if (!b.launched) {
@@ -385,6 +398,27 @@ DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
     if (he != hipSuccess) return -(int)he;
   }
   return forced;
+}
+
+// End of backward on `compute` (overlap mode, where finalize does not join): timing marker only.
+DDPX_API int ddpx_reducer_mark_backward_end(void* h, hipStream_t compute) {
+  Reducer* r = static_cast<Reducer*>(h);
+  r->bwd_marked = true;
+  return (int)hipEventRecord(r->t_bwd, compute);
+}
+
+// Communication time of the last completed iteration and the part of it after backward ended
+// (exposed).  Synchronises on the timing events; call outside the hot loop.
+DDPX_API int ddpx_reducer_comm_stats(void* h, float* comm_ms, float* exposed_ms) {
+  Reducer* r = static_cast<Reducer*>(h);
+  *comm_ms = 0.f;
+  *exposed_ms = 0.f;
+  if (!r->timed) return 1;
+  if (hipEventSynchronize(r->t_last) != hipSuccess) return 2;
+  float t = 0.f;
+  if (hipEventElapsedTime(&t, r->t_first, r->t_last) == hipSuccess) *comm_ms = t;
+  if (r->bwd_marked && hipEventElapsedTime(&t, r->t_bwd, r->t_last) == hipSuccess) *exposed_ms = t > 0.f ? t : 0.f;
+  return 0;
 }
 
 // Sharded optimizer: after `compute` wrote this rank's shard of bucket i's parameter copy,
@@ -428,6 +462,9 @@ DDPX_API int ddpx_reducer_destroy(void* h) {
     hipEventDestroy(b.gready);
     hipEventDestroy(b.gdone);
   }
+  hipEventDestroy(r->t_first);
+  hipEventDestroy(r->t_last);
+  hipEventDestroy(r->t_bwd);
   delete r;
   return 0;
 }

@@ -208,7 +208,15 @@ class _NativeReducer:
             if rc < 0:
                 raise RuntimeError(f"reducer finalize failed: {rc}")
             return rc
+        self.rt.ddpx_reducer_mark_backward_end(self.h, native.stream_handle())
         return 0
+
+    def comm_stats(self):
+        c, e = native.ctypes.c_float(0), native.ctypes.c_float(0)
+        if self.rt.ddpx_reducer_comm_stats(self.h, native.ctypes.byref(c), native.ctypes.byref(e)) != 0:
+            return None
+        return {"comm_ms": c.value, "comm_exposed_ms": e.value,
+                "comm_overlap": (1.0 - e.value / c.value) if c.value > 0 else None}
 
     def close(self):
         if self.h:
@@ -460,6 +468,8 @@ class DistributedDataParallel(nn.Module):
                 if missing:
                     self.reducer.finalize(join=True)
                     self._overlap_pending = False
+                else:
+                    self.reducer.finalize(join=False)  # timing marker for comm_stats()
         else:
             self.reducer.finalize(join=True)
 
@@ -491,6 +501,12 @@ class DistributedDataParallel(nn.Module):
             for b in range(len(self.bucket_ranges)):
                 self.reducer.wait_bucket(b)
             self._overlap_pending = False
+
+    def comm_stats(self):
+        """{'comm_ms', 'comm_exposed_ms', 'comm_overlap'} of the last iteration (native RCCL reducer)."""
+        if self.reducer is None or not hasattr(self.reducer, "comm_stats"):
+            return None
+        return self.reducer.comm_stats()
 
     # ----------------------------------------------------------------- misc
     def state_dict(self, *args, **kwargs):

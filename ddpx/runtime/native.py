@@ -114,6 +114,8 @@ def _declare_rt(lib):
     _sig(lib, "ddpx_reducer_set_gather", I, P, I, P, S, I)
     _sig(lib, "ddpx_reducer_gather", I, P, I, P)
     _sig(lib, "ddpx_reducer_wait_gather", I, P, I, P)
+    _sig(lib, "ddpx_reducer_mark_backward_end", I, P, P)
+    _sig(lib, "ddpx_reducer_comm_stats", I, P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float))
     _sig(lib, "ddpx_reducer_prepare", I, P)
     _sig(lib, "ddpx_reducer_mark_ready", I, P, I, I, P)
     _sig(lib, "ddpx_reducer_wait_bucket", I, P, I, P)

@@ -123,8 +123,19 @@ class Trainer:
         if self.metrics is not None:
             loss = float(self.last_loss.detach().float().item()) if self.last_loss is not None else float("nan")
             dt = time.time() - t0
+            extra = {}
+            if self.distributed and torch.distributed.is_initialized():
+                t = torch.tensor([loss, float(n)], dtype=torch.float64)
+                torch.distributed.all_reduce(t)  # CPU tensor: the c10d (gloo) group
+                ws = torch.distributed.get_world_size()
+                extra["loss_mean_ranks"] = float(t[0]) / ws
+                extra["samples_all_ranks"] = int(t[1])
+            if hasattr(self.model, "comm_stats"):
+                cs = self.model.comm_stats()
+                if cs:
+                    extra.update(cs)
             self.metrics.log(epoch=epoch, step=self.global_step, loss=loss, samples=n, seconds=dt,
-                             samples_per_s=n / max(dt, 1e-9), lr=self.optimizer.param_groups[0]["lr"])
+                             samples_per_s=n / max(dt, 1e-9), lr=self.optimizer.param_groups[0]["lr"], **extra)
 
     def _save_checkpoint(self, epoch):
         path = ckpt.save_checkpoint(self.model, self.ckpt_path)
