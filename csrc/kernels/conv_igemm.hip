@@ -64,10 +64,19 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// Tile picks from the per-layer MI355X sweep (benchmarks/conv_sweep.py, profiles/r1_conv): the
+// 8-wave 256x128 tile (cfg 8, 2x the operand reuse of 128x128) wins every VGG layer with >= 128
+// output channels and >= 8x8 spatial size by 25-40 %; 4x4 layers (P = 8192) want 64x128; the
+// 64-channel layer at 32x32 stays on 64x64.
 static int pick_fwd(int P, int Co) {
-  // conv0/1 (Co 64/128, P = 512K): 128x64 tiles; small spatial layers: 64x64 for >= 256 WGs
-  if ((long long)((P + 127) / 128) * ((Co + 63) / 64) >= 1024) return 6;  // 128x64, 3 stages
-  return 7;                                                               // 64x64, 3 stages
+  if (Co <= 64) return 7;     // conv0 (3->64 @32): 64x64, 3 stages
+  if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
+  return 8;                   // 256x128, 8 waves
+}
+static int pick_dgrad(int P, int C) {
+  if (C <= 64) return 6;      // dx of conv1 (C = 64 @32): 128x64, 3 stages
+  if (P <= 8192) return 5;
+  return 8;
 }
 
 }  // namespace conv
@@ -144,13 +153,16 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = ConvGeom{H, W, Co, P};
-  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C);
   return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
 }
 
 static int pick_wgrad(int P, int C, int Co) {
   (void)P;
-  return (Co >= 128 && 9 * C >= 128) ? 4 : 7;  // 128x128 / 3 stages where the weight is big enough
+  (void)Co;
+  if (C <= 8) return 12;      // conv0 (K = 9 x 8): 64x64, BK 128
+  if (C <= 64) return 0;      // conv1: 128x128, 4 stages
+  return 8;                   // 256x128, 8 waves
 }
 
 // Number of K splits the weight-gradient GEMM uses for a tile config (cfg < 0: default).
