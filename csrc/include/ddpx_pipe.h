@@ -70,6 +70,7 @@ struct Params {
   ConvGeom conv;
   int klen;        // split-K: K elements per split (0: no split)
   long long split_stride;  // elements between the output slabs of consecutive splits
+  int sgd_plain;           // fused-SGD epilogue: 1 = ordinary (cached) loads/stores instead of non-temporal
 };
 
 constexpr unsigned kOOB = 0x80000000u;
@@ -229,9 +230,14 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
     if (m >= p.M) continue;
     const size_t off = (size_t)m * p.ldc + n;
     if (vec) {
-      if constexpr (E == EPI_SGD) {  // read-once / write-once streams: non-temporal
-        pin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.p + off));
-        if (p.sgd.mom != 0.f) bin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.buf + off));
+      if constexpr (E == EPI_SGD) {  // read-once / write-once streams: non-temporal (default)
+        if (p.sgd_plain) {
+          pin[i] = *reinterpret_cast<const f32x4*>(p.sgd.p + off);
+          if (p.sgd.mom != 0.f) bin[i] = *reinterpret_cast<const f32x4*>(p.sgd.buf + off);
+        } else {
+          pin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.p + off));
+          if (p.sgd.mom != 0.f) bin[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.buf + off));
+        }
       } else if constexpr (E == EPI_F32) {
         if (p.accumulate) cin[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(Cbase) + off);
       } else if constexpr (E == EPI_BF16) {
@@ -264,9 +270,14 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
       if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cbase) + off) = (f32x4){st[0], st[1], st[2], st[3]};
       } else if constexpr (E == EPI_SGD) {
-        __builtin_nontemporal_store((f32x4){po[0], po[1], po[2], po[3]}, reinterpret_cast<f32x4*>(p.sgd.p + off));
-        if (p.sgd.mom != 0.f)
-          __builtin_nontemporal_store((f32x4){bo[0], bo[1], bo[2], bo[3]}, reinterpret_cast<f32x4*>(p.sgd.buf + off));
+        if (p.sgd_plain) {
+          *reinterpret_cast<f32x4*>(p.sgd.p + off) = (f32x4){po[0], po[1], po[2], po[3]};
+          if (p.sgd.mom != 0.f) *reinterpret_cast<f32x4*>(p.sgd.buf + off) = (f32x4){bo[0], bo[1], bo[2], bo[3]};
+        } else {
+          __builtin_nontemporal_store((f32x4){po[0], po[1], po[2], po[3]}, reinterpret_cast<f32x4*>(p.sgd.p + off));
+          if (p.sgd.mom != 0.f)
+            __builtin_nontemporal_store((f32x4){bo[0], bo[1], bo[2], bo[3]}, reinterpret_cast<f32x4*>(p.sgd.buf + off));
+        }
         if (p.sgd.shadow)
           *reinterpret_cast<u32x2*>(p.sgd.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
       } else {

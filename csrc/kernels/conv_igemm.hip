@@ -171,7 +171,10 @@ DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co, int tile_cfg) {
   int bm, bn;
   tile_of(cfg, &bm, &bn);
   const int tiles = ((Co + bm - 1) / bm) * ((9 * C + bn - 1) / bn);
-  int S = (512 + tiles - 1) / tiles;
+  // one resident 8-wave workgroup per CU: 256 of them fill the chip; the 4-wave tiles want 2 per CU.
+  // Fewer splits = proportionally less fp32 partial traffic for the reduce kernel.
+  const int target = cfg == 8 ? 256 : 512;
+  int S = (target + tiles - 1) / tiles;
   const int maxS = (P + 1023) / 1024;  // >= 16 K-steps per split
   if (S > maxS) S = maxS;
   return S < 1 ? 1 : S;

@@ -24,6 +24,8 @@
 //    written straight into DDP buckets, bf16 (+accumulate), ReLU-mask
 //    backward, and an optional per-tile column sum of the stored output (the
 //    bias gradient of the layer below) written as [tiles_m][N] partials.
+#include <cstdlib>
+
 #include "ddpx_pipe.h"
 
 namespace ddpx {
@@ -156,6 +158,11 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
                  SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
                  pipe::ConvGeom{0, 0, 0, 0}, 0, 0};
   if (epi == pipe::EPI_SGD && (!sgd_p || !sgd_lr || (sgd_mom != 0.f && !sgd_buf))) return -5;
+  static const int sgd_plain = [] {
+    const char* e = getenv("DDPX_SGD_PLAIN");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  p.sgd_plain = sgd_plain;
   const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
   hipError_t e;
   if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
