@@ -29,6 +29,10 @@ import torch
 import torch.distributed as dist
 
 BASELINE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+# The reference publishes no numbers: vs_baseline stays null.  For context the line also
+# carries the ratio to the stock PyTorch-ROCm recipe measured on one MI355X with this same data
+# (--impl torch; profiles/r1_first, profiles/r1_gemm, profiles/r1_tune), samples/s at batch 512.
+STOCK_MEASURED_1GPU = {"mlp": 706_000.0, "mlp_wide": 100_040.0, "vgg": 26_400.0}
 
 
 def parse():
@@ -279,6 +283,8 @@ def main():
                    "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
                    "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
                    "replicas_consistent": consistent,
+                   "vs_stock_pytorch_1gpu": (round(value / (STOCK_MEASURED_1GPU[args.model] * world), 4)
+                                             if args.impl == "ddpx" and args.model in STOCK_MEASURED_1GPU else None),
                    "comm_ms_per_step": round(comm["comm_ms"], 4) if comm else None,
                    "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None},
     }
