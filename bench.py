@@ -122,7 +122,9 @@ def resolve_defaults(args, world):
     if args.overlap_optimizer is None:
         args.overlap_optimizer = int(multi)
     if args.shard_optimizer is None:
-        args.shard_optimizer = int(multi)
+        # ZeRO-1 pays off where only the bf16 shadow must be all-gathered (MLP weights); the native
+        # VGG reads fp32 masters (per-step weight repack), so it keeps the replicated all-reduce
+        args.shard_optimizer = int(multi and args.model.startswith("mlp"))
 
 
 def build_ddpx(args, device, world):
