@@ -114,3 +114,20 @@ def test_ddpx_launch_wrapper(tmp_path):
                 "--batch_size", "64", "--device", "cpu", "--model", "mlp", "--hidden", "64", "--data", "synthetic",
                 "--train_size", "256", "--test_size", "64", "--no_eval"], tmp_path)
     assert "[GPU1] Epoch 0 | Batchsize: 64 | Steps: 2" in out
+
+
+def test_port_in_use_gives_clear_error(tmp_path):
+    """SURVEY §4 'Fault': a taken MASTER_PORT fails fast with an address-in-use error, not a hang."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        s.listen(1)
+        port = s.getsockname()[1]
+        env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   TORCH_DIST_INIT_BARRIER="0")
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "multigpu.py"), "1", "1", "--device", "cpu",
+                            "--nprocs", "2", "--model", "mlp", "--hidden", "64", "--data", "synthetic",
+                            "--train_size", "128", "--test_size", "64", "--no_eval"], cwd=tmp_path, env=env,
+                           capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert re.search(r"address already in use|EADDRINUSE|Address already in use", p.stdout + p.stderr, re.I)

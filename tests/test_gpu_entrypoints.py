@@ -1,0 +1,67 @@
+"""singlegpu.py / multigpu.py / bench.py end to end on the MI355X (SURVEY §4 'Integration')."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from tests._dist_util import free_port
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, cwd, extra_env=None, timeout=600):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    if extra_env:
+        env.update(extra_env)
+    r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return r.stdout
+
+
+def test_singlegpu_mlp_graph_on_gpu(gpu, tmp_path):
+    out = _run([os.path.join(ROOT, "singlegpu.py"), "2", "1", "--model", "mlp", "--data", "synthetic",
+                "--train_size", "4096", "--test_size", "1024", "--graph", "--seed", "0", "--lr", "0.05",
+                "--full_checkpoint", "--metrics", "m.jsonl"], tmp_path)
+    assert "[GPU0] Epoch 1 | Batchsize: 512 | Steps: 8" in out
+    acc = float(re.search(r"accuracy=(\d+\.\d\d)%", out).group(1))
+    assert acc > 15.0, out
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    assert sd["fc0.weight"].dtype == torch.float32 and sd["fc0.weight"].shape == (4096, 3072)
+    recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
+    assert any("samples_per_s" in r for r in recs)
+
+
+def test_singlegpu_vgg_native_on_gpu(gpu, tmp_path):
+    out = _run([os.path.join(ROOT, "singlegpu.py"), "1", "1", "--data", "synthetic", "--train_size", "2048",
+                "--test_size", "512"], tmp_path)
+    assert "fp32 model has size=35.20 MiB" in out
+    assert re.search(r"fp32 model has accuracy=\d+\.\d\d%", out)
+
+
+def test_multigpu_single_rank_rccl_sharded(gpu, tmp_path):
+    """The distributed entry point with the native RCCL communicator at world size 1 (ZeRO-1, bf16 grads)."""
+    out = _run([os.path.join(ROOT, "multigpu.py"), "1", "1", "--nprocs", "1", "--model", "mlp", "--data",
+                "synthetic", "--train_size", "2048", "--test_size", "512", "--shard_optimizer", "--grad_dtype",
+                "bf16", "--overlap_optimizer", "--metrics", "m.jsonl"], tmp_path,
+               extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port())})
+    assert "[GPU0] Epoch 0 | Batchsize: 512 | Steps: 4" in out
+    recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
+    assert any(r.get("comm_ms") is not None for r in recs)
+
+
+def test_bench_contract_one_gpu(gpu, tmp_path):
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3"], tmp_path)
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["n_gpus"] == 1 and rec["steps"] == 10 and rec["value"] > 0 and rec["dtype"] == "bf16"
