@@ -195,7 +195,11 @@ def main():
         model, net, opt, sched = build_ddpx(args, device, world)
         static_x, static_y = loader.make_batch(idx_all[:bs], 0)
 
+        # the LR schedule lives on the device: the captured step advances it (no per-step host write)
+        opt.attach_device_schedule(sched)
+
         def step_body(x, y):
+            opt.device_lr_step()
             opt.zero_grad()
             loss, _ = net.forward_loss(x, y) if hasattr(model, "forward_loss") else (
                 torch.nn.functional.cross_entropy(net(x), y), None)

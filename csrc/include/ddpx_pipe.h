@@ -204,7 +204,7 @@ __device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t of
 
 template <int E, int BM, int BN, int NT = 256>
 __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const float* T, int m0, int n0, int tid,
-                                             float (&csum)[4]) {
+                                             float (&csum)[4], const float* pf = nullptr) {
   constexpr int Q = BN / 4;           // column quads per row
   constexpr int RSTEP = NT / Q;       // rows between a thread's consecutive vectors
   constexpr int NV = BM / RSTEP;      // vectors per thread
@@ -231,7 +231,11 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
     const size_t off = (size_t)m * p.ldc + n;
     if (vec) {
       if constexpr (E == EPI_SGD) {  // read-once / write-once streams: non-temporal (default)
-        if (p.sgd_plain) {
+        if (pf) {  // p / momentum tile prefetched into LDS during the main loop
+          const int r = r0 + (i0 + i) * RSTEP;
+          pin[i] = *reinterpret_cast<const f32x4*>(pf + r * BN + 4 * cq);
+          bin[i] = *reinterpret_cast<const f32x4*>(pf + BM * BN + r * BN + 4 * cq);
+        } else if (p.sgd_plain) {
           pin[i] = *reinterpret_cast<const f32x4*>(p.sgd.p + off);
           if (p.sgd.mom != 0.f) bin[i] = *reinterpret_cast<const f32x4*>(p.sgd.buf + off);
         } else {
@@ -332,7 +336,10 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 
 // NW = 4: 2x2 waves; NW = 8: 4 (M) x 2 (N) waves.  Wave tile (BM/WGM) x (BN/2).
 // KSUB: 64-wide K sub-tiles per stage (one barrier per 64*KSUB of K).
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1>
+// SGDPF (fused-SGD wgrad only): the tile's fp32 master / momentum rows are LDS-DMA'd into a side
+// buffer during the main loop, so the optimizer epilogue only streams writes.
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
+          bool SGDPF = false>
 __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
@@ -342,7 +349,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int SLOT = A_BYTES + B_BYTES;
   constexpr int FM = BM / WGM / 16, FN = BN / 32;
   constexpr int LPW = KSUB * (BM + BN) / (8 * NW);  // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
+  constexpr int PF_BYTES = SGDPF ? 2 * BM * BN * 4 : 0;
+  constexpr int PF_CPR = BN / 4, PF_RPI = 64 / PF_CPR;      // 16-B chunks per row, rows per wave-instruction
+  constexpr int PF_PER_WAVE = SGDPF ? (BM / PF_RPI) / NW : 0;  // per array
+  constexpr int PFW = 2 * PF_PER_WAVE;                        // prefetch DMA ops per wave
+  static_assert(!SGDPF || (BM % (PF_RPI * NW) == 0 && 64 % PF_CPR == 0), "prefetch geometry");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT + PF_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -382,18 +394,41 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     }
   };
 
+  auto prefetch_sgd = [&]() {
+    if constexpr (SGDPF) {
+      char* pfb = smem + STAGES * SLOT;
+      const unsigned nbytes = (unsigned)((size_t)p.M * p.ldc * 4);
+#pragma unroll
+      for (int arr = 0; arr < 2; ++arr) {
+        const float* src = (arr && p.sgd.buf) ? p.sgd.buf : p.sgd.p;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, nbytes, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < PF_PER_WAVE; ++j) {
+          const int inst = j * NW + wave;
+          const int r = inst * PF_RPI + lane / PF_CPR, c = lane % PF_CPR;
+          const int gm = m0 + r, gn = n0 + 4 * c;
+          const unsigned voff = (gm < p.M && gn + 3 < p.N) ? (unsigned)(((size_t)gm * p.ldc + gn) * 4) : kOOB;
+          dma16(rs, pfb + arr * BM * BN * 4 + inst * 1024, voff);
+        }
+      }
+    }
+  };
+
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s);
 
   for (int t = 0; t < nk; ++t) {
     const int ahead = min(STAGES - 2, nk - 1 - t);
-    if (ahead >= 2) wait_vmcnt<2 * LPW>();
-    else if (ahead == 1) wait_vmcnt<LPW>();
-    else wait_vmcnt<0>();
+    // stages 1..STAGES-1 were issued before the prefetch (t = 0): its PFW ops are younger than them
+    const bool pf_young = SGDPF && t >= 1 && t <= STAGES - 1;
+    if (ahead >= 2) { if (pf_young) wait_vmcnt<2 * LPW + PFW>(); else wait_vmcnt<2 * LPW>(); }
+    else if (ahead == 1) { if (pf_young) wait_vmcnt<LPW + PFW>(); else wait_vmcnt<LPW>(); }
+    else { if (pf_young) wait_vmcnt<PFW>(); else wait_vmcnt<0>(); }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    if (t == 0) prefetch_sgd();
 
     const char* sa0 = smem + (t % STAGES) * SLOT;
     const char* sb0 = sa0 + A_BYTES;
@@ -419,6 +454,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int TLD = BN + 4;
   float* T = reinterpret_cast<float*>(smem);
   static_assert(BM * TLD * 4 + (NT / (BN / 4) + 2) * BN * 4 <= STAGES * SLOT, "epilogue LDS overflow");
+  if constexpr (SGDPF) wait_vmcnt<0>();  // the prefetch (if the loop ended before waiting on it)
   __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
   {
     const int mr = wm * (BM / WGM) + 4 * (lane >> 4);
@@ -438,7 +474,10 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
     case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
     case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_SGD: epilogue_vec<EPI_SGD, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
+    case EPI_SGD:
+      epilogue_vec<EPI_SGD, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs,
+                                        SGDPF ? reinterpret_cast<const float*>(smem + STAGES * SLOT) : nullptr);
+      break;
     case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
     default: epilogue_vec<EPI_RELUMASK_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
   }
@@ -482,11 +521,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   }
 }
 
-template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1>
+template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
+          bool SGDPF = false>
 static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB>), dim3(tiles, splits),
-                     dim3(NW * 64), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB, SGDPF>),
+                     dim3(tiles, splits), dim3(NW * 64), 0, s, p);
   return hipGetLastError();
 }
 
@@ -514,6 +554,19 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 5: return launch<64, 128, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
     case 6: return launch<128, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
     default: return launch<64, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  48 KiB, 3 WG/CU
+  }
+}
+
+// Fused-SGD weight-gradient tiles with the master/momentum prefetch (plain A/B layouts only).
+// Returns hipErrorInvalidValue for configs without a prefetch variant.
+template <bool AK, bool BKc>
+static hipError_t dispatch_sgd_prefetch(const Params& p, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 3: return launch<64, 64, 4, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, true>(p, 1, s);   //  96 KiB
+    case 5: return launch<64, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, true>(p, 1, s);  // 136 KiB
+    case 7: return launch<64, 64, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, true>(p, 1, s);   //  80 KiB, 2 WG/CU
+    case 12: return launch<64, 64, 2, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 2, true>(p, 1, s);  //  96 KiB
+    default: return hipErrorInvalidValue;
   }
 }
 

@@ -164,6 +164,14 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   p.sgd_plain = sgd_plain;
   const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  static const int sgd_pf = [] {
+    const char* e = getenv("DDPX_SGD_PREFETCH");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (epi == pipe::EPI_SGD && sgd_pf && !a_kcontig && !b_kcontig && (ldc & 3) == 0 &&
+      (size_t)M * ldc * 4 < 0x80000000ull && (cfg == 3 || cfg == 5 || cfg == 7 || cfg == 12)) {
+    return (int)pipe::dispatch_sgd_prefetch<false, false>(p, cfg, stream);
+  }
   hipError_t e;
   if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
   else if (a_kcontig) e = pipe::dispatch<true, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);

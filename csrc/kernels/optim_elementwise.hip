@@ -176,3 +176,19 @@ DDPX_API int ddpx_scale_f32(float* x, int64_t n, float scale, hipStream_t s) {
   hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, scale);
   return (int)hipGetLastError();
 }
+
+// Device-side LR schedule: lr = table[min(step, n-1)], step += 1 — one thread, captured inside the
+// training-step HIP graph, so a replayed step needs no host write of the learning rate.
+__global__ void lr_advance_kernel(const float* __restrict__ table, int n, int* __restrict__ counter,
+                                  float* __restrict__ lr) {
+  const int k = *counter;
+  *lr = table[k < n ? k : n - 1];
+  *counter = k + 1;
+}
+
+DDPX_API int ddpx_lr_advance(const float* table, int n, int* counter, float* lr, hipStream_t s) {
+  if (n <= 0) return -1;
+  hipLaunchKernelGGL(lr_advance_kernel, dim3(1), dim3(1), 0, s, table, n, counter, lr);
+  return (int)hipGetLastError();
+}
+

@@ -54,6 +54,8 @@ class SGD(Optimizer):
         self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if need_dev_lr else None
         if self.fused_backward:
             flat.fused_opt = self
+        self._lr_table = None  # device-side LR schedule (attach_device_schedule)
+        self._lr_counter = None
         self.bucket_source = None  # set by DDP when the optimizer overlaps the all-reduce or is sharded
         flat.optimizer = self
         if getattr(flat.sink, "sharded", False):
@@ -77,9 +79,39 @@ class SGD(Optimizer):
             self.flat.fused_opt = None
 
     def sync_lr(self):
-        """Copy the host learning rate into the device scalar (outside graph capture)."""
-        if self.lr_dev is not None:
+        """Copy the host learning rate into the device scalar (outside graph capture).
+
+        No-op while a device-side schedule is attached (the step kernel sequence advances it)."""
+        if self.lr_dev is not None and self._lr_table is None:
             self.lr_dev.fill_(float(self.param_groups[0]["lr"]))
+
+    def attach_device_schedule(self, scheduler, horizon: int | None = None):
+        """Tabulate a LambdaLR-style schedule on the device (lr[k] = base_lr * lambda(k)).
+
+        After this, :meth:`device_lr_step` — called at the start of every training step, inside the
+        captured graph — sets ``lr_dev`` from the table and advances a device step counter, so graph
+        replays need no host-to-device write.  The host scheduler keeps stepping for bookkeeping
+        (state_dict, logging).  ``horizon``: table length (default: the one-cycle's end + 1).
+        """
+        if self.lr_dev is None or not self.lr_dev.is_cuda:
+            return False
+        lam = scheduler.lr_lambdas[0]
+        base = scheduler.base_lrs[0]
+        if horizon is None:
+            spe, ne = getattr(lam, "steps_per_epoch", None), getattr(lam, "num_epochs", None)
+            horizon = spe * ne + 1 if spe and ne else 100_000
+        table = torch.tensor([base * lam(k) for k in range(horizon)], dtype=torch.float32)
+        self._lr_table = table.to(self.lr_dev.device)
+        self._lr_counter = torch.tensor([scheduler.last_epoch], dtype=torch.int32, device=self.lr_dev.device)
+        return True
+
+    def device_lr_step(self):
+        if self._lr_table is None:
+            return
+        from ..runtime import native
+        native.check(native.kernels().ddpx_lr_advance(self._lr_table.data_ptr(), self._lr_table.numel(),
+                                                      self._lr_counter.data_ptr(), self.lr_dev.data_ptr(),
+                                                      native.stream_handle()), "ddpx_lr_advance")
 
     def _lr_arg(self):
         return self.lr_dev if self.lr_dev is not None else float(self.param_groups[0]["lr"])
@@ -159,4 +191,5 @@ class SGD(Optimizer):
                 if s is not None and s.get("momentum_buffer") is not None:
                     j = self.flat.index[id(p)]
                     self.momentum_buffer[self.flat.slice(j)].copy_(s["momentum_buffer"].reshape(-1))
+        self._lr_table = None  # a resumed schedule position: re-attach the device schedule
         self.sync_lr()

@@ -50,6 +50,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_cast_f32_bf16", I, P, P, I64, P)
     _sig(lib, "ddpx_colsum_bf16", I, P, P, I, I, I, F, I, P)
     _sig(lib, "ddpx_scale_f32", I, P, I64, F, P)
+    _sig(lib, "ddpx_lr_advance", I, P, I, P, P, P)
     _sig(lib, "ddpx_gemm_pipe", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_gemm_pipe_tiles_m", I, I, I, I, I, I, I)
     _sig(lib, "ddpx_gemm_splitk_plan", I, I, I, I, I, I, ctypes.POINTER(c_int64), ctypes.POINTER(c_int))

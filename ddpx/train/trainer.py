@@ -41,6 +41,7 @@ class Trainer:
         self.train_data = train_data
         self.optimizer = optimizer
         self.save_every = save_every
+        self._device_lr = False  # LR schedule tabulated on the device (set at train start)
         self.fault_step = None  # fault injection
         self.scheduler = scheduler
         self.distributed = distributed
@@ -65,6 +66,8 @@ class Trainer:
         return F.cross_entropy(output, targets)
 
     def _step_body(self, source, targets):
+        if self._device_lr:
+            self.optimizer.device_lr_step()
         self.optimizer.zero_grad()
         with trace_range("forward"):
             loss = self._forward_loss(source, targets)
@@ -144,6 +147,9 @@ class Trainer:
             ckpt.save_full_checkpoint(ckpt.FULL_CKPT_PATH, self.model, self.optimizer, self.scheduler, epoch)
 
     def train(self, max_epochs: int):
+        if (not self._device_lr and hasattr(self.optimizer, "attach_device_schedule")
+                and hasattr(self.scheduler, "lr_lambdas")):
+            self._device_lr = bool(self.optimizer.attach_device_schedule(self.scheduler))
         for epoch in range(self.start_epoch, max_epochs):
             self._run_epoch(epoch)
             if self.distributed and epoch % self.save_every == 0 and hasattr(self.model, "consolidate"):

@@ -332,3 +332,23 @@ def test_linear_mlp_shapes_splitk(gpu, splitk, monkeypatch):
     ws = w[:, :3072].contiguous()
     y3 = G.linear_fwd(xs, ws, b, relu=True)
     assert _rel(y3, torch.relu(xs.float() @ ws.float().t() + b)) < 5e-3
+
+
+def test_device_lr_schedule_matches_lambdalr(gpu):
+    """SGD.attach_device_schedule: the device table + counter reproduce torch LambdaLR step by step."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.optim.schedule import one_cycle
+    from ddpx.optim.sgd import SGD
+    m = MLP(hidden=256)
+    ddpx.prepare_model(m, gpu)
+    opt = SGD(m.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=True)
+    sched = one_cycle(opt, 7, num_epochs=3)
+    for _ in range(3):  # start mid-schedule
+        sched.step()
+    assert opt.attach_device_schedule(sched)
+    for _ in range(30):
+        host = opt.param_groups[0]["lr"]
+        opt.device_lr_step()
+        assert abs(opt.lr_dev.item() - host) < 1e-7
+        sched.step()
