@@ -58,7 +58,53 @@ head_logits_partial_kernel(const unsigned short* __restrict__ H, const unsigned 
   if (m0 + rr < M) partial[((size_t)ks * M + m0 + rr) * kHeadC + cc] = s;
 }
 
-// One thread per row: logits, log-softmax, NLL, dlogits, argmax.
+// Per row: logits, log-softmax, NLL, dlogits, argmax.  Returns the row loss (0 for no target).
+__device__ __forceinline__ float head_row(const float* __restrict__ partial, int KS, const float* __restrict__ b,
+                                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, int m,
+                                          float* __restrict__ logits, float* __restrict__ dlogits, int* hit) {
+  float z[kHeadC];
+#pragma unroll
+  for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
+  for (int ks = 0; ks < KS; ++ks) {
+    const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = pp[q];
+      z[4 * q] += v[0];
+      z[4 * q + 1] += v[1];
+      z[4 * q + 2] += v[2];
+      z[4 * q + 3] += v[3];
+    }
+  }
+  float mx = -INFINITY;
+  int am = 0;
+#pragma unroll
+  for (int c = 0; c < kHeadC; ++c) {
+    if (c < C) {
+      z[c] += b[c];
+      if (z[c] > mx) { mx = z[c]; am = c; }
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < kHeadC; ++c)
+    if (c < C) se += __expf(z[c] - mx);
+  const float lse = mx + __logf(se);
+  const int t = tgt ? (int)tgt[m] : 0;
+  float zt = 0.f;
+#pragma unroll
+  for (int c = 0; c < kHeadC; ++c) {
+    if (c < C) {
+      if (c == t) zt = z[c];
+      if (logits) logits[(size_t)m * C + c] = z[c];
+      if (dlogits) dlogits[(size_t)m * C + c] = (__expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * inv_m;
+    }
+  }
+  *hit = tgt ? (am == t) : 0;
+  return lse - zt;
+}
+
+// One thread per row.
 __global__ void __launch_bounds__(256)
 head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
                      const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
@@ -66,50 +112,45 @@ head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __r
   const int m = blockIdx.x * 256 + threadIdx.x;
   int hit = 0;
   if (m < M) {
-    float z[kHeadC];
-#pragma unroll
-    for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
-    for (int ks = 0; ks < KS; ++ks) {
-      const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = pp[q];
-        z[4 * q] += v[0];
-        z[4 * q + 1] += v[1];
-        z[4 * q + 2] += v[2];
-        z[4 * q + 3] += v[3];
-      }
-    }
-    float mx = -INFINITY;
-    int am = 0;
-#pragma unroll
-    for (int c = 0; c < kHeadC; ++c) {
-      if (c < C) {
-        z[c] += b[c];
-        if (z[c] > mx) { mx = z[c]; am = c; }
-      }
-    }
-    float se = 0.f;
-#pragma unroll
-    for (int c = 0; c < kHeadC; ++c)
-      if (c < C) se += __expf(z[c] - mx);
-    const float lse = mx + __logf(se);
-    const int t = tgt ? (int)tgt[m] : 0;
-    float zt = 0.f;
-#pragma unroll
-    for (int c = 0; c < kHeadC; ++c) {
-      if (c < C) {
-        if (c == t) zt = z[c];
-        if (logits) logits[(size_t)m * C + c] = z[c];
-        if (dlogits) dlogits[(size_t)m * C + c] = (__expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * inv_m;
-      }
-    }
-    if (loss_rows) loss_rows[m] = lse - zt;
-    hit = tgt ? (am == t) : 0;
+    const float l = head_row(partial, KS, b, tgt, M, C, inv_m, m, logits, dlogits, &hit);
+    if (loss_rows) loss_rows[m] = l;
   }
   if (correct) {
     const unsigned long long bal = __ballot(hit);
     if ((threadIdx.x & 63) == 0 && bal) atomicAdd(correct, __popcll(bal));  // integer: deterministic
+  }
+}
+
+// Single workgroup (M <= 8192): every row plus the mean loss in one launch.  Rows are assigned to
+// threads in a fixed pattern and reduced in a fixed order: deterministic.
+__global__ void __launch_bounds__(1024)
+head_finalize_mean_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
+                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
+                          float* __restrict__ loss_rows, float* __restrict__ dlogits, int* __restrict__ correct,
+                          float* __restrict__ loss_mean) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  int hits = 0;
+  for (int m = threadIdx.x; m < M; m += 1024) {
+    int hit = 0;
+    const float l = head_row(partial, KS, b, tgt, M, C, inv_m, m, logits, dlogits, &hit);
+    if (loss_rows) loss_rows[m] = l;
+    acc += l;
+    hits += hit;
+  }
+  if (correct) {
+    int hsum = hits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hsum += __shfl_xor(hsum, o, 64);
+    if ((threadIdx.x & 63) == 0 && hsum) atomicAdd(correct, hsum);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) *loss_mean = t / (float)M;
   }
 }
 
@@ -322,9 +363,11 @@ DDPX_API int64_t ddpx_head_bwd_scratch(int M, int K, int C) {
   return rs * (C + 1) * K + rs * C;
 }
 
+// loss_mean (optional): mean row loss written by the same launch (M <= 8192) or by a follow-up
+// single-workgroup reduction (larger M); loss_rows may then be null for M <= 8192.
 DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K, int C,
                            int ldh, float inv_m, float* logits, float* loss_rows, float* dlogits, int* correct,
-                           float* scratch, hipStream_t s) {
+                           float* scratch, float* loss_mean, hipStream_t s) {
   if (M <= 0) return 0;
   if (C < 1 || C > kHeadC) return -1;
   if (K % 8 || ldh % 8) return -2;
@@ -333,8 +376,15 @@ DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const i
   kslice = (kslice + 127) / 128 * 128;  // whole 32-k MFMA steps for each of the 4 waves
   hipLaunchKernelGGL(head_logits_partial_kernel, dim3((M + 15) / 16, ks), dim3(256), 0, s, (const unsigned short*)H,
                      (const unsigned short*)W, M, K, C, ldh, kslice, scratch);
+  if (loss_mean && tgt && M <= 8192) {
+    hipLaunchKernelGGL(head_finalize_mean_kernel, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                       logits, loss_rows, dlogits, correct, loss_mean);
+    return (int)hipGetLastError();
+  }
+  if (loss_mean && !loss_rows) return -3;
   hipLaunchKernelGGL(head_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, s, scratch, ks, b, tgt, M, C, inv_m,
                      logits, loss_rows, dlogits, correct);
+  if (loss_mean && tgt) hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, s, loss_rows, M, loss_mean);
   return (int)hipGetLastError();
 }
 

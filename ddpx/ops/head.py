@@ -43,19 +43,17 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
     dev = h.device
     logits = torch.empty((M, C), dtype=torch.float32, device=dev) if want_logits else None
     have_t = targets is not None
-    loss_rows = torch.empty((M,), dtype=torch.float32, device=dev) if have_t else None
+    # M <= 8192: logits, loss rows, dlogits and the mean loss come out of one finalize launch
+    loss_rows = torch.empty((M,), dtype=torch.float32, device=dev) if (have_t and M > 8192) else None
     dl = torch.empty((M, C), dtype=torch.float32, device=dev) if (want_grad and have_t) else None
+    loss = torch.empty((), dtype=torch.float32, device=dev) if have_t else None
     lib = native.kernels()
     scratch = torch.empty((int(lib.ddpx_head_fwd_scratch(M, K)),), dtype=torch.float32, device=dev)
     s = native.stream_handle()
     rc = lib.ddpx_head_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, C, h.stride(0),
                            1.0 / M, native.ptr(logits), native.ptr(loss_rows), native.ptr(dl), native.ptr(correct),
-                           scratch.data_ptr(), s)
+                           scratch.data_ptr(), native.ptr(loss), s)
     native.check(rc, "ddpx_head_fwd")
-    loss = None
-    if have_t:
-        loss = torch.empty((), dtype=torch.float32, device=dev)
-        native.check(lib.ddpx_mean(loss_rows.data_ptr(), M, loss.data_ptr(), s), "ddpx_mean")
     return loss, logits, dl
 
 

@@ -61,7 +61,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_reduce_partials", I, P, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_head_fwd_scratch", I64, I, I)
     _sig(lib, "ddpx_head_bwd_scratch", I64, I, I, I)
-    _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P)
+    _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P, P)
     _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, F, F,
          P)
     _sig(lib, "ddpx_mean", I, P, I, P, P)
