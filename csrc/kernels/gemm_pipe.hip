@@ -164,9 +164,12 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   p.sgd_plain = sgd_plain;
   const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  // Master/momentum LDS prefetch for the fused-SGD tiles: opt-in (DDPX_SGD_PREFETCH=1).  Measured
+  // slower on MI355X (toy fc1 64x128: 112 vs 77 us; profiles/r1_epi): the 64 KiB side buffer halves
+  // occupancy and the prefetch lands on the critical path of short (K = 512) main loops.
   static const int sgd_pf = [] {
     const char* e = getenv("DDPX_SGD_PREFETCH");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '1' ? 1 : 0;
   }();
   if (epi == pipe::EPI_SGD && sgd_pf && !a_kcontig && !b_kcontig && (ldc & 3) == 0 &&
       (size_t)M * ldc * 4 < 0x80000000ull && (cfg == 3 || cfg == 5 || cfg == 7 || cfg == 12)) {
