@@ -197,13 +197,14 @@ def main():
 
         # the LR schedule lives on the device: the captured step advances it (no per-step host write)
         opt.attach_device_schedule(sched)
+        one = torch.ones((), device=device)  # d(loss)/d(loss): no fill kernel per step
 
         def step_body(x, y):
             opt.device_lr_step()
             opt.zero_grad()
             loss, _ = net.forward_loss(x, y) if hasattr(model, "forward_loss") else (
                 torch.nn.functional.cross_entropy(net(x), y), None)
-            loss.backward()
+            loss.backward(one)
             opt.step()
             return loss
 

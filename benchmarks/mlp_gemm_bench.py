@@ -30,7 +30,7 @@ def main():
             row[f"fwd_auto_split{int(sk)}"] = timeit(lambda: G.linear_fwd(x, w, b, relu=True))
             row[f"dgrad_auto_split{int(sk)}"] = timeit(lambda: G.linear_dgrad(dy, w, relu_mask_of=x))
         G.SPLITK = True
-        for t in range(13):
+        for t in range(14):
             row[f"fwd_t{t}"] = timeit(lambda: G.linear_fwd(x, w, b, relu=True, tile=t))
             row[f"dgrad_t{t}"] = timeit(lambda: G.linear_dgrad(dy, w, relu_mask_of=x, tile=t))
         res[name] = row

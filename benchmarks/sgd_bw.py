@@ -69,7 +69,7 @@ def main():
         o32 = torch.empty(N, K, device=dev)
         o16 = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
         row = {}
-        for tile in range(13):
+        for tile in range(14):
             try:
                 row[f"f32_t{tile}"] = timeit(lambda: G.linear_wgrad(dy, x, o32, tile=tile))
                 row[f"bf16_t{tile}"] = timeit(lambda: G.linear_wgrad(dy, x, o16, tile=tile))

@@ -451,74 +451,93 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   }
 
   // ---- stage the accumulator tile through LDS (all DMA has landed: last wait was vmcnt(0)) ----
+  // The fp32 tile is staged through LDS in EH row-parts when BM x BN does not fit beside the
+  // reduction scratch (256x256: 4 parts of 64 rows): waves owning the part's rows write it, every
+  // thread runs the epilogue on it.
   constexpr int TLD = BN + 4;
+  constexpr int SCR = (NT / (BN / 4) + 2) * BN * 4;
+  constexpr int EH = (BM * TLD * 4 + SCR <= STAGES * SLOT) ? 1 : ((BM / 2) * TLD * 4 + SCR <= STAGES * SLOT) ? 2 : 4;
+  static_assert(WGM % EH == 0, "epilogue parts must align with wave rows");
+  constexpr int BMH = BM / EH;
+  constexpr int WPH = WGM / EH;  // wave rows per half
   float* T = reinterpret_cast<float*>(smem);
-  static_assert(BM * TLD * 4 + (NT / (BN / 4) + 2) * BN * 4 <= STAGES * SLOT, "epilogue LDS overflow");
+  static_assert(BMH * TLD * 4 + SCR <= STAGES * SLOT, "epilogue LDS overflow");
+  static_assert(EH == 1 || !SGDPF, "prefetch needs a single-pass epilogue");
   if constexpr (SGDPF) wait_vmcnt<0>();  // the prefetch (if the loop ended before waiting on it)
-  __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
-  {
-    const int mr = wm * (BM / WGM) + 4 * (lane >> 4);
-    const int nc = wn * (BN / 2) + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) T[(mr + i * 16 + r) * TLD + nc + j * 16] = acc[i][j][r];
-  }
-  __syncthreads();
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  switch (p.epi) {
-    case EPI_F32: epilogue_vec<EPI_F32, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BF16: epilogue_vec<EPI_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    case EPI_SGD:
-      epilogue_vec<EPI_SGD, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs,
-                                        SGDPF ? reinterpret_cast<const float*>(smem + STAGES * SLOT) : nullptr);
-      break;
-    case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-    default: epilogue_vec<EPI_RELUMASK_BF16, BM, BN, NT>(p, Cbase, T, m0, n0, tid, cs); break;
-  }
-  if (!p.colsum) return;
-
-  // ---- per-tile column reductions (bias gradient / BatchNorm statistics) ----
-  // scratch after the tile image: [NT/(BN/4)][BN] partials + [BN] results
-  float* red = T + BM * TLD;
+  float* red = T + BMH * TLD;
   float* colres = red + (NT / (BN / 4)) * BN;
-  __syncthreads();
-  quad_colsum<BN, NT>(red, cs, tid, colres);
-  if (p.epi != EPI_BNSTAT_BF16) {
-    if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
-    return;
-  }
-  // BatchNorm statistics of the stored (bf16-rounded) values: tile mean, then M2 = sum (y - mean)^2.
-  const int rows_valid = min(BM, p.M - m0);
-  float* tmean = colres + BN;
-  if (tid < BN) tmean[tid] = colres[tid] / (float)rows_valid;
-  __syncthreads();
-  {
-    constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BM / RSTEP;
-    const int cq = tid % Q, r0 = tid / Q;
-    float m2[4] = {0.f, 0.f, 0.f, 0.f};
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int r = r0 + i * RSTEP;
-      if (m0 + r >= p.M) continue;
+  for (int h = 0; h < EH; ++h) {
+    if (h == 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
+    else __syncthreads();                      // the previous half's epilogue is done with T
+    if (wm / WPH == h) {
+      const int mr = (wm % WPH) * (BM / WGM) + 4 * (lane >> 4);
+      const int nc = wn * (BN / 2) + (lane & 15);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float y = bf2f(f2bf(T[r * TLD + 4 * cq + q] * p.alpha));
-        const float d = y - tmean[4 * cq + q];
-        m2[q] += d * d;
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) T[(mr + i * 16 + r) * TLD + nc + j * 16] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int mh = m0 + h * BMH;
+    float ch[4] = {0.f, 0.f, 0.f, 0.f};
+    switch (p.epi) {
+      case EPI_F32: epilogue_vec<EPI_F32, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_BF16: epilogue_vec<EPI_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_SGD:
+        epilogue_vec<EPI_SGD, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch,
+                                           SGDPF ? reinterpret_cast<const float*>(smem + STAGES * SLOT) : nullptr);
+        break;
+      case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      default: epilogue_vec<EPI_RELUMASK_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs[q] += ch[q];
+    if (p.colsum && p.epi == EPI_BNSTAT_BF16) {
+      // BatchNorm statistics of the stored (bf16-rounded) values per BMH-row stat tile (tm*EH + h):
+      // tile mean, then M2 = sum (y - mean)^2 over this half's rows.
+      __syncthreads();
+      quad_colsum<BN, NT>(red, ch, tid, colres);
+      const int rows_valid = min(BMH, p.M - mh);
+      float* tmean = colres + BN;
+      if (tid < BN) tmean[tid] = rows_valid > 0 ? colres[tid] / (float)rows_valid : 0.f;
+      __syncthreads();
+      {
+        constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BMH / RSTEP;
+        const int cq = tid % Q, r0 = tid / Q;
+        float m2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int r = r0 + i * RSTEP;
+          if (mh + r >= p.M) continue;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float y = bf2f(f2bf(T[r * TLD + 4 * cq + q] * p.alpha));
+            const float d = y - tmean[4 * cq + q];
+            m2[q] += d * d;
+          }
+        }
+        quad_colsum<BN, NT>(red, m2, tid, colres);
+      }
+      const size_t st = (size_t)tm * EH + h;
+      if (tid < BN && n0 + tid < p.N) {
+        p.colsum[(st * 2) * p.N + n0 + tid] = tmean[tid];
+        p.colsum[(st * 2 + 1) * p.N + n0 + tid] = colres[tid];
       }
     }
-    quad_colsum<BN, NT>(red, m2, tid, colres);
   }
-  if (tid < BN && n0 + tid < p.N) {
-    p.colsum[((size_t)tm * 2) * p.N + n0 + tid] = tmean[tid];
-    p.colsum[((size_t)tm * 2 + 1) * p.N + n0 + tid] = colres[tid];
-  }
+  if (!p.colsum || p.epi == EPI_BNSTAT_BF16) return;
+
+  // ---- per-tile column sums (bias gradient) ----
+  __syncthreads();
+  quad_colsum<BN, NT>(red, cs, tid, colres);
+  if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
 }
 
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
@@ -530,10 +549,13 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Row-parts the epilogue stages the tile in (BatchNorm statistics come out per part).
+static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
+
 static inline void tile_of(int cfg, int* bm, int* bn) {
-  static const int t[13][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
-                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64}};
-  const int c = (cfg >= 0 && cfg <= 12) ? cfg : 7;
+  static const int t[14][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
+                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256}};
+  const int c = (cfg >= 0 && cfg <= 13) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
 }
@@ -546,6 +568,7 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 10: return launch<64, 128, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s); // BK 128, 96 KiB
     case 11: return launch<128, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s); // BK 128, 96 KiB
     case 12: return launch<64, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s);  // BK 128, 64 KiB (2 WG/CU)
+    case 13: return launch<256, 256, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 64x128 each, 128 KiB
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
     case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB

@@ -41,6 +41,7 @@ class Trainer:
         self.train_data = train_data
         self.optimizer = optimizer
         self.save_every = save_every
+        self._one = None
         self._device_lr = False  # LR schedule tabulated on the device (set at train start)
         self.fault_step = None  # fault injection
         self.scheduler = scheduler
@@ -72,7 +73,9 @@ class Trainer:
         with trace_range("forward"):
             loss = self._forward_loss(source, targets)
         with trace_range("backward"):
-            loss.backward()
+            if self._one is None or self._one.device != loss.device:
+                self._one = torch.ones((), device=loss.device, dtype=loss.dtype)
+            loss.backward(self._one)  # preallocated seed gradient: no fill kernel inside the step
         with trace_range("optimizer"):
             self.optimizer.step()
         return loss

@@ -14,7 +14,7 @@ def _rand_bf16(*shape, dev):
 
 
 @pytest.mark.parametrize("impl_tile", [("v1", -1), ("v1", 0), ("v1", 1), ("v1", 2), ("v1", 3)] +
-                         [("pipe", t) for t in range(-1, 13)])
+                         [("pipe", t) for t in range(-1, 14)])
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
                                  (200, 136, 1000)])
