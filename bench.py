@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--json_out", default=None)
     p.add_argument("--ddp_single", action="store_true",
                    help="N=1: still run the DDP machinery (RCCL reducer at world size 1) to measure its overhead")
+    p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                   help="host: gloo-staged collectives so several ranks can share one GPU (logic rehearsal on a "
+                        "1-GPU box; not graph-capturable, not a performance path)")
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args()
 
@@ -78,7 +81,8 @@ def baseline_value(metric_key: str):
         return None
 
 
-def setup_dist(n, impl):
+def setup_dist(args):
+    n, impl = args.gpus, args.impl
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -86,8 +90,10 @@ def setup_dist(n, impl):
         if n > 1 and world == 1:
             print(f"bench.py: --gpus {n} needs a launcher (torchrun --nproc-per-node {n})", file=sys.stderr)
             sys.exit(2)
+    if args.comm == "host":
+        local = local % torch.cuda.device_count()  # ranks may share a device
     torch.cuda.set_device(local)
-    if world > 1 or (n == 1 and "--ddp_single" in sys.argv):
+    if world > 1 or (n == 1 and args.ddp_single):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1 and "MASTER_PORT" not in os.environ:
             import socket
@@ -131,7 +137,7 @@ def build_ddpx(args, device, world):
     from ddpx.models import build_model
     from ddpx.optim.schedule import one_cycle, resolve_steps_per_epoch
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import RcclComm
+    from ddpx.parallel.comm import HostStagedComm, RcclComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
@@ -143,7 +149,8 @@ def build_ddpx(args, device, world):
               fused_backward=(world == 1 and not args.ddp_single and not args.no_fused_optimizer))
     net = model
     if world > 1 or args.ddp_single:
-        net = DistributedDataParallel(model, comm=RcclComm(device), bucket_cap_mb=args.bucket_cap_mb,
+        comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
+        net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=bool(args.overlap_optimizer),
@@ -181,8 +188,10 @@ def build_torch(args, device, world):
 
 def main():
     args = parse()
-    rank, world, local = setup_dist(args.gpus, args.impl)
+    rank, world, local = setup_dist(args)
     resolve_defaults(args, world)
+    if args.comm == "host":
+        args.no_graph = True
     device = torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
     idx_all = loader._epoch_indices()

@@ -129,6 +129,54 @@ class TorchComm(Comm):
             dist.all_gather(list(out.chunk(self.world_size)), inp.clone(), group=self.group)
 
 
+class HostStagedComm(TorchComm):
+    """GPU tensors reduced through a CPU gloo group (synchronous, staged in fp32 host copies).
+
+    Not a production path: RCCL refuses two ranks on one device, so this is how several ranks
+    sharing ONE MI355X exercise the multi-rank DDP / ZeRO-1 logic together with the native
+    kernels (``tests/test_gpu_multirank.py``, ``bench.py --comm host``).  Not graph-capturable.
+    """
+
+    def __init__(self, group=None):
+        super().__init__(group)
+
+    def _host(self, t):
+        return t.detach().to("cpu", torch.float32 if t.is_floating_point() else t.dtype, copy=True)
+
+    def allreduce_(self, t, op="avg", stream=None, async_op=False):
+        if self.world_size == 1:
+            return None
+        h = self._host(t)
+        rop = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+               "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(h, op=rop, group=self.group)
+        if op == "avg":
+            h.div_(self.world_size)
+        t.copy_(h)
+        return None
+
+    def broadcast_(self, t, src=0, stream=None):
+        if self.world_size > 1:
+            h = self._host(t)
+            dist.broadcast(h, src=src, group=self.group)
+            t.copy_(h)
+
+    def reduce_scatter(self, out, inp, op="avg", stream=None):
+        h = self._host(inp)
+        if self.world_size > 1:
+            dist.all_reduce(h, group=self.group)
+        r = h.chunk(self.world_size)[self.rank]
+        if op == "avg":
+            r = r / self.world_size
+        out.copy_(r)
+
+    def allgather(self, out, inp, stream=None):
+        h = self._host(inp)
+        parts = [torch.empty_like(h) for _ in range(self.world_size)]
+        dist.all_gather(parts, h, group=self.group)
+        out.copy_(torch.cat(parts))
+
+
 class _ScaleOnWait:
     def __init__(self, work, t, s):
         self.work, self.t, self.s = work, t, s
@@ -214,7 +262,12 @@ class RcclComm(Comm):
 
 
 def default_comm(device: torch.device | None = None) -> Comm:
-    """RcclComm for GPU tensors (unless DDPX_COMM=torch), TorchComm otherwise."""
-    if device is not None and torch.device(device).type == "cuda" and os.environ.get("DDPX_COMM", "rccl") == "rccl":
-        return RcclComm(device)
+    """RcclComm for GPU tensors (DDPX_COMM=torch: torch.distributed; DDPX_COMM=host: gloo-staged), TorchComm
+    otherwise."""
+    kind = os.environ.get("DDPX_COMM", "rccl")
+    if device is not None and torch.device(device).type == "cuda":
+        if kind == "rccl":
+            return RcclComm(device)
+        if kind == "host":
+            return HostStagedComm()
     return TorchComm()

@@ -8,11 +8,11 @@ import torch.nn.functional as F
 from tests._dist_util import free_port, init_gloo
 
 
-def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False):
+def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False, comm_kind="torch"):
     import ddpx
     from ddpx.models import VGG, DeepNN
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.comm import HostStagedComm, TorchComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from torch.nn.parallel import DistributedDataParallel as TorchDDP
     init_gloo(rank, ws, port)
@@ -26,7 +26,8 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False):
             ref.classifier[2].p = 0.0
         ref.load_state_dict(ours.state_dict())
         ddpx.prepare_model(ours, "cpu")
-        d_ours = DistributedDataParallel(ours, comm=TorchComm(), bucket_cap_mb=bucket_mb, first_bucket_mb=0.25,
+        d_ours = DistributedDataParallel(ours, comm=HostStagedComm() if comm_kind == "host" else TorchComm(),
+                                         bucket_cap_mb=bucket_mb, first_bucket_mb=0.25,
                                          overlap_optimizer=overlap, shard_optimizer=shard)
         d_ref = TorchDDP(ref, bucket_cap_mb=bucket_mb)
         if shard:
@@ -77,11 +78,17 @@ def test_ddp_matches_torch_ddp(ws, model, overlap, bucket, shard):
     mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3, shard), nprocs=ws, join=True)
 
 
+@pytest.mark.parametrize("shard", [False, True])
+def test_host_staged_comm_matches_torch_ddp(shard):
+    """HostStagedComm (the one-GPU multi-rank rehearsal comm) has the same semantics as gloo."""
+    mp.spawn(_worker, args=(2, free_port(), "deepnn", True, 1.0, 2, shard, "host"), nprocs=2, join=True)
+
+
 def _no_sync_worker(rank, ws, port):
     import ddpx
     from ddpx.models import DeepNN
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.comm import HostStagedComm, TorchComm
     from ddpx.parallel.ddp import DistributedDataParallel
     init_gloo(rank, ws, port)
     try:
@@ -139,7 +146,7 @@ def _syncbn_worker(rank, ws, port):
     import ddpx
     from ddpx.models import VGG
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.comm import HostStagedComm, TorchComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.parallel.sync_bn import SyncBatchNorm2d, convert_sync_batchnorm
     init_gloo(rank, ws, port)
