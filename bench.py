@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--batch_size", type=int, default=512, help="per-GPU batch")
     p.add_argument("--hidden", type=int, default=None, help="MLP hidden width (default 4096 toy, 16384 wide)")
     p.add_argument("--layers", type=int, default=3)
-    p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg"])
+    p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg", "deepnn"])
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
     p.add_argument("--fp8", type=int, default=0,
                    help="1: MX-FP8 hidden-layer forward/wgrad GEMMs (mlp models).  Off by default: on MI355X the "
@@ -114,7 +114,7 @@ def make_data(args, device, rank, world, layout=None):
     sampler = DistributedIndexSampler(len(ds), world, rank, shuffle=True, seed=0)
     if layout is None:
         layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
-        if args.impl == "ddpx" and args.model == "vgg":
+        if args.impl == "ddpx" and args.model in ("vgg", "deepnn"):
             layout = "nhwc8_bf16"
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
 
@@ -167,9 +167,9 @@ def build_torch(args, device, world):
     from torch.nn.parallel import DistributedDataParallel as TDDP
     from ddpx.optim.schedule import OneCycleLambda, resolve_steps_per_epoch
     torch.manual_seed(args.seed)
-    if args.model == "vgg":
-        from ddpx.models import VGG
-        model = VGG().to(device)
+    if args.model in ("vgg", "deepnn"):
+        from ddpx.models import VGG, DeepNN
+        model = (VGG if args.model == "vgg" else DeepNN)().to(device)
         if args.torch_amp:
             model = model.to(memory_format=torch.channels_last)
     else:
@@ -240,7 +240,7 @@ def main():
             b = full[k % len(full)]
             x, y = loader.make_batch(idx_all[b * bs:(b + 1) * bs], k)
             opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model != "vgg" or args.torch_amp):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model not in ("vgg", "deepnn") or args.torch_amp):
                 out = net(x)
             loss = torch.nn.functional.cross_entropy(out.float(), y)
             loss.backward()
@@ -283,12 +283,12 @@ def main():
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
     model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}", "mlp_wide": f"wide-mlp-3072x{args.hidden}x{args.layers}",
-                  "vgg": "vgg11-cifar"}[args.model]
+                  "vgg": "vgg11-cifar", "deepnn": "deepnn-cifar"}[args.model]
     base = baseline_value(f"{args.model}_x{world}") if args.impl == "ddpx" else None
     rec = {
         "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": (round(value / base, 4) if base else None), "dtype": ("mxfp8/bf16" if args.fp8 else "bf16") if (args.model != "vgg" or args.impl == "ddpx" or args.torch_amp) else "fp32",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": ("mxfp8/bf16" if args.fp8 else "bf16") if (args.model not in ("vgg", "deepnn") or args.impl == "ddpx" or args.torch_amp) else "fp32",
         "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),

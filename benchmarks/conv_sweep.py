@@ -16,6 +16,8 @@ from ddpx.ops import conv as K  # noqa: E402
 
 LAYERS = [(3, 64, 32), (64, 128, 32), (128, 256, 16), (256, 256, 16), (256, 512, 8), (512, 512, 8), (512, 512, 4),
           (512, 512, 4)]
+# the reference's DeepNN (/root/reference/singlegpu.py:21-31): (Ci, Co, H)
+DEEPNN_LAYERS = [(3, 128, 32), (128, 64, 32), (64, 64, 16), (64, 32, 16)]
 
 
 def timeit(fn, iters=10, warm=3):
@@ -35,11 +37,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--net", default="vgg", choices=["vgg", "deepnn"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N = a.batch
     res = []
-    for (Ci, Co, H) in LAYERS:
+    for (Ci, Co, H) in (LAYERS if a.net == "vgg" else DEEPNN_LAYERS):
         Cp = K.padded_channels(Ci)
         x = (torch.rand(N, H, H, Cp, device=dev) * 2 - 1).to(torch.bfloat16)
         w = torch.randn(Co, Ci, 3, 3, device=dev) * 0.05

@@ -281,12 +281,12 @@ bwd_finalize_kernel(const float* __restrict__ part, int B, int C, int M, float* 
   put(sb, dbeta, s1);
 }
 
-// Pass 2: dy = a * (gz - c1 - xhat * c2)   (bf16 [P][C])
+// Pass 2: dy = a * (gz - c1 - xhat * c2)   (bf16 [P][C]);  norm == 0: dy = gz (conv bias + ReLU only)
 __global__ void __launch_bounds__(256)
 bwd_apply_kernel(const unsigned short* __restrict__ gout, const unsigned short* __restrict__ y,
                  const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ mean,
                  const float* __restrict__ rstd, const float* __restrict__ c1, const float* __restrict__ c2, int N,
-                 int H, int W, int C, int pool, int relu, unsigned short* __restrict__ dy) {
+                 int H, int W, int C, int pool, int relu, int norm, unsigned short* __restrict__ dy) {
   const int G = C / 8;
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int P = N * H * W;
@@ -298,11 +298,16 @@ bwd_apply_kernel(const unsigned short* __restrict__ gout, const unsigned short* 
   for (int j = 0; j < 8; ++j) { av[j] = a[g * 8 + j]; bv[j] = b[g * 8 + j]; }
   unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
   grad_z(gout, y, av, bv, n, h, w, H, W, C, g, pool, relu, f, gz);
+  if (norm) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = g * 8 + j;
-    const float xh = (f[j] - mean[c]) * rstd[c];
-    out[j] = av[j] * (gz[j] - c1[c] - xh * c2[c]);
+    for (int j = 0; j < 8; ++j) {
+      const int c = g * 8 + j;
+      const float xh = (f[j] - mean[c]) * rstd[c];
+      out[j] = av[j] * (gz[j] - c1[c] - xh * c2[c]);
+    }
+  } else {  // bias + activation only (conv with bias, no BN): dy = routed, masked gradient
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = gz[j];
   }
   *reinterpret_cast<u32x4*>(dy + (size_t)pix * C + g * 8) = pack8(out);
 }
@@ -370,7 +375,29 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
                      SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
   const int n = N * H * W * (C / 8);
   hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu,
+                     (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu, 1,
+                     (unsigned short*)dy);
+  return (int)hipGetLastError();
+}
+
+// Backward of  out = [maxpool2](relu(y + bias))  — a 3x3 conv WITH bias followed by ReLU (and pool),
+// no BatchNorm: the reference's DeepNN blocks (/root/reference/singlegpu.py:21-31).  Same two
+// passes as BatchNorm with a = 1, b = bias, mean = 0, rstd = 1: pass 1 yields dbias = sum gz
+// (fixed-order, deterministic), pass 2 writes dy = gz for the conv dgrad / wgrad GEMMs.
+DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bias, const float* ones,
+                               const float* zeros, int N, int H, int W, int C, int pool, int relu, float* part,
+                               float* c1, float* c2, void* dbias, int out_bf16, int accumulate, void* dy,
+                               hipStream_t s) {
+  if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
+  const int B = ddpx_bn_bwd_blocks(N, H, W, C);
+  hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
+                     nullptr, dbias, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                     SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+  const int n = N * H * W * (C / 8);
+  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,
                      (unsigned short*)dy);
   return (int)hipGetLastError();
 }

@@ -159,8 +159,10 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
 
 static int pick_wgrad(int P, int C, int Co) {
   (void)P;
-  (void)Co;
   if (C <= 8) return 12;      // conv0 (K = 9 x 8): 64x64, BK 128
+  // M = Co <= 64 (DeepNN's 128->64, 64->64, 64->32 layers): a 256-row tile would be 3/4 empty;
+  // 64x64 / 3 stages measured 2.6x faster on 128->64@32 (profiles/r1_deepnn/conv_sweep_deepnn.json)
+  if (Co <= 64) return 7;
   if (C <= 64) return 0;      // conv1: 128x128, 4 stages
   return 8;                   // 256x128, 8 waves
 }

@@ -171,7 +171,9 @@ __global__ void __launch_bounds__(1024) mean_kernel(const float* __restrict__ x,
 
 // Backward partials.  Workgroup (column tile ct of 64, row split rs):
 //   g[m][k]  = go * sum_c dlogits[m][c] * W[c][k]
-//   dH[m][k] = relu_mask ? g * (H[m][k] > 0) : g                       (bf16, stored)
+//   dH[m][k] = hscale * (relu_mask ? g * (H[m][k] > 0) : g)             (bf16, stored)
+//   (hscale = 1/(1-p) when H is the output of an inverted Dropout(p) after a ReLU: H > 0 is then
+//    exactly "kept and positive", so the dropout + ReLU backward costs nothing extra)
 //   pdw[rs][c][k]  = go * sum_{m in split} dlogits[m][c] * H[m][k]
 //   pdb[rs][k]     = sum_{m in split} dH[m][k]     (bias grad of the layer that produced H)
 // 8 lanes x 8 columns per row, 32 rows per pass, ROWS_PER_SPLIT/32 passes.
@@ -180,7 +182,7 @@ __global__ void __launch_bounds__(256)
 head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
                         const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K,
                         int ldh, int rows_per_split, unsigned short* __restrict__ dH, float* __restrict__ pdw,
-                        float* __restrict__ pdb, float* __restrict__ pdbh, int relu_mask) {
+                        float* __restrict__ pdb, float* __restrict__ pdbh, int relu_mask, float hscale) {
   __shared__ float red[4][64][C + 1];
   __shared__ float redh[16][C];
   const float go = go_ptr ? *go_ptr : 1.f;
@@ -225,7 +227,7 @@ head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restri
 #pragma unroll
       for (int c = 0; c < C; ++c) s = fmaf(dl[c], wv[c][j], s);
       if (relu_mask && !(h[j] > 0.f)) s = 0.f;
-      g[j] = s;
+      g[j] = s * hscale;
 #pragma unroll
       for (int c = 0; c < C; ++c) dw[c][j] = fmaf(dl[c], h[j], dw[c][j]);
     }
@@ -394,7 +396,8 @@ DDPX_API int ddpx_mean(const float* x, int n, float* out, hipStream_t s) {
 }
 
 DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K, int C,
-                           int ldh, void* dH, void* dW, void* db, void* dbprev, int relu_mask, int out_bf16,
+                           int ldh, void* dH, void* dW, void* db, void* dbprev, int relu_mask, float hscale,
+                           int out_bf16,
                            int accumulate, float* scratch, float* sw_p, float* sw_buf, void* sw_sh, float* sb_p,
                            float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh, const float* lr,
                            float mom, float wd, hipStream_t s) {
@@ -408,7 +411,7 @@ DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H,
   float* pdbh = pdb + (size_t)rs * K;
   hipLaunchKernelGGL(head_bwd_partial_kernel<10>, dim3(K / 64, rs), dim3(256), 0, s, dlogits, go,
                      (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, rps, (unsigned short*)dH, pdw, pdb,
-                     pdbh, relu_mask);
+                     pdbh, relu_mask, hscale);
   hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + C + 255) / 256), dim3(256), 0, s, pdw, pdb,
                      pdbh, rs, K, dW, db, dbprev, out_bf16, accumulate,
                      SgdArgs{sw_p, sw_buf, (unsigned short*)sw_sh, lr, mom, wd},

@@ -22,6 +22,7 @@ def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", de
         m.use_native = kernels == "native" and dev.type == "cuda" and dtype != "fp32"
     elif name == "deepnn":
         m = DeepNN()
+        m.use_native = kernels == "native" and dev.type == "cuda" and dtype != "fp32"
     elif name in ("mlp", "mlp_wide"):
         h = hidden or (16384 if name == "mlp_wide" else 4096)
         m = MLP(hidden=h, layers=layers, compute_dtype=cdt)

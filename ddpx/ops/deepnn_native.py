@@ -1,0 +1,225 @@
+"""The reference's DeepNN as one autograd node on ddpx's MI355X kernels (NHWC, bf16 compute).
+
+``/root/reference/singlegpu.py:18-44`` (defined there, never instantiated):
+
+    features   : [conv3x3+bias → ReLU] x2 → MaxPool2 → [conv3x3+bias → ReLU] x2 → MaxPool2
+    classifier : flatten(C,H,W) → Linear(2048→512) → ReLU → Dropout(0.1) → Linear(512→10)
+
+Schedule:
+
+    forward : y  = conv3x3(x, W)                  implicit-GEMM MFMA (no BN statistics)
+              x' = [maxpool2](relu(y + bias))     fused elementwise pass (BN apply kernel, a = 1, b = bias)
+              f  = flatten in torch's (C,H,W) order (NHWC → NCHW view of 2048 features)
+              a0 = relu(f W0ᵀ + b0)               MFMA GEMM, bias+ReLU epilogue
+              d0 = dropout(a0)                    Philox kernel, device-resident (seed, offset)
+              loss, dlogits = head(d0, W1, b1)    fused Linear(512→10) + softmax cross-entropy
+    backward: dd0, dW1, db1, db0 = head_bwd(...)  dropout+ReLU backward folded in: mask = d0 > 0,
+                                                  scale 1/(1-p); db0 = Σ dd0 from the same kernel
+              dW0 = dd0ᵀ f,  df = dd0 W0          MFMA GEMMs
+              per conv block (reverse): dy, dbias = bias_act_bwd(g, y)  (pool routing + ReLU mask
+              recomputed from y); dW = wgrad(dy, x) (split-K MFMA); g = dgrad(dy, W)
+
+Gradients land in the flat store (DDP buckets) in grad-ready order, or — single process with
+``SGD(fused_backward=True)`` — weights are updated inside the kernels that produce their
+gradients (conv weights, Linear weights, classifier); conv biases are stepped by the optimizer.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import conv as K
+from . import gemm as G
+from .head import head_backward, head_forward
+from .vgg_native import _prep_input
+from ..runtime import native
+
+
+class _Plan:
+    def __init__(self, model):
+        mods = list(model.features.children())
+        self.blocks = []  # (conv, pool)
+        i = 0
+        while i < len(mods):
+            conv = mods[i]
+            assert isinstance(conv, nn.Conv2d) and conv.bias is not None and isinstance(mods[i + 1], nn.ReLU)
+            i += 2
+            pool = i < len(mods) and isinstance(mods[i], nn.MaxPool2d)
+            if pool:
+                i += 1
+            self.blocks.append((conv, pool))
+        cls = list(model.classifier.children())
+        self.lin0, self.drop, self.lin1 = cls[0], cls[2], cls[3]
+        assert isinstance(self.lin0, nn.Linear) and isinstance(self.drop, nn.Dropout) and isinstance(self.lin1,
+                                                                                                  nn.Linear)
+        dev = self.lin0.weight.device
+        self.wf, self.wd = [], []
+        for conv, _ in self.blocks:
+            Co, Ci = conv.weight.shape[:2]
+            n = Co * 9 * K.padded_channels(Ci)
+            self.wf.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
+            self.wd.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
+        cmax = max(c.weight.shape[0] for c, _ in self.blocks)
+        self.ones = torch.ones(cmax, dtype=torch.float32, device=dev)
+        self.zeros = torch.zeros(cmax, dtype=torch.float32, device=dev)
+        # dropout generator state on the device: [seed, offset] (+ workgroup completion counter)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.rng = torch.tensor([seed, 0], dtype=torch.int64, device=dev)
+        self.rng_done = torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+def plan_of(model):
+    p = getattr(model, "_ddpx_plan", None)
+    if p is None:
+        p = _Plan(model)
+        model._ddpx_plan = p
+    return p
+
+
+def dropout_(x, p, plan, out=None):
+    """Inverted dropout of a bf16 tensor with the plan's device-resident Philox state."""
+    _req = K._req
+    _req(x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0,
+         "dropout: x must be contiguous bf16 with numel % 8 == 0")
+    out = torch.empty_like(x) if out is None else out
+    native.check(native.kernels().ddpx_dropout_fwd(x.data_ptr(), out.data_ptr(), x.numel(), float(p),
+                                                   plan.rng.data_ptr(), plan.rng_done.data_ptr(),
+                                                   native.stream_handle()), "ddpx_dropout_fwd")
+    return out
+
+
+def bias_act_backward(gout, y, bias, N, H, W, C, pool, plan, dbias, accumulate=False):
+    """dy [N*H*W, C] bf16 and dbias (=|+=) Σ dy for out = [pool](relu(y + bias))."""
+    K._nhwc(gout, "gout", C)
+    K._nhwc(y, "y", C)
+    lib = native.kernels()
+    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
+    dev = y.device
+    part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
+    c1 = torch.empty(C, dtype=torch.float32, device=dev)
+    c2 = torch.empty(C, dtype=torch.float32, device=dev)
+    dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)
+    native.check(lib.ddpx_bias_act_bwd(gout.data_ptr(), y.data_ptr(), bias.data_ptr(), plan.ones.data_ptr(),
+                                       plan.zeros.data_ptr(), N, H, W, C, int(pool), 1, part.data_ptr(),
+                                       c1.data_ptr(), c2.data_ptr(), dbias.data_ptr(),
+                                       int(dbias.dtype == torch.bfloat16), int(accumulate), dy.data_ptr(),
+                                       native.stream_handle()), "ddpx_bias_act_bwd")
+    return dy
+
+
+def _forward(model, x, targets, want_logits, want_grad, training):
+    plan = plan_of(model)
+    flat = plan.lin0.weight._ddpx_flat
+    N, H, W, C = x.shape
+    saved = []
+    for bi, (conv, pool) in enumerate(plan.blocks):
+        Co = conv.weight.shape[0]
+        K.weight_prep(conv.weight, plan.wf[bi], plan.wd[bi])
+        y, _, _, _ = K.conv_fwd(x, plan.wf[bi], Co, stats=False)
+        xn = K.bn_apply(y, plan.ones, conv.bias, N, H, W, Co, relu=True, pool=pool)
+        saved.append((x, y, (N, H, W, C, Co), pool))
+        x = xn
+        H, W, C = xn.shape[1], xn.shape[2], Co
+    # torch.flatten(x, 1) of the NCHW tensor: features in (C, H, W) order
+    feat = x.permute(0, 3, 1, 2).reshape(N, C * H * W).contiguous()
+    a0 = G.linear_fwd(feat, flat.shadow_of(plan.lin0.weight), plan.lin0.bias, relu=True)
+    p = float(plan.drop.p)
+    drop = training and p > 0.0
+    d0 = dropout_(a0, p, plan) if drop else a0
+    loss, logits, dl = head_forward(d0, flat.shadow_of(plan.lin1.weight), plan.lin1.bias, targets,
+                                    want_logits=want_logits, want_grad=want_grad)
+    scale = 1.0 / (1.0 - p) if drop else 1.0
+    return saved, (x.shape, feat, d0, scale), loss, logits, dl
+
+
+def _backward(model, saved, last, dl, grad_out):
+    plan = plan_of(model)
+    flat = plan.lin0.weight._ddpx_flat
+    xshape, feat, d0, scale = last
+    l0, l1 = plan.lin0, plan.lin1
+    dd0 = torch.empty_like(d0)
+    sw, sb, sp = flat.fused_spec(l1.weight), flat.fused_spec(l1.bias), flat.fused_spec(l0.bias)
+    if sw is not None and sb is not None and sp is not None:
+        head_backward(dl, grad_out, d0, flat.shadow_of(l1.weight), None, None, dH=dd0, relu_mask=True,
+                      sgd_w=sw, sgd_b=sb, sgd_prev=sp, dh_scale=scale)
+        for q in (l1.weight, l1.bias, l0.bias):
+            flat.mark_updated(q)
+    else:
+        dW1, acc = flat.grad_target(l1.weight)
+        db1, acc1 = flat.grad_target(l1.bias)
+        db0, acc0 = flat.grad_target(l0.bias)
+        if not (acc == acc1 == acc0):
+            raise NotImplementedError("mixed gradient-accumulation state inside the DeepNN classifier")
+        head_backward(dl, grad_out, d0, flat.shadow_of(l1.weight), dW1, db1, dH=dd0, dbprev=db0, relu_mask=True,
+                      accumulate=acc, dh_scale=scale)
+        for q in (l1.weight, l1.bias, l0.bias):
+            flat.grad_done(q)
+    # data gradient first: it reads W0's shadow before a fused update rewrites it
+    dfeat = G.linear_dgrad(dd0, flat.shadow_of(l0.weight))
+    s0 = flat.fused_spec(l0.weight)
+    if s0 is not None:
+        G.linear_wgrad(dd0, feat, None, sgd=s0)
+        flat.mark_updated(l0.weight)
+    else:
+        dW0, acc = flat.grad_target(l0.weight)
+        G.linear_wgrad(dd0, feat, dW0, accumulate=acc)
+        flat.grad_done(l0.weight)
+    N, Hf, Wf, Cf = xshape
+    g = dfeat.view(N, Cf, Hf, Wf).permute(0, 2, 3, 1).contiguous()
+    for bi in range(len(plan.blocks) - 1, -1, -1):
+        conv, pool = plan.blocks[bi]
+        x, y, (N, H, W, C, Co), _ = saved[bi]
+        dbias, accb = flat.grad_target(conv.bias)
+        dy = bias_act_backward(g, y, conv.bias, N, H, W, Co, pool, plan, dbias, accumulate=accb)
+        flat.grad_done(conv.bias)
+        Cr = conv.weight.shape[1]
+        sc = flat.fused_spec(conv.weight)
+        if sc is not None:
+            K.conv_wgrad(dy, x, Co, Cr, sgd=sc)
+            flat.mark_updated(conv.weight)
+        else:
+            dw, accw = flat.grad_target(conv.weight)
+            K.conv_wgrad(dy, x, Co, Cr, out=dw, accumulate=accw)
+            flat.grad_done(conv.weight)
+        if bi > 0:
+            g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+
+
+class _DeepNNLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, targets, model, *params):
+        saved, last, loss, _, dl = _forward(model, x, targets, False, True, model.training)
+        ctx.model, ctx.saved, ctx.last, ctx.dl, ctx.n = model, saved, last, dl, len(params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        _backward(ctx.model, ctx.saved, ctx.last, ctx.dl, grad_loss)
+        ctx.saved = ctx.last = ctx.dl = None
+        return (None, None, None) + (None,) * ctx.n
+
+
+class _DeepNNLogits(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, model, *params):
+        saved, last, _, logits, _ = _forward(model, x, None, True, False, model.training)
+        ctx.model, ctx.saved, ctx.last, ctx.n = model, saved, last, len(params)
+        return logits
+
+    @staticmethod
+    def backward(ctx, grad_logits):
+        _backward(ctx.model, ctx.saved, ctx.last, grad_logits.float().contiguous(), None)
+        ctx.saved = ctx.last = None
+        return (None, None) + (None,) * ctx.n
+
+
+def deepnn_loss(model, x, targets):
+    return _DeepNNLoss.apply(_prep_input(x), targets, model, *model.parameters())
+
+
+def deepnn_forward(model, x):
+    x = _prep_input(x)
+    if not torch.is_grad_enabled():
+        _, _, _, logits, _ = _forward(model, x, None, True, False, model.training)
+        return logits
+    return _DeepNNLogits.apply(x, model, *model.parameters())

@@ -58,11 +58,13 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
 
 
 def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_mask=True, accumulate=False,
-                  sgd_w=None, sgd_b=None, sgd_prev=None):
+                  sgd_w=None, sgd_b=None, sgd_prev=None, dh_scale=1.0):
     """Backward of the fused head.
 
     dW [C,K] fp32, db [C] fp32 (=|+=); dH [M,K] bf16 = (grad · W) ⊙ (h>0 if relu_mask);
     dbprev [K] fp32 = Σ_m dH (bias gradient of the layer that produced h).
+    dh_scale: multiplies dH — 1/(1-p) when h is an inverted-Dropout(p) output of a ReLU (DeepNN's
+    classifier, ``/root/reference/singlegpu.py:33-38``): h > 0 is then the keep-and-positive mask.
     sgd_w / sgd_b / sgd_prev: fused optimizer targets (master, momentum, shadow, lr, mom, wd) that
     replace dW / db / dbprev (the gradients are applied instead of stored).
     """
@@ -82,6 +84,7 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
             gh = g @ w.float()
             if relu_mask:
                 gh = gh * (h > 0)
+            gh = gh * dh_scale
             dH.copy_(gh)
             if dbprev is not None:
                 s = dH.float().sum(0)
@@ -113,7 +116,7 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
     mom, wd = (sw[4], sw[5]) if fused else (0.0, 0.0)
     rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
                            native.ptr(dH), native.ptr(dW), native.ptr(db), native.ptr(dbprev), int(relu_mask),
-                           int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3], *sp[:3],
+                           float(dh_scale), int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3], *sp[:3],
                            lr_ptr, mom, wd, native.stream_handle())
     native.check(rc, "ddpx_head_bwd")
     return dH

@@ -62,8 +62,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_head_fwd_scratch", I64, I, I)
     _sig(lib, "ddpx_head_bwd_scratch", I64, I, I, I)
     _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P, P)
-    _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P, F, F,
-         P)
+    _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, F, I, I, P, P, P, P, P, P, P, P, P, P, P, F,
+         F, P)
     _sig(lib, "ddpx_mean", I, P, I, P, P)
     _sig(lib, "ddpx_accuracy", I, P, P, I, I, P, P)
     _sig(lib, "ddpx_augment", I, P, P, P, I, I, I, I, I, c_uint64, I, I, P, P, P)
@@ -79,6 +79,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_bn_apply", I, P, P, P, I, I, I, I, I, I, P, P)
     _sig(lib, "ddpx_bn_bwd_blocks", I, I, I, I, I)
     _sig(lib, "ddpx_bn_bwd", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_bias_act_bwd", I, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P)
+    _sig(lib, "ddpx_dropout_fwd", I, P, P, I64, F, P, P, P)
     _sig(lib, "ddpx_avgpool", I, P, I, I, I, P, P)
     _sig(lib, "ddpx_avgpool_bwd", I, P, I, I, I, P, P)
     for extra in _EXTRA_KERNEL_SIGS:

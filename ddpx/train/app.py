@@ -23,7 +23,7 @@ from ..data.sampler import DistributedIndexSampler
 from ..models import build_model
 from ..optim.schedule import one_cycle, resolve_steps_per_epoch
 from ..optim.sgd import SGD
-from ..parallel.comm import RcclComm, TorchComm
+from ..parallel.comm import HostStagedComm, RcclComm, TorchComm
 from ..parallel.sync_bn import convert_sync_batchnorm
 from ..parallel.ddp import DistributedDataParallel
 from ..runtime.setup import prepare_model
@@ -63,7 +63,8 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
     p.add_argument("--no_fused_optimizer", action="store_true",
                    help="single GPU: run SGD as its own pass instead of inside the backward kernels")
-    p.add_argument("--comm", default="rccl", choices=["rccl", "torch"], help="GPU collective backend")
+    p.add_argument("--comm", default="rccl", choices=["rccl", "torch", "host"],
+                   help="GPU collective backend (host: gloo-staged, lets several ranks share one GPU)")
     p.add_argument("--shard_optimizer", action="store_true",
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
@@ -190,6 +191,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
     if distributed:
         if device.type == "cuda" and args.comm == "rccl":
             comm = RcclComm(device)
+        elif device.type == "cuda" and args.comm == "host":
+            comm = HostStagedComm()
         else:
             comm = TorchComm()
     dataset, model, optimizer, testdata, scheduler = load_train_objs(
