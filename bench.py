@@ -59,6 +59,12 @@ def parse():
                    help="gradient buffer / reduction dtype (bf16 = values of the bf16 MFMA wgrads, as under "
                         "autocast); auto: fp32 at N=1 (grads never leave the fused kernels), bf16 for N>1")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
+    p.add_argument("--chunk_mb", type=float, default=None,
+                   help="split weights larger than this into row-chunk buckets, each reduced as soon as its "
+                        "slice of the weight gradient is written (default 64 for the wide MLP at N>1, else off)")
+    p.add_argument("--defer_gather", type=int, default=None,
+                   help="1: ZeRO-1 all-gathers issued at the start of the next step and waited per chunk "
+                        "inside the forward (default 1 with --shard_optimizer on the MLPs)")
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
@@ -131,6 +137,14 @@ def resolve_defaults(args, world):
         # ZeRO-1 pays off where only the bf16 shadow must be all-gathered (MLP weights); the native
         # VGG reads fp32 masters (per-step weight repack), so it keeps the replicated all-reduce
         args.shard_optimizer = int(multi and args.model.startswith("mlp"))
+    if args.chunk_mb is None:
+        # row-chunk buckets pay only where one chunk's GEMM still fills the chip: the wide MLP's
+        # 16384-wide layers.  At the toy MLP's M = 512 rows a quarter-width forward / wgrad GEMM is
+        # launch- and fill-bound (measured 36 vs 34 us for a 1024-column chunk vs the whole 4096-column
+        # layer, profiles/r1_chunk), so the toy MLP keeps whole-layer buckets
+        args.chunk_mb = 64.0 if (multi and args.model == "mlp_wide") else 0.0
+    if args.defer_gather is None:
+        args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 
 
 def build_ddpx(args, device, world):
@@ -154,7 +168,8 @@ def build_ddpx(args, device, world):
                                       reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=bool(args.overlap_optimizer),
-                                      shard_optimizer=bool(args.shard_optimizer))
+                                      shard_optimizer=bool(args.shard_optimizer), chunk_mb=args.chunk_mb or None,
+                                      defer_gather=bool(args.defer_gather))
         if args.overlap_optimizer or args.shard_optimizer:
             net.attach_optimizer(opt)
     sched = one_cycle(opt, resolve_steps_per_epoch("compat", 0, world > 1))
@@ -295,7 +310,8 @@ def main():
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
                        " fused-into-backward" if (args.impl == "ddpx" and not multi and not args.no_fused_optimizer)
                        else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
-                   "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(final_loss, 4),
+                   "bucket_cap_mb": args.bucket_cap_mb, "chunk_mb": args.chunk_mb or None,
+                   "defer_gather": bool(args.defer_gather) if multi else None, "final_loss": round(final_loss, 4),
                    "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
                    "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
                    "replicas_consistent": consistent,

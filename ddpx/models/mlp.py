@@ -96,3 +96,9 @@ class MLP(nn.Module):
 
     def input_layout(self, device) -> str:
         return "flat_bf16" if self.native_active(device) else "nchw_f32"
+
+    @property
+    def ddpx_lazy_gather(self) -> bool:
+        """The native forward (``ddpx.ops.mlp``) announces every weight read (``FlatParams.before_read``),
+        so DDP may defer ZeRO all-gathers into it; the torch path reads parameters directly."""
+        return self.use_native and self.compute_dtype == torch.bfloat16 and self.fc0.weight.is_cuda

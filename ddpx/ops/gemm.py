@@ -132,8 +132,10 @@ def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, 
         epi = EPI_BIAS_F32 if bias is not None else EPI_F32
     if out is None:
         out = torch.empty((M, N), dtype=_OUT_DTYPE[epi], device=x.device)
-    _req(out.shape == (M, N) and out.is_contiguous() and out.dtype == _OUT_DTYPE[epi], "bad out tensor")
-    return gemm_raw(x, w, out, M=M, N=N, K=K, lda=x.stride(0), ldb=w.stride(0), ldc=N, a_kcontig=True,
+    # out may be a column slice of a wider activation (row-chunked weights): row-contiguous is enough
+    _req(tuple(out.shape) == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0
+         and out.data_ptr() % 16 == 0 and out.dtype == _OUT_DTYPE[epi], "bad out tensor")
+    return gemm_raw(x, w, out, M=M, N=N, K=K, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), a_kcontig=True,
                     b_kcontig=True, epi=epi, bias=bias, tile=tile)
 
 

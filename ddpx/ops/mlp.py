@@ -55,6 +55,18 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
         for_backward = want_grad
     saved8 = [] if (fp8 and for_backward) else None
     for (w, b) in ps[:-1]:
+        rc = None if fp8 else flat.chunks_of(w)
+        if rc is not None:
+            # row-chunked weight (DDP chunk buckets, deferred ZeRO gathers): each chunk's output columns
+            # are computed as soon as that chunk's all-gather has landed
+            h = torch.empty((hs[-1].shape[0], w.shape[0]), dtype=torch.bfloat16, device=hs[-1].device)
+            sw = flat.shadow_of(w)
+            for c, (r0, r1) in enumerate(rc):
+                flat.before_read(w, c)
+                G.linear_fwd(hs[-1], sw[r0:r1], b[r0:r1], relu=True, out=h[:, r0:r1])
+            hs.append(h)
+            continue
+        flat.before_read(w)
         if fp8:
             from . import fp8 as F8
             if for_backward:
@@ -67,6 +79,7 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
         else:
             hs.append(G.linear_fwd(hs[-1], flat.shadow_of(w), b, relu=True))
     wl, bl = ps[-1]
+    flat.before_read(wl)
     loss, logits, dl = head_forward(hs[-1], flat.shadow_of(wl), bl, targets, want_logits=want_logits,
                                     want_grad=want_grad)
     return hs, loss, logits, dl, saved8
@@ -127,8 +140,16 @@ def _backward(model, hs, dl, grad_out, saved8=None):
     for l in range(L - 1, -1, -1):
         w, _ = ps[l]
         dWl, accw = flat.grad_target(w)
-        _wgrad(saved8, l, dpre, hs[l], dWl, accumulate=accw)
-        flat.grad_done(w)
+        rc = None if saved8 else flat.chunks_of(w)
+        if rc is None:
+            _wgrad(saved8, l, dpre, hs[l], dWl, accumulate=accw)
+            flat.grad_done(w)
+        else:
+            # one weight-gradient GEMM per row chunk, each announced at once: that chunk's bucket
+            # collective (reduce-scatter / all-reduce) overlaps the remaining chunks and the dgrad
+            for c, (r0, r1) in enumerate(rc):
+                G.linear_wgrad(dpre[:, r0:r1], hs[l], dWl[r0:r1], accumulate=accw)
+                flat.grad_done(w, chunk=c)
         if l > 0:
             bp = ps[l - 1][1]
             dbl, accl = flat.grad_target(bp)

@@ -69,6 +69,47 @@ def compute_bucket_assignment(sizes_bytes, limits_bytes):
     return buckets
 
 
+def plan_buckets(order, sizes_bytes, limits_bytes, chunked=()):
+    """torch's greedy rule over ``order``; a parameter in ``chunked`` closes the open bucket and becomes
+    its own entry ("c", i) (expanded into one bucket per row chunk); others group as ("p", [i, ...])."""
+    out, cur, cur_size, li = [], [], 0, 0
+    for i in order:
+        if i in chunked:
+            if cur:
+                out.append(("p", cur))
+                cur, cur_size = [], 0
+                li += 1
+            out.append(("c", i))
+            li += 1
+            continue
+        cur.append(i)
+        cur_size += sizes_bytes[i]
+        if cur_size >= limits_bytes[min(li, len(limits_bytes) - 1)]:
+            out.append(("p", cur))
+            cur, cur_size = [], 0
+            li += 1
+    if cur:
+        out.append(("p", cur))
+    return out
+
+
+def row_chunks(shape, elem_bytes, chunk_bytes, pad):
+    """Row ranges of ~chunk_bytes for a parameter of ``shape``; every chunk boundary is a multiple of
+    ``pad`` elements (equal aligned shards per chunk) and of 64 rows' worth of 16-B column offsets."""
+    import math
+    rows = shape[0]
+    cols = 1
+    for d in shape[1:]:
+        cols *= d
+    g = pad // math.gcd(cols, pad)
+    g = g * 64 // math.gcd(g, 64)  # also a multiple of 64 rows (aligned column slices of dY)
+    n = max(1, round(rows * cols * elem_bytes / max(1, chunk_bytes)))
+    per = -(-(-(-rows // n)) // g) * g  # ceil(rows / n), rounded up to the granule: near-equal chunks
+    if per >= rows:
+        return None
+    return [(r, min(rows, r + per)) for r in range(0, rows, per)]
+
+
 class FlatBuffers:
     """Module buffers rebound as views of one flat tensor per dtype (broadcast in one call each)."""
 
@@ -228,7 +269,8 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, comm: Comm | None = None,
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
-                 reduce_single: bool = False, shard_optimizer: bool = False):
+                 reduce_single: bool = False, shard_optimizer: bool = False, chunk_mb: float | None = None,
+                 defer_gather: bool = False):
         super().__init__()
         self.module = module
         dev = next(module.parameters()).device
@@ -268,21 +310,62 @@ class DistributedDataParallel(nn.Module):
         self.sharded = bool(shard_optimizer and active)
         esz = self.flat.grad.element_size()
         limits = [int(first_bucket_mb * 1024 * 1024), int(bucket_cap_mb * 1024 * 1024)]
+        # big weights split into row chunks, each its own bucket (its collective starts as soon as that
+        # chunk's gradient is written; producers that do not announce chunks complete them all at once)
+        pad = self.world_size * ALIGN if self.sharded else ALIGN
+        chunk_plan = {}
+        if chunk_mb and active:
+            for i, p in enumerate(self.flat.params):
+                if p.dim() >= 2 and p.numel() * esz > chunk_mb * 1024 * 1024:
+                    rc = row_chunks(tuple(p.shape), esz, int(chunk_mb * 1024 * 1024), pad)
+                    if rc:
+                        chunk_plan[id(p)] = rc
         if self.sharded:
-            assign, modes = self._shard_layout(limits, esz)
+            plan, modes = self._shard_layout(limits, esz, chunk_plan)
         else:
             sizes = [n * esz for n in self.flat.numels]
-            assign = compute_bucket_assignment(sizes, limits)
-            modes = [0] * len(assign)
+            chunked = {i for i, p in enumerate(self.flat.params) if id(p) in chunk_plan}
+            plan = plan_buckets(range(len(self.flat.params)), sizes, limits, chunked)
+            modes = None
+        for p in self.flat.params:
+            self.flat.set_chunks(p, chunk_plan.get(id(p)))
+        # expand the plan into buckets: (param list, chunk index or None, flat range)
+        f = self.flat
+        assign, ranges, expected, chunk_ids, bmodes = [], [], [], [], []
+        self.bucket_of = [0] * len(f.params)
+        self.chunk_bucket = {}
+        for k, entry in enumerate(plan):
+            mode = modes[k] if modes is not None else 0
+            if entry[0] == "p":
+                idxs = entry[1]
+                for i in idxs:
+                    self.bucket_of[i] = len(assign)
+                assign.append(list(idxs))
+                ranges.append(f.span(idxs[0], idxs[-1]))
+                expected.append(len(idxs))
+                chunk_ids.append(None)
+                bmodes.append(mode)
+            else:
+                i = entry[1]
+                rc = f.chunk_rows[i]
+                cols = f.numels[i] // f.params[i].shape[0]
+                s0, e0 = f.span(i, i)
+                if self.sharded:
+                    e0 = f.group_spans[k][1]
+                self.chunk_bucket[i] = []
+                for c, (r0, r1) in enumerate(rc):
+                    self.chunk_bucket[i].append(len(assign))
+                    self.bucket_of[i] = len(assign)
+                    assign.append([i])
+                    ranges.append((s0 + r0 * cols, e0 if c == len(rc) - 1 else s0 + r1 * cols))
+                    expected.append(1)
+                    chunk_ids.append(c)
+                    bmodes.append(mode)
+        modes = bmodes
         self.bucket_params = assign
         self.bucket_modes = modes
-        self.bucket_of = [0] * len(self.flat.params)
-        ranges, expected = [], []
-        for b, idxs in enumerate(assign):
-            for i in idxs:
-                self.bucket_of[i] = b
-            ranges.append(self.flat.span(idxs[0], idxs[-1]))
-            expected.append(len(idxs))
+        self.bucket_chunk = chunk_ids
+        self.bucket_expected = expected
         self.bucket_ranges = ranges
         if active:
             cls = _NativeReducer if isinstance(comm, RcclComm) else _PyReducer
@@ -306,9 +389,22 @@ class DistributedDataParallel(nn.Module):
         self.debug = os.environ.get("DDPX_DEBUG", "0") == "1"
         self.flat.sink = self
         self._completion_order = []
+        self._marks = [0] * len(self.bucket_ranges)
+        # deferred all-gather (ZeRO-1 shadow gathers): the optimizer leaves the gathers of the updated
+        # shards to the NEXT forward, which issues them first thing, in forward order, and waits per
+        # bucket right before the first read, so the traffic overlaps the forward GEMMs (and, captured
+        # in one HIP graph per step, still overlaps: issue and waits live in the same replay)
+        self.defer_gather = bool(defer_gather and self.sharded and self.gather_what == "shadow")
+        self._gather_todo = []
+        self._gather_wait = set()
+        if self.sharded:
+            def fwd_key(b):
+                return (-max(self.bucket_params[b]), self.bucket_chunk[b] or 0)
+            self._gather_order = sorted([b for b, m in enumerate(self.bucket_modes) if m == 1], key=fwd_key)
 
-    def _shard_layout(self, limits, esz):
-        """Re-pack the flat store for ZeRO-1 (see module docstring); returns (bucket params, modes)."""
+    def _shard_layout(self, limits, esz, chunk_plan):
+        """Re-pack the flat store for ZeRO-1 (see module docstring); returns (bucket plan, modes) in the
+        new parameter indices (a chunked parameter is one group, expanded into chunk buckets later)."""
         f = self.flat
         if f.shadow is not None and f.shadow_only:
             S = [i for i, p in enumerate(f.params) if id(p) in f.shadow_only]
@@ -317,18 +413,24 @@ class DistributedDataParallel(nn.Module):
             S = list(range(len(f.params)))
             self.gather_what = "master"
         R = [i for i in range(len(f.params)) if i not in set(S)]
-        groups = [[S[j] for j in g] for g in compute_bucket_assignment([f.numels[i] * esz for i in S], limits)]
+        chunked = {i for i in S if id(f.params[i]) in chunk_plan}
+        sizes = {i: f.numels[i] * esz for i in S}
+        plan = plan_buckets(S, sizes, limits, chunked)
+        groups = [e[1] if e[0] == "p" else [e[1]] for e in plan]
+        kinds = [e[0] for e in plan]
         modes = [1] * len(groups)
         if R:
             groups.append(R)  # fp32-read params: one replicated (all-reduced) bucket, produced last
+            kinds.append("p")
             modes.append(0)
         f.relayout(groups, pad_to=self.world_size * ALIGN)
         self._gather_src = f.shadow if self.gather_what == "shadow" else f.master
-        assign, k = [], 0
-        for g in groups:
-            assign.append(list(range(k, k + len(g))))
+        out, k = [], 0
+        for g, kind in zip(groups, kinds):
+            idxs = list(range(k, k + len(g)))
+            out.append(("p", idxs) if kind == "p" else ("c", idxs[0]))
             k += len(g)
-        return assign, modes
+        return out, modes
 
     # ------------------------------------------------------- sharded optimizer
     def bucket_order(self):
@@ -339,6 +441,9 @@ class DistributedDataParallel(nn.Module):
 
     def wait_bucket(self, b):
         self.reducer.wait_bucket(b)
+        if b in self._gather_wait:  # the shard about to be updated must not race its pending gather
+            self.reducer.wait_gather(b)
+            self._gather_wait.discard(b)
 
     def update_ranges(self, b):
         s, e = self.bucket_ranges[b]
@@ -349,9 +454,43 @@ class DistributedDataParallel(nn.Module):
 
     def gather_bucket(self, b):
         if self.bucket_modes[b] == 1:
-            self.reducer.gather(b)
+            if self.defer_gather:
+                self._gather_todo.append(b)
+            else:
+                self.reducer.gather(b)
+
+    def _issue_gathers(self):
+        todo = set(self._gather_todo)
+        self._gather_todo = []
+        for b in self._gather_order:
+            if b in todo:
+                self.reducer.gather(b)
+                self._gather_wait.add(b)
+
+    def _wait_gathers(self, buckets=None):
+        for b in (sorted(self._gather_wait) if buckets is None else buckets):
+            if b in self._gather_wait:
+                self.reducer.wait_gather(b)
+                self._gather_wait.discard(b)
+
+    def flush_gathers(self):
+        """Complete every deferred all-gather (before eval, checkpoints, or handing weights out)."""
+        if self._gather_todo:
+            self._issue_gathers()
+        self._wait_gathers()
+
+    def before_read(self, i, chunk=None):
+        if not self._gather_wait:
+            return
+        if i in self.chunk_bucket:
+            bs = self.chunk_bucket[i] if chunk is None else [self.chunk_bucket[i][chunk]]
+        else:
+            bs = [self.bucket_of[i]]
+        self._wait_gathers(bs)
 
     def _join_gathers(self):
+        if self.defer_gather:
+            return
         for b, m in enumerate(self.bucket_modes):
             if m == 1:
                 self.reducer.wait_gather(b)
@@ -369,6 +508,7 @@ class DistributedDataParallel(nn.Module):
         """
         if not self.sharded:
             return
+        self.flush_gathers()
         tensors = [self.flat.master] + list(self.flat.state_tensors.values())
         for b, (s, e) in enumerate(self.bucket_ranges):
             if self.bucket_modes[b] != 1:
@@ -399,11 +539,16 @@ class DistributedDataParallel(nn.Module):
     # ---------------------------------------------------------------- forward
     def _pre_forward(self):
         self.comm.check()
+        if self._gather_todo:
+            self._issue_gathers()
+            if not getattr(self.module, "ddpx_lazy_gather", False):
+                self._wait_gathers()  # the model's ops do not announce reads: wait for everything now
         if torch.is_grad_enabled() and self.reducer is not None and self._sync_enabled:
             if self._overlap_pending:
                 raise RuntimeError("DDP: optimizer.step() did not consume the previous iteration's buckets")
             self.reducer.prepare()
             self._completion_order = []
+            self._marks = [0] * len(self.bucket_ranges)
         self._queued = False
         if self.module.training:
             self._sync_buffers()
@@ -426,27 +571,27 @@ class DistributedDataParallel(nn.Module):
             self._sync_enabled = old
 
     # ------------------------------------------------------ gradient protocol
-    def grad_ready(self, i: int):
+    def grad_ready(self, i: int, chunk=None):
         if self.reducer is None or not self._sync_enabled:
             return
         if not self._queued:
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
-        b = self.bucket_of[i]
-        self.reducer.mark_ready(b, 1)
-        if self.reducer_launched(b):
-            self._completion_order.append(b)
+        if i in self.chunk_bucket:
+            bs = self.chunk_bucket[i] if chunk is None else [self.chunk_bucket[i][chunk]]
+        else:
+            bs = [self.bucket_of[i]]
+        for b in bs:
+            self._marks[b] += 1
+            self.reducer.mark_ready(b, 1)
+            if self._marks[b] == self.bucket_expected[b]:
+                self._completion_order.append(b)
 
     def reducer_launched(self, b):
-        r = self.reducer
-        if isinstance(r, _PyReducer):
-            return r.launched[b]
-        # native: the bucket launched iff all its params have been marked
         return self._marks_complete(b)
 
     def _marks_complete(self, b):
-        idxs = self.bucket_params[b]
-        return all(self.flat.written[i] for i in idxs)
+        return self._marks[b] == self.bucket_expected[b]
 
     def _finalize(self):
         if self.reducer is None:

@@ -89,6 +89,9 @@ class FlatParams:
         self.state_tensors = {}
         self.layout_version = 0
         self.group_spans = None
+        # row-chunked parameters (DDP splits big weights into per-chunk buckets): index -> [(r0, r1)]
+        self.chunk_rows = {}
+        self._chunks_done = {}
         self._warned_unused = False
         self._hooks = []
         for p in self.params:
@@ -129,6 +132,7 @@ class FlatParams:
         if pad_to % ALIGN:
             raise ValueError("pad_to must be a multiple of the alignment")
         new_params = [self.params[i] for i in order]
+        old_params = list(self.params)
         offsets, spans, off, k = [], [], 0, 0
         for g in groups:
             start = off
@@ -167,9 +171,33 @@ class FlatParams:
         self.refresh_shadow()
         self.written = [False] * len(self.params)
         self.updated = [False] * len(self.params)
+        self.chunk_rows = {self.index[id(p)]: r for p, r in ((old_params[i], r) for i, r in self.chunk_rows.items())}
+        self._chunks_done = {}
         self.group_spans = spans
         self.layout_version += 1
         return spans
+
+    # -- row chunks --------------------------------------------------------------
+    def set_chunks(self, p, ranges):
+        """Declare p's gradient/parameter as row chunks [(r0, r1), ...] (dim 0), each its own DDP bucket.
+
+        Producers that know about chunks announce them one by one (``grad_done(p, chunk=c)``) so each
+        chunk's collective starts while the rest of the gradient is still being computed; producers that
+        do not simply call ``grad_done(p)``, which completes every chunk."""
+        i = self.index[id(p)]
+        if ranges:
+            self.chunk_rows[i] = list(ranges)
+        else:
+            self.chunk_rows.pop(i, None)
+
+    def chunks_of(self, p):
+        return self.chunk_rows.get(self.index[id(p)])
+
+    def before_read(self, p, chunk=None):
+        """Called by native ops right before they read p (or its row chunk) in a forward: a sharded
+        optimizer with deferred all-gathers makes the current stream wait for that data here."""
+        if self.sink is not None and hasattr(self.sink, "before_read"):
+            self.sink.before_read(self.index[id(p)], chunk)
 
     # -- gradient protocol -----------------------------------------------------
     def grad_target(self, p):
@@ -196,11 +224,30 @@ class FlatParams:
         self.updated[i] = True
         self.written[i] = True
 
-    def grad_done(self, p):
+    def grad_done(self, p, chunk=None):
         i = self.index[id(p)]
+        if chunk is not None and i in self.chunk_rows:
+            done = self._chunks_done.setdefault(i, set())
+            if chunk in done:
+                raise RuntimeError(f"chunk {chunk} of {self.names.get(id(p), i)} announced twice")
+            done.add(chunk)
+            if len(done) == len(self.chunk_rows[i]):
+                self.written[i] = True
+                del self._chunks_done[i]
+            if self.sink is not None:
+                self.sink.grad_ready(i, chunk)
+            return
+        if i in self._chunks_done:  # remaining chunks of a partially announced parameter
+            rest = [c for c in range(len(self.chunk_rows[i])) if c not in self._chunks_done.pop(i)]
+        else:
+            rest = None
         self.written[i] = True
         if self.sink is not None:
-            self.sink.grad_ready(i)
+            if rest is None:
+                self.sink.grad_ready(i)
+            else:
+                for c in rest:
+                    self.sink.grad_ready(i, c)
 
     def _on_accumulated(self, p):
         i = self.index[id(p)]
@@ -217,6 +264,7 @@ class FlatParams:
             self.sink.grad_ready(i)
 
     def zero_grad(self):
+        self._chunks_done = {}
         self.written = [False] * len(self.params)
         self.updated = [False] * len(self.params)
         for p in self.params:

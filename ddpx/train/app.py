@@ -67,6 +67,11 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                    help="GPU collective backend (host: gloo-staged, lets several ranks share one GPU)")
     p.add_argument("--shard_optimizer", action="store_true",
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
+    p.add_argument("--chunk_mb", type=float, default=None,
+                   help="split weights larger than this (MB of gradient) into row-chunk DDP buckets")
+    p.add_argument("--defer_gather", action="store_true",
+                   help="with --shard_optimizer: all-gather updated shards at the start of the next forward, "
+                        "overlapped with it (MLP native path)")
     p.add_argument("--sync_bn", action="store_true", help="SyncBatchNorm (reference: commented out)")
     p.add_argument("--resume", action="store_true", help=f"resume from {FULL_CKPT_PATH}")
     p.add_argument("--full_checkpoint", action="store_true", help=f"also write {FULL_CKPT_PATH}")
@@ -204,7 +209,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=args.overlap_optimizer,
-                                      shard_optimizer=args.shard_optimizer)
+                                      shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
+                                      defer_gather=args.defer_gather)
         if args.overlap_optimizer:
             net.attach_optimizer(optimizer)
     metrics = MetricsWriter(args.metrics, rank) if args.metrics else None

@@ -8,7 +8,7 @@ import torch.nn.functional as F
 from tests._dist_util import free_port, init_gloo
 
 
-def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False, comm_kind="torch"):
+def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False, comm_kind="torch", chunk_mb=None):
     import ddpx
     from ddpx.models import VGG, DeepNN
     from ddpx.optim.sgd import SGD
@@ -28,7 +28,13 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False, 
         ddpx.prepare_model(ours, "cpu")
         d_ours = DistributedDataParallel(ours, comm=HostStagedComm() if comm_kind == "host" else TorchComm(),
                                          bucket_cap_mb=bucket_mb, first_bucket_mb=0.25,
-                                         overlap_optimizer=overlap, shard_optimizer=shard)
+                                         overlap_optimizer=overlap, shard_optimizer=shard, chunk_mb=chunk_mb)
+        if chunk_mb:
+            assert d_ours.chunk_bucket, "expected row-chunked buckets"
+            f = d_ours.flat
+            for i, bs in d_ours.chunk_bucket.items():
+                spans = [d_ours.bucket_ranges[b] for b in bs]
+                assert spans[0][0] == f.offsets[i] and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
         d_ref = TorchDDP(ref, bucket_cap_mb=bucket_mb)
         if shard:
             assert d_ours.sharded and all((e - s) % (ws * 64) == 0 for s, e in d_ours.bucket_ranges)
@@ -76,6 +82,33 @@ def _worker(rank, ws, port, model_name, overlap, bucket_mb, steps, shard=False, 
 ])
 def test_ddp_matches_torch_ddp(ws, model, overlap, bucket, shard):
     mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3, shard), nprocs=ws, join=True)
+
+
+@pytest.mark.parametrize("ws,model,overlap,bucket,shard,chunk", [
+    (2, "vgg", True, 4.0, False, 1.0),
+    (2, "vgg", False, 4.0, True, 1.0),
+    (4, "deepnn", True, 1.0, True, 0.5),
+])
+def test_ddp_row_chunk_buckets_match_torch_ddp(ws, model, overlap, bucket, shard, chunk):
+    """Big weights split into row-chunk buckets (each its own collective) keep torch-DDP semantics."""
+    mp.spawn(_worker, args=(ws, free_port(), model, overlap, bucket, 3, shard, "torch", chunk), nprocs=ws,
+             join=True)
+
+
+def test_plan_buckets_matches_torch_rule_without_chunks():
+    from ddpx.parallel.ddp import compute_bucket_assignment, plan_buckets, row_chunks
+    g = torch.Generator().manual_seed(0)
+    for _ in range(20):
+        sizes = (torch.randint(1, 3_000_000, (30,), generator=g)).tolist()
+        limits = [1 << 20, 25 << 20]
+        ref = compute_bucket_assignment(sizes, limits)
+        got = plan_buckets(range(30), sizes, limits)
+        assert [e[1] for e in got] == ref
+    # a chunked parameter closes the open bucket and stands alone
+    got = plan_buckets(range(4), [10, 10, 10, 10], [100, 100], chunked={2})
+    assert got == [("p", [0, 1]), ("c", 2), ("p", [3])]
+    rc = row_chunks((4096, 3072), 2, 8 << 20, 8 * 64)
+    assert rc[0][0] == 0 and rc[-1][1] == 4096 and all((r1 - r0) * 3072 % 512 == 0 for r0, r1 in rc[:-1])
 
 
 @pytest.mark.parametrize("shard", [False, True])

@@ -86,8 +86,9 @@ def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard):
     comm.close()
 
 
-@pytest.mark.parametrize("shard", [False, True])
-def test_graph_capture_with_rccl(gpu, pg, shard):
+@pytest.mark.parametrize("shard,chunk_mb,defer", [(False, None, False), (True, None, False), (True, 0.25, True),
+                                                  (False, 0.25, False)])
+def test_graph_capture_with_rccl(gpu, pg, shard, chunk_mb, defer):
     """Whole step (fwd, bwd with bucketed all-reduce on the comm stream, SGD) in one HIP graph."""
     import ddpx
     from ddpx.models import MLP
@@ -102,7 +103,10 @@ def test_graph_capture_with_rccl(gpu, pg, shard):
         ddpx.prepare_model(m, gpu)
     comm = RcclComm(gpu)
     da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
-                                 shard_optimizer=shard)
+                                 shard_optimizer=shard, chunk_mb=chunk_mb, defer_gather=defer)
+    if chunk_mb:
+        assert da.chunk_bucket
+    assert da.defer_gather == defer
     oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True)
     ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
     xs = [torch.rand(128, 3072, device=gpu).to(torch.bfloat16) for _ in range(4)]
@@ -129,8 +133,11 @@ def test_graph_capture_with_rccl(gpu, pg, shard):
         ob.step()
         if i:
             assert abs(loss.item() - losses[i - 1]) < 1e-6
+    da.consolidate()  # deferred gathers: complete the last step's all-gathers
     torch.cuda.synchronize()
     for p, q in zip(a.parameters(), b.parameters()):
         assert torch.equal(p, q)
+    if defer:  # the bf16 compute copies must agree too (they are what the deferred gather moves)
+        assert torch.equal(a.fc0.weight._ddpx_shadow, b.fc0.weight._ddpx_shadow)
     da.close()
     comm.close()

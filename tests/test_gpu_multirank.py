@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _mlp_worker(rank, ws, port, overlap, shard, grad_dtype, steps, errq):
+def _mlp_worker(rank, ws, port, overlap, shard, grad_dtype, steps, chunk_mb, defer, errq):
     import torch.distributed as dist
     try:
         import ddpx
@@ -39,9 +39,13 @@ def _mlp_worker(rank, ws, port, overlap, shard, grad_dtype, steps, errq):
         ddpx.prepare_model(ours, dev, grad_dtype=gd)
         ddpx.prepare_model(ref, dev)
         d = DistributedDataParallel(ours, comm=HostStagedComm(), bucket_cap_mb=1.0, first_bucket_mb=0.25,
-                                    overlap_optimizer=overlap, shard_optimizer=shard)
+                                    overlap_optimizer=overlap, shard_optimizer=shard, chunk_mb=chunk_mb,
+                                    defer_gather=defer)
         if shard:
             assert d.sharded and d.gather_what == "shadow"
+        if chunk_mb:
+            assert len(d.chunk_bucket) == 2 and all(len(v) >= 2 for v in d.chunk_bucket.values())
+        assert d.defer_gather == bool(defer and shard)
         o = SGD(ours.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
         if overlap or shard:
             d.attach_optimizer(o)
@@ -99,14 +103,17 @@ def _run(fn, ws, *args):
         raise AssertionError("\n".join(msgs) or "worker failed")
 
 
-@pytest.mark.parametrize("overlap,shard,grad_dtype", [
-    (False, False, "fp32"),
-    (True, False, "bf16"),
-    (True, True, "bf16"),
-    (False, True, "fp32"),
+@pytest.mark.parametrize("overlap,shard,grad_dtype,chunk_mb,defer", [
+    (False, False, "fp32", None, False),
+    (True, False, "bf16", None, False),
+    (True, True, "bf16", None, False),
+    (False, True, "fp32", None, False),
+    (True, False, "bf16", 0.125, False),   # row-chunk buckets, all-reduce
+    (True, True, "bf16", 0.125, True),     # chunks + ZeRO-1 + deferred, per-chunk-waited all-gathers
+    (False, True, "fp32", 0.25, True),
 ])
-def test_mlp_two_ranks_one_gpu(gpu, overlap, shard, grad_dtype):
-    _run(_mlp_worker, 2, overlap, shard, grad_dtype, 3)
+def test_mlp_two_ranks_one_gpu(gpu, overlap, shard, grad_dtype, chunk_mb, defer):
+    _run(_mlp_worker, 2, overlap, shard, grad_dtype, 3, chunk_mb, defer)
 
 
 def test_bench_two_ranks_one_gpu(gpu, tmp_path):
@@ -116,11 +123,12 @@ def test_bench_two_ranks_one_gpu(gpu, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--comm", "host", "--hidden", "1024",
-           "--json_out", str(out)]
+           "--chunk_mb", "0.5", "--json_out", str(out)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     import json
     rec = json.loads(out.read_text().strip().splitlines()[-1])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["sharded_optimizer"] is True and rec["config"]["replicas_consistent"] is True
+    assert rec["config"]["defer_gather"] is True and rec["config"]["chunk_mb"] == 0.5
     assert rec["value"] > 0
