@@ -39,53 +39,72 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nn;
 }
 
+// One 256-thread workgroup per channel: every thread merges a strided subset of the tiles (at most
+// T/256, loads issued ahead of the merges), a fixed-shape butterfly merges each wave, and thread 0
+// merges the 4 wave results in wave order — deterministic, and enough workgroups (C of them) to keep
+// the per-tile load latency off a serial chain (VGG's 32x32 layers have T = 2048 tiles).
+__device__ __forceinline__ void wave_chan_merge(float& n, float& mu, float& m2, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64), qb = __shfl_xor(m2, o, 64);
+    // lower lane merges the upper lane's state; the upper lane computes the same merge in the same order
+    if ((lane & o) == 0) chan_merge(n, mu, m2, nb, mb, qb);
+    else {
+      float n2 = nb, mu2 = mb, q2 = qb;
+      chan_merge(n2, mu2, q2, n, mu, m2);
+      n = n2; mu = mu2; m2 = q2;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256)
 finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, const float* __restrict__ gamma,
                 const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
                 int64_t* __restrict__ nbt, float momentum, float eps, int training, float* __restrict__ a_out,
                 float* __restrict__ b_out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ float wres[4][3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = blockIdx.x;
   float mean, var;
   if (training) {
     float n = 0.f, mu = 0.f, m2 = 0.f;
-    for (int t = lane; t < T; t += 64) {
-      const float nt = (float)min(BM, M - t * BM);
-      chan_merge(n, mu, m2, nt, stats[((size_t)t * 2) * C + c], stats[((size_t)t * 2 + 1) * C + c]);
-    }
+    int t = tid;
+    for (; t + 3 * 256 < T; t += 4 * 256) {  // 4 tiles' loads in flight per thread
+      float tm[4], tq[4];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64), qb = __shfl_xor(m2, o, 64);
-      // symmetric merge: lower lane merges upper lane's state (same result in both lanes up to order;
-      // use the lower lane as the canonical order)
-      if ((lane & o) == 0) chan_merge(n, mu, m2, nb, mb, qb);
-      else {
-        float n2 = nb, mu2 = mb, q2 = qb;
-        chan_merge(n2, mu2, q2, n, mu, m2);
-        n = n2; mu = mu2; m2 = q2;
+      for (int u = 0; u < 4; ++u) {
+        tm[u] = stats[((size_t)(t + u * 256) * 2) * C + c];
+        tq[u] = stats[((size_t)(t + u * 256) * 2 + 1) * C + c];
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) chan_merge(n, mu, m2, (float)min(BM, M - (t + u * 256) * BM), tm[u], tq[u]);
     }
+    for (; t < T; t += 256)
+      chan_merge(n, mu, m2, (float)min(BM, M - t * BM), stats[((size_t)t * 2) * C + c],
+                 stats[((size_t)t * 2 + 1) * C + c]);
+    wave_chan_merge(n, mu, m2, lane);
+    if (lane == 0) { wres[w][0] = n; wres[w][1] = mu; wres[w][2] = m2; }
+    __syncthreads();
+    if (tid != 0) return;
+    n = wres[0][0]; mu = wres[0][1]; m2 = wres[0][2];
+    for (int q = 1; q < 4; ++q) chan_merge(n, mu, m2, wres[q][0], wres[q][1], wres[q][2]);
     mean = mu;
     var = m2 / (float)M;  // biased, for normalisation
-    if (lane == 0) {
-      const float unbiased = M > 1 ? m2 / (float)(M - 1) : m2;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
-      if (c == 0 && nbt) nbt[0] += 1;
-    }
+    const float unbiased = M > 1 ? m2 / (float)(M - 1) : m2;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+    if (c == 0 && nbt) nbt[0] += 1;
   } else {
+    if (tid != 0) return;
     mean = rmean[c];
     var = rvar[c];
   }
-  if (lane == 0) {
-    const float rstd = rsqrtf(var + eps);
-    const float a = gamma[c] * rstd;
-    a_out[c] = a;
-    b_out[c] = beta[c] - mean * a;
-    mean_out[c] = mean;
-    rstd_out[c] = rstd;
-  }
+  const float rstd = rsqrtf(var + eps);
+  const float a = gamma[c] * rstd;
+  a_out[c] = a;
+  b_out[c] = beta[c] - mean * a;
+  mean_out[c] = mean;
+  rstd_out[c] = rstd;
 }
 
 // ---------------------------------------------------------------- apply
@@ -248,22 +267,31 @@ __global__ void __launch_bounds__(256)
 bwd_finalize_kernel(const float* __restrict__ part, int B, int C, int M, float* __restrict__ c1,
                     float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta, int out_bf16,
                     int accumulate, SgdArgs sg, SgdArgs sb) {
-  // 16 lanes per channel: strided partial sums, then a fixed butterfly (deterministic)
-  const int sub = threadIdx.x & 15;
-  const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
+  // one wave (64 lanes) per channel: strided partial sums with 4 loads in flight, then a fixed
+  // butterfly (deterministic)
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float s1 = 0.f, s2 = 0.f;
   if (c < C) {
-    for (int k = sub; k < B; k += 16) {
+    int k = lane;
+    for (; k + 3 * 64 < B; k += 4 * 64) {
+      float a[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = part[((size_t)(k + u * 64) * 2) * C + c];
+        q[u] = part[((size_t)(k + u * 64) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += q[u]; }
+    }
+    for (; k < B; k += 64) {
       s1 += part[((size_t)k * 2) * C + c];
       s2 += part[((size_t)k * 2 + 1) * C + c];
     }
   }
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    s1 += __shfl_xor(s1, o, 64);
-    s2 += __shfl_xor(s2, o, 64);
-  }
-  if (c >= C || sub != 0) return;
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (c >= C || lane != 0) return;
   c1[c] = s1 / (float)M;
   c2[c] = s2 / (float)M;
   auto put = [&](const SgdArgs& sgd, void* out, float v) {
@@ -339,7 +367,7 @@ using namespace ddpx;
 DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
                               float* a, float* b, float* mean, float* rstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn::finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, stats, T, BM, M, C, gamma, beta, rmean,
+  hipLaunchKernelGGL(bn::finalize_kernel, dim3(C), dim3(256), 0, s, stats, T, BM, M, C, gamma, beta, rmean,
                      rvar, nbt, momentum, eps, training, a, b, mean, rstd);
   return (int)hipGetLastError();
 }
@@ -370,7 +398,7 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
                      dgamma, dbeta, out_bf16, accumulate, SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd},
                      SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
   const int n = N * H * W * (C / 8);
@@ -392,7 +420,7 @@ DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bia
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
                      nullptr, dbias, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
   const int n = N * H * W * (C / 8);

@@ -114,11 +114,14 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
     sw, sb, sp = (native.sgd_args(x) for x in (sgd_w, sgd_b, sgd_prev))
     lr_ptr = sw[3] if fused else None
     mom, wd = (sw[4], sw[5]) if fused else (0.0, 0.0)
-    rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
-                           native.ptr(dH), native.ptr(dW), native.ptr(db), native.ptr(dbprev), int(relu_mask),
-                           float(dh_scale), int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3], *sp[:3],
-                           lr_ptr, mom, wd, native.stream_handle())
-    native.check(rc, "ddpx_head_bwd")
+    rc = lib.ddpx_head_bwd_partial(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C,
+                                   h.stride(0), native.ptr(dH), int(relu_mask), float(dh_scale), scratch.data_ptr(),
+                                   native.stream_handle())
+    native.check(rc, "ddpx_head_bwd_partial")
+    rc = lib.ddpx_head_bwd_finalize(M, K, C, native.ptr(dW), native.ptr(db), native.ptr(dbprev),
+                                    int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3],
+                                    *sp[:3], lr_ptr, mom, wd, native.stream_handle())
+    native.check(rc, "ddpx_head_bwd_finalize")
     return dH
 
 

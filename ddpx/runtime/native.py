@@ -62,8 +62,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_head_fwd_scratch", I64, I, I)
     _sig(lib, "ddpx_head_bwd_scratch", I64, I, I, I)
     _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P, P)
-    _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, P, P, P, I, F, I, I, P, P, P, P, P, P, P, P, P, P, P, F,
-         F, P)
+    _sig(lib, "ddpx_head_bwd_partial", I, P, P, P, P, I, I, I, I, P, I, F, P, P)
+    _sig(lib, "ddpx_head_bwd_finalize", I, I, I, I, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_mean", I, P, I, P, P)
     _sig(lib, "ddpx_accuracy", I, P, P, I, I, P, P)
     _sig(lib, "ddpx_augment", I, P, P, P, I, I, I, I, I, c_uint64, I, I, P, P, P)
