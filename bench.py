@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this into row-chunk buckets, each reduced as soon as its "
-                        "slice of the weight gradient is written (default 64 for the wide MLP at N>1, else off)")
+                        "slice of the weight gradient is written (opt-in; default off)")
     p.add_argument("--defer_gather", type=int, default=None,
                    help="1: ZeRO-1 all-gathers issued at the start of the next step and waited per chunk "
                         "inside the forward (default 1 with --shard_optimizer on the MLPs)")
@@ -138,11 +138,11 @@ def resolve_defaults(args, world):
         # VGG reads fp32 masters (per-step weight repack), so it keeps the replicated all-reduce
         args.shard_optimizer = int(multi and args.model.startswith("mlp"))
     if args.chunk_mb is None:
-        # row-chunk buckets pay only where one chunk's GEMM still fills the chip: the wide MLP's
-        # 16384-wide layers.  At the toy MLP's M = 512 rows a quarter-width forward / wgrad GEMM is
-        # launch- and fill-bound (measured 36 vs 34 us for a 1024-column chunk vs the whole 4096-column
-        # layer, profiles/r1_chunk), so the toy MLP keeps whole-layer buckets
-        args.chunk_mb = 64.0 if (multi and args.model == "mlp_wide") else 0.0
+        # row-chunk buckets: off by default.  At the toy MLP's M = 512 rows a quarter-width forward /
+        # wgrad GEMM is launch- and fill-bound (36 vs 34 us for a 1024-column chunk vs the whole
+        # 4096-column layer), and the wide MLP measured 5.52 vs 4.32 ms/step with 64 MB chunks at world
+        # size 1 (profiles/r1_chunk); the multi-GPU benefit is unmeasured here, so it stays opt-in
+        args.chunk_mb = 0.0
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 

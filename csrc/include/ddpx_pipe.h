@@ -49,10 +49,40 @@ enum Epi : int {
 
 enum Mode : int { MODE_PLAIN = 0, MODE_IM2COL_FWD = 1, MODE_IM2COL_BWD = 2, MODE_IM2COL_COL = 3 };
 
+// Division by a runtime constant d >= 1 as a multiply-high and a shift (n < 2^31): the im2col
+// address of every 16-B DMA chunk needs (tap, channel) = divmod(k, C) and (h, w) = divmod(pixel, W, H),
+// and a v_rcp_iflag-based integer division is ~12 VALU instructions each — enough, 4 per chunk, to
+// make the conv GEMMs VALU-issue-bound (ISA count of the 256x128 fwd kernel: 842 VALU per K-step
+// against 32 MFMAs).  s = ceil(log2 d), magic = ceil(2^(31+s) / d) (< 2^32), n / d = umulhi(n, magic)
+// >> (s - 1);  d == 1: magic 0 (identity).
+struct FastDiv {
+  unsigned magic;
+  int shift;
+};
+
+static inline FastDiv make_fastdiv(int d) {
+  FastDiv f{0u, 0};
+  if (d <= 1) return f;
+  int s = 0;
+  while ((1ll << s) < d) ++s;
+  f.shift = s - 1;
+  f.magic = (unsigned)(((1ull << (31 + s)) + (unsigned long long)d - 1) / (unsigned long long)d);
+  return f;
+}
+
+__device__ __forceinline__ int fdiv(int n, FastDiv f) {
+  return f.magic ? (int)(__umulhi((unsigned)n, f.magic) >> f.shift) : n;
+}
+
 struct ConvGeom {
   int H, W, C;  // spatial size and channel count of the NHWC tensor being im2col'd
   int npix;     // N*H*W
+  FastDiv dW, dH, dC;
 };
+
+static inline ConvGeom make_geom(int H, int W, int C, int npix) {
+  return ConvGeom{H, W, C, npix, make_fastdiv(W), make_fastdiv(H), make_fastdiv(C)};
+}
 
 struct Params {
   const unsigned short* A;
@@ -95,12 +125,13 @@ __device__ __forceinline__ unsigned src_off(const ConvGeom& g, int ld, int row, 
     // pixel index p and (tap, channel) index q
     const int p = KC ? row : k;
     const int q = KC ? k : row;
-    const int tap = q / g.C, c = q - tap * g.C;
-    const int ky = tap / 3, kx = tap - ky * 3;
+    const int tap = fdiv(q, g.dC), c = q - tap * g.C;
+    const int ky = (tap * 11) >> 5, kx = tap - ky * 3;  // tap / 3 for tap < 9 (tap >= 9 rejected below)
     int dy = ky - 1, dx = kx - 1;
     if constexpr (MODE == MODE_IM2COL_BWD) { dy = -dy; dx = -dx; }
-    const int w = p % g.W;
-    const int h = (p / g.W) % g.H;
+    const int pw = fdiv(p, g.dW);
+    const int w = p - pw * g.W;
+    const int h = pw - fdiv(pw, g.dH) * g.H;
     const int hh = h + dy, ww = w + dx;
     if (tap >= 9 || hh < 0 || hh >= g.H || ww < 0 || ww >= g.W) return kOOB;
     return (unsigned)(((p + dy * g.W + dx) * g.C + c) * 2);

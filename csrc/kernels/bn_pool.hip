@@ -217,6 +217,37 @@ __device__ __forceinline__ void grad_z(const unsigned short* __restrict__ gout, 
   for (int j = 0; j < 8; ++j) gz[j] = (arg[j] == me && (!relu || zs[j] > 0.f)) ? gg[j] : 0.f;
 }
 
+// Pooled layers, one thread per (2x2 window, 8-channel group): the window's 4 y vectors and the pooled
+// gradient are read once (not once per pre-pool pixel) and the routed, ReLU-masked gradient gz of all
+// four pixels comes out together (same first-max tie rule and mask as grad_z).
+__device__ __forceinline__ void grad_window(const unsigned short* __restrict__ gout,
+                                            const unsigned short* __restrict__ y, const float (&av)[8],
+                                            const float (&bv)[8], int n, int ho, int wo, int H, int W, int C, int g,
+                                            int relu, float (&f)[4][8], float (&gz)[4][8]) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  float gg[8];
+  unpack8(*reinterpret_cast<const u32x4*>(gout + (((size_t)n * Ho + ho) * Wo + wo) * C + g * 8), gg);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int hh = 2 * ho + (q >> 1), ww = 2 * wo + (q & 1);
+    unpack8(*reinterpret_cast<const u32x4*>(y + (((size_t)n * H + hh) * W + ww) * C + g * 8), f[q]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float best = -INFINITY;
+    int arg = 0;
+    float zs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      zs[q] = fmaf(av[j], f[q][j], bv[j]);
+      const float z = relu ? fmaxf(zs[q], 0.f) : zs[q];
+      if (z > best) { best = z; arg = q; }  // strict: first max wins
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gz[q][j] = (arg == q && (!relu || zs[q] > 0.f)) ? gg[j] : 0.f;
+  }
+}
+
 // Pass 1: part[blk][0][c] = sum gz, part[blk][1][c] = sum gz * xhat over this block's pixels.
 // Block = 256 threads = (C/8 channel groups) x (256/(C/8) pixel lanes); grid-strided over pixels.
 __global__ void __launch_bounds__(256)
@@ -235,15 +266,31 @@ bwd_reduce_kernel(const unsigned short* __restrict__ gout, const unsigned short*
     av[j] = a[g * 8 + j]; bv[j] = b[g * 8 + j]; mu[j] = mean[g * 8 + j]; rs[j] = rstd[g * 8 + j];
     s1[j] = 0.f; s2[j] = 0.f;
   }
-  for (int pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
-    const int w = pix % W, h = (pix / W) % H, n = pix / (W * H);
-    float f[8], gz[8];
-    unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
-    grad_z(gout, y, av, bv, n, h, w, H, W, C, g, pool, relu, f, gz);
+  if (pool) {
+    const int Ho = H >> 1, Wo = W >> 1, PP = N * Ho * Wo;
+    for (int pp = blockIdx.x * lanes + pl; pp < PP; pp += gridDim.x * lanes) {
+      const int wo = pp % Wo, ho = (pp / Wo) % Ho, n = pp / (Wo * Ho);
+      float f[4][8], gz[4][8];
+      grad_window(gout, y, av, bv, n, ho, wo, H, W, C, g, relu, f, gz);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s1[j] += gz[j];
-      s2[j] = fmaf(gz[j], (f[j] - mu[j]) * rs[j], s2[j]);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s1[j] += gz[q][j];
+          s2[j] = fmaf(gz[q][j], (f[q][j] - mu[j]) * rs[j], s2[j]);
+        }
+    }
+  } else {
+    for (int pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
+      const int w = pix % W, h = (pix / W) % H, n = pix / (W * H);
+      float f[8], gz[8];
+      unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
+      grad_z(gout, y, av, bv, n, h, w, H, W, C, g, pool, relu, f, gz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += gz[j];
+        s2[j] = fmaf(gz[j], (f[j] - mu[j]) * rs[j], s2[j]);
+      }
     }
   }
 #pragma unroll
@@ -317,11 +364,43 @@ bwd_apply_kernel(const unsigned short* __restrict__ gout, const unsigned short* 
                  int H, int W, int C, int pool, int relu, int norm, unsigned short* __restrict__ dy) {
   const int G = C / 8;
   const int t = blockIdx.x * 256 + threadIdx.x;
+  float av[8], bv[8];
+  if (pool) {  // one thread per (2x2 window, channel group): writes the window's 4 dy vectors
+    const int Ho = H >> 1, Wo = W >> 1;
+    if (t >= N * Ho * Wo * G) return;
+    const int g = t % G, pp = t / G;
+    const int wo = pp % Wo, ho = (pp / Wo) % Ho, n = pp / (Wo * Ho);
+    // per-channel coefficients in registers once per window (not re-loaded for each of the 4 pixels)
+    float mu[8], rs[8], k1[8], k2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = a[g * 8 + j];
+      bv[j] = b[g * 8 + j];
+      mu[j] = mean[g * 8 + j];
+      rs[j] = rstd[g * 8 + j];
+      k1[j] = c1[g * 8 + j];
+      k2[j] = c2[g * 8 + j];
+    }
+    float f[4][8], gz[4][8];
+    grad_window(gout, y, av, bv, n, ho, wo, H, W, C, g, relu, f, gz);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float out[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (f[q][j] - mu[j]) * rs[j];
+        out[j] = norm ? av[j] * (gz[q][j] - k1[j] - xh * k2[j]) : gz[q][j];
+      }
+      const int hh = 2 * ho + (q >> 1), ww = 2 * wo + (q & 1);
+      *reinterpret_cast<u32x4*>(dy + (((size_t)n * H + hh) * W + ww) * C + g * 8) = pack8(out);
+    }
+    return;
+  }
   const int P = N * H * W;
   if (t >= P * G) return;
   const int g = t % G, pix = t / G;
   const int w = pix % W, h = (pix / W) % H, n = pix / (W * H);
-  float av[8], bv[8], f[8], gz[8], out[8];
+  float f[8], gz[8], out[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { av[j] = a[g * 8 + j]; bv[j] = b[g * 8 + j]; }
   unpack8(*reinterpret_cast<const u32x4*>(y + (size_t)pix * C + g * 8), f);
@@ -401,7 +480,7 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
   hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
                      dgamma, dbeta, out_bf16, accumulate, SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd},
                      SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
-  const int n = N * H * W * (C / 8);
+  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
   hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu, 1,
                      (unsigned short*)dy);
@@ -423,7 +502,7 @@ DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bia
   hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
                      nullptr, dbias, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
-  const int n = N * H * W * (C / 8);
+  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
   hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,
                      (unsigned short*)dy);

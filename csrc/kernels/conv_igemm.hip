@@ -40,27 +40,71 @@ __global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restric
   if (wd) wd[((size_t)t * Co + o) * Cp + c] = h;
 }
 
-// out (torch layout [Co][Cr][3][3]) (=|+=) sum_s part[s][Co][9*Cp]   or fused SGD on the parameter
+// out (torch layout [Co][Cr][3][3]) (=|+=) sum_s part[s][Co][9*Cp]   or fused SGD on the parameter.
+// Workgroup = (output channel o, 64-channel tile): the S partial slabs are read tap-major with the
+// channel index fastest (coalesced, 4 slabs' loads in flight per thread), the sums are transposed
+// through LDS, and the [c][tap] run of the torch layout — 64 x 9 consecutive floats — is written (or
+// SGD-updated) contiguously.  Fixed summation order: deterministic.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Cr,
                                                            int Cp, void* __restrict__ out, int out_bf16,
                                                            int accumulate, SgdArgs sgd) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over torch-layout elements Co*Cr*9
-  if (i >= Co * Cr * 9) return;
-  const int t = i % 9;
-  const int c = (i / 9) % Cr;
-  const int o = i / (9 * Cr);
-  const size_t src = (size_t)o * 9 * Cp + t * Cp + c;
+  constexpr int CT = 64;
+  __shared__ float red[9][CT + 1];
+  __shared__ float sred[256];
+  const int o = blockIdx.x;
+  const int c0 = blockIdx.y * CT;
+  const int nc = min(CT, Cr - c0);
   const size_t slab = (size_t)Co * 9 * Cp;
-  float s = 0.f;
-  for (int k = 0; k < S; ++k) s += part[k * slab + src];
-  if (sgd.p) {
-    sgd_apply(sgd, i, s, *sgd.lr);
-  } else if (out_bf16) {
-    unsigned short* d = reinterpret_cast<unsigned short*>(out) + i;
-    *d = f2bf(accumulate ? s + bf2f(*d) : s);
-  } else {
-    float* d = reinterpret_cast<float*>(out) + i;
-    *d = accumulate ? s + *d : s;
+  const int items = 9 * nc;
+  // few outputs per workgroup (thin layers, e.g. 3 input channels) but many slabs: TS threads share an
+  // output, each summing every TS-th slab, then a fixed-order combine (deterministic)
+  int TS = 1;
+  while (TS < 16 && items * TS * 2 <= 256) TS *= 2;
+  for (int j0 = 0; j0 < items; j0 += 256 / TS) {
+    const int j = j0 + threadIdx.x / TS, sub = threadIdx.x % TS;
+    float s = 0.f;
+    if (j < items && threadIdx.x / TS < 256 / TS) {
+      const int t = j / nc, cc = j % nc;
+      const float* src = part + (size_t)o * 9 * Cp + (size_t)t * Cp + c0 + cc;
+      int k = sub;
+      for (; k + 3 * TS < S; k += 4 * TS) {
+        const float a0 = src[(size_t)k * slab], a1 = src[(size_t)(k + TS) * slab];
+        const float a2 = src[(size_t)(k + 2 * TS) * slab], a3 = src[(size_t)(k + 3 * TS) * slab];
+        s += a0;
+        s += a1;
+        s += a2;
+        s += a3;
+      }
+      for (; k < S; k += TS) s += src[(size_t)k * slab];
+    }
+    if (TS == 1) {
+      if (j < items) red[j / nc][j % nc] = s;
+    } else {
+      sred[threadIdx.x] = s;
+      __syncthreads();
+      if (sub == 0 && j < items) {
+        float v = 0.f;
+        for (int q = 0; q < TS; ++q) v += sred[threadIdx.x + q];
+        red[j / nc][j % nc] = v;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const size_t base = ((size_t)o * Cr + c0) * 9;
+  for (int q = threadIdx.x; q < nc * 9; q += 256) {
+    const int cc = q / 9, t = q % 9;
+    const float v = red[t][cc];
+    const size_t i = base + q;
+    if (sgd.p) {
+      sgd_apply(sgd, i, v, *sgd.lr);
+    } else if (out_bf16) {
+      unsigned short* d = reinterpret_cast<unsigned short*>(out) + i;
+      *d = f2bf(accumulate ? v + bf2f(*d) : v);
+    } else {
+      float* d = reinterpret_cast<float*>(out) + i;
+      *d = accumulate ? v + *d : v;
+    }
   }
 }
 
@@ -129,7 +173,7 @@ DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats,
   const size_t ab = (size_t)P * C * 2, bb = (size_t)Co * K * 2;
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
-  p.conv = ConvGeom{H, W, C, P};
+  p.conv = make_geom(H, W, C, P);
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
   return (int)dispatch<true, true, MODE_IM2COL_FWD, MODE_PLAIN>(p, cfg, 1, s);
 }
@@ -152,7 +196,7 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   const size_t ab = (size_t)P * Co * 2, bb = (size_t)K * C * 2;
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
-  p.conv = ConvGeom{H, W, Co, P};
+  p.conv = make_geom(H, W, Co, P);
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C);
   return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
 }
@@ -199,7 +243,7 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
   const size_t ab = (size_t)P * Co * 2, bb = (size_t)P * C * 2;
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
-  p.conv = ConvGeom{H, W, C, P};
+  p.conv = make_geom(H, W, C, P);
   p.klen = ((P + S - 1) / S + 63) / 64 * 64;
   p.split_stride = (long long)Co * 9 * C;
   const int Sreal = (P + p.klen - 1) / p.klen;
@@ -214,8 +258,7 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
 DDPX_API int ddpx_conv_wgrad_reduce(const float* part, int S, int Co, int Cr, int Cp, void* out, int out_bf16,
                                     int accumulate, float* sgd_p, float* sgd_buf, void* sgd_shadow,
                                     const float* sgd_lr, float sgd_mom, float sgd_wd, hipStream_t s) {
-  const int n = Co * Cr * 9;
-  hipLaunchKernelGGL(conv::wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, S, Co, Cr, Cp, out,
+  hipLaunchKernelGGL(conv::wgrad_reduce_kernel, dim3(Co, (Cr + 63) / 64), dim3(256), 0, s, part, S, Co, Cr, Cp, out,
                      out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
   return (int)hipGetLastError();
 }

@@ -336,7 +336,7 @@ DDPX_API int ddpx_gemm_mx8(const void* A, const void* sa, const void* B, const v
                          nullptr, M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes,
                          (unsigned)b_bytes, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom,
                                                      sgd_wd},
-                         pipe::ConvGeom{0, 0, 0, 0}, 0, 0};
+                         pipe::make_geom(0, 0, 0, 0), 0, 0};
   mp.sa = (const unsigned char*)sa;
   mp.sb = (const unsigned char*)sb;
   mp.sa_bytes = (unsigned)((size_t)M * (K / 32));

@@ -156,7 +156,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   pipe::Params p{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
                  M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes,
                  SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
-                 pipe::ConvGeom{0, 0, 0, 0}, 0, 0};
+                 pipe::make_geom(0, 0, 0, 0), 0, 0};
   if (epi == pipe::EPI_SGD && (!sgd_p || !sgd_lr || (sgd_mom != 0.f && !sgd_buf))) return -5;
   static const int sgd_plain = [] {
     const char* e = getenv("DDPX_SGD_PLAIN");
@@ -213,7 +213,7 @@ DDPX_API int ddpx_gemm_pipe_splitk(const void* A, const void* B, void* C, const 
   const int S = (K + klen - 1) / klen;
   pipe::Params pp{(const unsigned short*)A, (const unsigned short*)B, scratch, nullptr, nullptr, nullptr,
                   M, N, K, lda, ldb, N, 0, pipe::EPI_F32, 0, 1.f, (unsigned)a_bytes, (unsigned)b_bytes,
-                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::ConvGeom{0, 0, 0, 0}, klen,
+                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::make_geom(0, 0, 0, 0), klen,
                   (long long)M * N};
   hipError_t e = b_kcontig
                      ? pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(pp, 8, S, stream)
@@ -221,7 +221,7 @@ DDPX_API int ddpx_gemm_pipe_splitk(const void* A, const void* B, void* C, const 
   if (e != hipSuccess) return (int)e;
   pipe::Params fp{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
                   M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, 0u, 0u,
-                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::ConvGeom{0, 0, 0, 0}, 0, 0};
+                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::make_geom(0, 0, 0, 0), 0, 0};
   const dim3 grid((N + 255) / 256, (M + 3) / 4);
   switch (epi) {
     case pipe::EPI_F32: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_F32>, grid, dim3(256), 0, stream, fp, scratch, S); break;

@@ -58,24 +58,11 @@ head_logits_partial_kernel(const unsigned short* __restrict__ H, const unsigned 
   if (m0 + rr < M) partial[((size_t)ks * M + m0 + rr) * kHeadC + cc] = s;
 }
 
-// Per row: logits, log-softmax, NLL, dlogits, argmax.  Returns the row loss (0 for no target).
-__device__ __forceinline__ float head_row(const float* __restrict__ partial, int KS, const float* __restrict__ b,
-                                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, int m,
-                                          float* __restrict__ logits, float* __restrict__ dlogits, int* hit) {
-  float z[kHeadC];
-#pragma unroll
-  for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
-  for (int ks = 0; ks < KS; ++ks) {
-    const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = pp[q];
-      z[4 * q] += v[0];
-      z[4 * q + 1] += v[1];
-      z[4 * q + 2] += v[2];
-      z[4 * q + 3] += v[3];
-    }
-  }
+// Per row, given the summed logits z (bias not yet added): log-softmax, NLL, dlogits, argmax.
+// Returns the row loss (0 for no target).
+__device__ __forceinline__ float head_finish(float (&z)[kHeadC], const float* __restrict__ b,
+                                             const int64_t* __restrict__ tgt, int C, float inv_m, int m,
+                                             float* __restrict__ logits, float* __restrict__ dlogits, int* hit) {
   float mx = -INFINITY;
   int am = 0;
 #pragma unroll
@@ -104,6 +91,32 @@ __device__ __forceinline__ float head_row(const float* __restrict__ partial, int
   return lse - zt;
 }
 
+// Partial-logit slices ks = k0, k0 + kstep, ... of row m summed into z.
+__device__ __forceinline__ void head_sum(const float* __restrict__ partial, int KS, int M, int m, int k0, int kstep,
+                                         float (&z)[kHeadC]) {
+#pragma unroll
+  for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
+  for (int ks = k0; ks < KS; ks += kstep) {
+    const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = pp[q];
+      z[4 * q] += v[0];
+      z[4 * q + 1] += v[1];
+      z[4 * q + 2] += v[2];
+      z[4 * q + 3] += v[3];
+    }
+  }
+}
+
+__device__ __forceinline__ float head_row(const float* __restrict__ partial, int KS, const float* __restrict__ b,
+                                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, int m,
+                                          float* __restrict__ logits, float* __restrict__ dlogits, int* hit) {
+  float z[kHeadC];
+  head_sum(partial, KS, M, m, 0, 1, z);
+  return head_finish(z, b, tgt, C, inv_m, m, logits, dlogits, hit);
+}
+
 // One thread per row.
 __global__ void __launch_bounds__(256)
 head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
@@ -121,22 +134,40 @@ head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __r
   }
 }
 
-// Single workgroup (M <= 8192): every row plus the mean loss in one launch.  Rows are assigned to
-// threads in a fixed pattern and reduced in a fixed order: deterministic.
+// Single workgroup (M <= 8192): every row plus the mean loss in one launch.  TL lanes share a row
+// (each sums every TL-th partial-logit slice, so the slice loads of a row are in flight together
+// instead of in one thread's serial chain), a butterfly combines them, and the group's first lane
+// finishes the row.  Rows are assigned in a fixed pattern and reduced in a fixed order: deterministic.
+template <int TL>
 __global__ void __launch_bounds__(1024)
 head_finalize_mean_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
                           const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
                           float* __restrict__ loss_rows, float* __restrict__ dlogits, int* __restrict__ correct,
                           float* __restrict__ loss_mean) {
   __shared__ float red[16];
+  constexpr int RPP = 1024 / TL;  // rows per pass
+  const int sub = threadIdx.x % TL, r = threadIdx.x / TL;
   float acc = 0.f;
   int hits = 0;
-  for (int m = threadIdx.x; m < M; m += 1024) {
-    int hit = 0;
-    const float l = head_row(partial, KS, b, tgt, M, C, inv_m, m, logits, dlogits, &hit);
-    if (loss_rows) loss_rows[m] = l;
-    acc += l;
-    hits += hit;
+  for (int m0 = 0; m0 < M; m0 += RPP) {
+    const int m = m0 + r;
+    float z[kHeadC];
+    if (m < M) head_sum(partial, KS, M, m, sub, TL, z);
+    else {
+#pragma unroll
+      for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
+    }
+#pragma unroll
+    for (int o = 1; o < TL; o <<= 1)
+#pragma unroll
+      for (int c = 0; c < kHeadC; ++c) z[c] += __shfl_xor(z[c], o, 64);
+    if (m < M && sub == 0) {
+      int hit = 0;
+      const float l = head_finish(z, b, tgt, C, inv_m, m, logits, dlogits, &hit);
+      if (loss_rows) loss_rows[m] = l;
+      acc += l;
+      hits += hit;
+    }
   }
   if (correct) {
     int hsum = hits;
@@ -379,8 +410,25 @@ DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const i
   hipLaunchKernelGGL(head_logits_partial_kernel, dim3((M + 15) / 16, ks), dim3(256), 0, s, (const unsigned short*)H,
                      (const unsigned short*)W, M, K, C, ldh, kslice, scratch);
   if (loss_mean && tgt && M <= 8192) {
-    hipLaunchKernelGGL(head_finalize_mean_kernel, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                       logits, loss_rows, dlogits, correct, loss_mean);
+    // lanes per row: as many as keep every row in ONE pass of the 1024 threads (M <= 1024 / TL), at most
+    // one per partial-logit slice — more passes would each pay the load latency again
+    int tl = 1;
+    while (tl < 16 && tl < ks && M * tl * 2 <= 1024) tl *= 2;
+    if (tl == 1)
+      hipLaunchKernelGGL(head_finalize_mean_kernel<1>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                         logits, loss_rows, dlogits, correct, loss_mean);
+    else if (tl == 2)
+      hipLaunchKernelGGL(head_finalize_mean_kernel<2>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                         logits, loss_rows, dlogits, correct, loss_mean);
+    else if (tl == 4)
+      hipLaunchKernelGGL(head_finalize_mean_kernel<4>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                         logits, loss_rows, dlogits, correct, loss_mean);
+    else if (tl == 8)
+      hipLaunchKernelGGL(head_finalize_mean_kernel<8>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                         logits, loss_rows, dlogits, correct, loss_mean);
+    else
+      hipLaunchKernelGGL(head_finalize_mean_kernel<16>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
+                         logits, loss_rows, dlogits, correct, loss_mean);
     return (int)hipGetLastError();
   }
   if (loss_mean && !loss_rows) return -3;
@@ -395,12 +443,12 @@ DDPX_API int ddpx_mean(const float* x, int n, float* out, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K, int C,
-                           int ldh, void* dH, void* dW, void* db, void* dbprev, int relu_mask, float hscale,
-                           int out_bf16,
-                           int accumulate, float* scratch, float* sw_p, float* sw_buf, void* sw_sh, float* sb_p,
-                           float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh, const float* lr,
-                           float mom, float wd, hipStream_t s) {
+// Backward in two launches: the partials (dH for every row + per-row-split dW / bias partials) and
+// the fixed-order finalize that stores or applies (fused SGD) the parameter gradients.  The finalize
+// is tiny (a separate entry point so a caller can time or reorder it).
+DDPX_API int ddpx_head_bwd_partial(const float* dlogits, const float* go, const void* H, const void* W, int M, int K,
+                                   int C, int ldh, void* dH, int relu_mask, float hscale, float* scratch,
+                                   hipStream_t s) {
   if (M <= 0) return 0;
   if (C != 10) return -1;
   if (K % 64 || ldh % 8) return -2;
@@ -412,6 +460,19 @@ DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H,
   hipLaunchKernelGGL(head_bwd_partial_kernel<10>, dim3(K / 64, rs), dim3(256), 0, s, dlogits, go,
                      (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, rps, (unsigned short*)dH, pdw, pdb,
                      pdbh, relu_mask, hscale);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_head_bwd_finalize(int M, int K, int C, void* dW, void* db, void* dbprev, int out_bf16,
+                                    int accumulate, const float* scratch, float* sw_p, float* sw_buf, void* sw_sh,
+                                    float* sb_p, float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh,
+                                    const float* lr, float mom, float wd, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (C != 10) return -1;
+  const int rs = head_row_splits(M, K);
+  const float* pdw = scratch;
+  const float* pdb = scratch + (size_t)rs * C * K;
+  const float* pdbh = pdb + (size_t)rs * K;
   hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + C + 255) / 256), dim3(256), 0, s, pdw, pdb,
                      pdbh, rs, K, dW, db, dbprev, out_bf16, accumulate,
                      SgdArgs{sw_p, sw_buf, (unsigned short*)sw_sh, lr, mom, wd},
