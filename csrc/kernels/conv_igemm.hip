@@ -108,19 +108,21 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
-// Tile picks from the per-layer MI355X sweep (benchmarks/conv_sweep.py, profiles/r1_conv): the
-// 8-wave 256x128 tile (cfg 8, 2x the operand reuse of 128x128) wins every VGG layer with >= 128
-// output channels and >= 8x8 spatial size by 25-40 %; 4x4 layers (P = 8192) want 64x128; the
-// 64-channel layer at 32x32 stays on 64x64.
+// Tile picks from the per-layer MI355X sweep after the fast-division addressing (benchmarks/conv_sweep.py,
+// profiles/r1_fdiv/conv_sweep_fdiv.json): the 8-wave 256x256 tile (cfg 13) wins every >= 128-channel
+// layer at 16x16 and 8x8 (fwd 512->512@8: 151 vs 198 us for 256x128); the 32x32 layers keep 256x128
+// (cfg 8); 4x4 layers (P = 8192) want 64x128; <= 64-channel outputs stay on 64x64.
 static int pick_fwd(int P, int Co) {
-  if (Co <= 64) return 7;     // conv0 (3->64 @32): 64x64, 3 stages
+  if (Co <= 64) return 7;     // conv0 (3->64 @32), DeepNN's 64/32-channel layers: 64x64, 3 stages
   if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
-  return 8;                   // 256x128, 8 waves
+  if (P >= 524288) return 8;  // 32x32 layers: 256x128, 8 waves
+  return 13;                  // 256x256, 8 waves
 }
-static int pick_dgrad(int P, int C) {
-  if (C <= 64) return 6;      // dx of conv1 (C = 64 @32): 128x64, 3 stages
+static int pick_dgrad(int P, int C, int Co) {
+  if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32): 128x64, 3 stages
   if (P <= 8192) return 5;
-  return 8;
+  if (Co <= 64 || Co > C) return 8;  // widening layers (dx narrower than dy) and thin DeepNN layers
+  return 13;
 }
 
 }  // namespace conv
@@ -197,7 +199,7 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = make_geom(H, W, Co, P);
-  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
   return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
 }
 
@@ -207,8 +209,8 @@ static int pick_wgrad(int P, int C, int Co) {
   // M = Co <= 64 (DeepNN's 128->64, 64->64, 64->32 layers): a 256-row tile would be 3/4 empty;
   // 64x64 / 3 stages measured 2.6x faster on 128->64@32 (profiles/r1_deepnn/conv_sweep_deepnn.json)
   if (Co <= 64) return 7;
-  if (C <= 64) return 0;      // conv1: 128x128, 4 stages
-  return 8;                   // 256x128, 8 waves
+  if (C <= 64) return 7;      // VGG conv1 (64->128 @32): 64x64 (259 vs 280 us for 128x128)
+  return 13;                  // 256x256, 8 waves (283 vs 393 us for 256x128 on 256->256@16)
 }
 
 // Number of K splits the weight-gradient GEMM uses for a tile config (cfg < 0: default).
