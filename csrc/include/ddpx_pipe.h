@@ -394,11 +394,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // XCD-aware (tile, split) order.  With split-K the grid's linear workgroup id is remapped over ALL
+  // workgroups, split-major: each XCD then owns whole K ranges (all tiles of a few splits), so a
+  // split's slice of both operands is fetched from HBM into one XCD's L2 and reused by its tiles there.
+  // Remapping only within a split spread every split's tiles over all 8 XCDs, and every XCD re-read
+  // every split's slice (8x the HBM traffic on the conv weight-gradient GEMMs).
+  const int ntiles = tiles_m * tiles_n;
+  int wg, split;
+  if (gridDim.y > 1) {
+    const int lg = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, ntiles * gridDim.y);
+    split = lg / ntiles;
+    wg = lg - split * ntiles;
+  } else {
+    wg = xcd_remap(blockIdx.x, ntiles);
+    split = 0;
+  }
   const int tm = wg % tiles_m, tn = wg / tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int split = blockIdx.y;
   const int kbeg = p.klen ? split * p.klen : 0;
   const int kend = p.klen ? min(p.K, kbeg + p.klen) : p.K;
   void* Cbase = p.C;

@@ -213,19 +213,38 @@ static int pick_wgrad(int P, int C, int Co) {
   return 13;                  // 256x256, 8 waves (283 vs 393 us for 256x128 on 256->256@16)
 }
 
-// Number of K splits the weight-gradient GEMM uses for a tile config (cfg < 0: default).
+// Workgroups of a tile config resident per CU (LDS-bound: STAGES x (BM+BN) x 64 x KSUB bf16 per
+// workgroup out of 160 KiB; the 8-wave configs also hold one per CU by registers).
+static int wgs_per_cu(int cfg) {
+  static const int t[14] = {1, 1, 1, 2, 1, 2, 2, 3, 1, 1, 1, 1, 2, 1};
+  return (cfg >= 0 && cfg <= 13) ? t[cfg] : 1;
+}
+
+// Number of K splits the weight-gradient GEMM uses for a tile config (cfg < 0: default).  Chosen so the
+// tiles x splits workgroups fill whole rounds of the chip's resident slots (256 CUs x workgroups/CU):
+// the candidate with the best last-round fill wins (smaller S on ties: less fp32 partial traffic),
+// among S giving at least 3/4 of a round and at most ~2 rounds.
 DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co, int tile_cfg) {
   const int cfg = tile_cfg >= 0 ? tile_cfg : pick_wgrad(P, C, Co);
   int bm, bn;
   tile_of(cfg, &bm, &bn);
   const int tiles = ((Co + bm - 1) / bm) * ((9 * C + bn - 1) / bn);
-  // one resident 8-wave workgroup per CU: 256 of them fill the chip; the 4-wave tiles want 2 per CU.
-  // Fewer splits = proportionally less fp32 partial traffic for the reduce kernel.
-  const int target = cfg == 8 ? 256 : 512;
-  int S = (target + tiles - 1) / tiles;
-  const int maxS = (P + 1023) / 1024;  // >= 16 K-steps per split
-  if (S > maxS) S = maxS;
-  return S < 1 ? 1 : S;
+  const int slots = 256 * wgs_per_cu(cfg);
+  const int maxS = max(1, (P + 1023) / 1024);  // >= 16 K-steps per split
+  const int S0 = min(maxS, max(1, (2 * slots + tiles - 1) / tiles));
+  int best = S0;
+  float best_eff = -1.f;
+  for (int S = 1; S <= S0; ++S) {
+    const long long w = (long long)tiles * S;
+    if (4 * w < 3LL * slots && S < S0) continue;
+    const long long rounds = (w + slots - 1) / slots;
+    const float eff = (float)w / (float)(rounds * slots);
+    if (eff > best_eff + 0.02f) {
+      best_eff = eff;
+      best = S;
+    }
+  }
+  return best;
 }
 
 // part[S][Co][9C] (fp32) = split-K partial weight gradients.  dy [P][Co], x NHWC [N][H][W][C].
