@@ -32,7 +32,7 @@ BASELINE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELI
 # The reference publishes no numbers: vs_baseline stays null.  For context the line also
 # carries the ratio to the stock PyTorch-ROCm recipe measured on one MI355X with this same data
 # (--impl torch; profiles/r1_first, profiles/r1_gemm, profiles/r1_tune), samples/s at batch 512.
-STOCK_MEASURED_1GPU = {"mlp": 706_000.0, "mlp_wide": 100_040.0, "vgg": 26_400.0}
+STOCK_MEASURED_1GPU = {"mlp": 706_000.0, "mlp_wide": 100_040.0, "vgg": 26_400.0, "deepnn": 118_494.0}
 
 
 def parse():
