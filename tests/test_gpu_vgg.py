@@ -15,7 +15,10 @@ def _bf(t):
 
 
 @pytest.mark.parametrize("N,H,Ci,Co", [(4, 32, 3, 64), (8, 16, 64, 128), (16, 8, 128, 256), (32, 4, 256, 512),
-                                       (64, 2, 512, 512), (6, 32, 64, 64)])
+                                       (64, 2, 512, 512), (6, 32, 64, 64),
+                                       # non-power-of-two H, W and channel counts: the im2col addressing
+                                       # divides by them with multiply-high fast division
+                                       (3, 12, 24, 40), (5, 6, 3, 24), (2, 10, 40, 48), (7, 5, 16, 8)])
 def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
     from ddpx.ops import conv as K
     torch.manual_seed(0)
