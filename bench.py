@@ -223,7 +223,17 @@ def main():
         opt.attach_device_schedule(sched)
         one = torch.ones((), device=device)  # d(loss)/d(loss): no fill kernel per step
 
+        # the batch comes from a device-side cursor over this epoch's index permutation (gather + crop/flip
+        # augment in one kernel that also advances the cursor), so the captured step needs no host work
+        # per replay besides the launch: batch k = full batch k % nfull, augmentation seed batch_seed(k),
+        # exactly the batches the eager loader would draw
+        nfull = len(full)
+        idx_dev = idx_all[:nfull * bs].contiguous()
+
+        counter = opt.step_counter()  # read by the batch gather, advanced by the LR-table kernel below
+
         def step_body(x, y):
+            loader.cursor_batch(idx_dev, nfull, x, y, counter=counter)
             opt.device_lr_step()
             opt.zero_grad()
             loss, _ = net.forward_loss(x, y) if hasattr(model, "forward_loss") else (
@@ -237,9 +247,6 @@ def main():
 
         def one_step(k):
             nonlocal graph
-            b = full[k % len(full)]
-            loader.make_batch(idx_all[b * bs:(b + 1) * bs], k, out=static_x, tgt=static_y)
-            opt.sync_lr()
             if use_graph and graph is None and k >= 2:
                 graph = CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True)
             if graph is not None:

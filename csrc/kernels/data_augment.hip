@@ -26,10 +26,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // each thread gathers its 8 source bytes (L2/Infinity-Cache hits) and writes
 // 8 contiguous outputs with one 16-B (bf16) or two 16-B (fp32) stores.
 // NHWC layouts: one thread per (sample, row, pixel), C channels each.
-__global__ void __launch_bounds__(256)
-augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
-               const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad, uint64_t seed,
-               int train, int layout, void* __restrict__ out, int64_t* __restrict__ tgt_out) {
+__device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
+                                             const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad,
+                                             uint64_t seed, int train, int layout, void* __restrict__ out,
+                                             int64_t* __restrict__ tgt_out) {
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
   const int G = W / 8;  // 8-pixel groups per row (W % 8 == 0 checked on the host)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -101,6 +101,24 @@ augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ l
   }
 }
 
+// cursor (optional): device-side step counter k (read only).  The batch is rows [k % nbatch * B, +B) of
+// the epoch's index permutation `idx` and the augmentation seed is seed + k (DeviceLoader.batch_seed(k)),
+// so a captured training step draws a new batch on every replay with no host work.  The counter is
+// advanced by its owner (the training step's LR-table kernel); advancing it here would need a
+// completion counter every workgroup hits with an atomic — measured 26 vs 6.6 us for 768 workgroups.
+__global__ void __launch_bounds__(256)
+augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
+               const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad, uint64_t seed,
+               int train, int layout, void* __restrict__ out, int64_t* __restrict__ tgt_out,
+               const int* __restrict__ cursor, int nbatch) {
+  if (cursor) {
+    const int k = *cursor;
+    idx += (size_t)(k % nbatch) * B;
+    seed += (uint64_t)k;
+  }
+  augment_body(images, labels, idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);
+}
+
 }  // namespace ddpx
 
 using namespace ddpx;
@@ -114,6 +132,21 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
   if (layout == OUT_NHWC8_BF16 && C > 8) return -2;
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
-                     idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);
+                     idx, B, C, H, W, pad, seed, train, layout, out, tgt_out, (const int*)nullptr, 1);
+  return (int)hipGetLastError();
+}
+
+// Batch k = *cursor of a device-resident epoch permutation (idx_all: nbatch x B indices), seed + k.
+// The cursor is read, not advanced.  Graph-capturable.
+DDPX_API int ddpx_augment_cursor(const void* images, const int64_t* labels, const int64_t* idx_all, int nbatch,
+                                 int B, int C, int H, int W, int pad, uint64_t seed, int train, int layout, void* out,
+                                 int64_t* tgt_out, const int* cursor, hipStream_t s) {
+  if (B <= 0 || nbatch <= 0 || !cursor) return -3;
+  if (W % 8) return -1;
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
+  if (layout == OUT_NHWC8_BF16 && C > 8) return -2;
+  const int n = nhwc ? B * H * W : B * C * H * (W / 8);
+  hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
+                     idx_all, B, C, H, W, pad, seed, train, layout, out, tgt_out, cursor, nbatch);
   return (int)hipGetLastError();
 }

@@ -144,6 +144,37 @@ class DeviceLoader:
             return out, tgt
         return x, y
 
+    def cursor_batch(self, idx_all: torch.Tensor, nbatch: int, out, tgt, counter: torch.Tensor | None = None):
+        """Batch k of ``idx_all`` (nbatch x batch_size indices) with augmentation seed ``batch_seed(k)``, k read
+        on the device from ``counter`` (int32 [1]), written into the static ``out`` / ``tgt``.
+
+        ``counter`` is the training step's own step counter (``SGD.step_counter()``: the LR-table kernel
+        advances it once per step), so a captured step draws the next batch on every replay with no
+        host work.  Without one, the loader keeps a private counter and advances it after the launch."""
+        if self.device.type != "cuda":
+            raise RuntimeError("cursor_batch needs the GPU-resident pipeline")
+        own = counter is None
+        if own:
+            if getattr(self, "_cursor", None) is None:
+                self._cursor = torch.zeros(1, dtype=torch.int32, device=self.device)
+            counter = self._cursor
+        if counter.dtype != torch.int32 or not counter.is_cuda:
+            raise ValueError("cursor_batch: counter must be an int32 device tensor")
+        B = self.batch_size
+        if idx_all.numel() < nbatch * B or idx_all.dtype != torch.int64 or not idx_all.is_cuda:
+            raise ValueError("cursor_batch: idx_all must hold nbatch x batch_size int64 device indices")
+        _, C, H, W = self.ds.images.shape
+        if out.numel() < B * C * H * W or tgt.numel() < B:
+            raise ValueError("cursor_batch: output buffers too small")
+        lib = native.kernels()
+        rc = lib.ddpx_augment_cursor(self.ds.images.data_ptr(), self.ds.labels.data_ptr(), idx_all.data_ptr(), nbatch,
+                                     B, C, H, W, self.pad, self.batch_seed(0), int(self.train), LAYOUTS[self.layout],
+                                     out.data_ptr(), tgt.data_ptr(), counter.data_ptr(), native.stream_handle())
+        native.check(rc, "ddpx_augment_cursor")
+        if own:
+            counter.add_(1)
+        return out, tgt
+
     def __iter__(self):
         idx = self._epoch_indices()
         for step in range(len(self)):

@@ -105,6 +105,11 @@ class SGD(Optimizer):
         self._lr_counter = torch.tensor([scheduler.last_epoch], dtype=torch.int32, device=self.lr_dev.device)
         return True
 
+    def step_counter(self):
+        """The device step counter the LR-table kernel advances once per ``device_lr_step`` (int32 [1]), or
+        None without a device schedule; other per-step device work (the data cursor) may read it."""
+        return getattr(self, "_lr_counter", None) if self._lr_table is not None else None
+
     def device_lr_step(self):
         if self._lr_table is None:
             return
