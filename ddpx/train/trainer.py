@@ -24,6 +24,7 @@ from __future__ import annotations
 import time
 
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 from torch import nn
 
@@ -159,5 +160,9 @@ class Trainer:
                 self.model.consolidate()  # collective: sharded optimizer -> complete fp32 state on every rank
             if (not self.distributed or self.rank == 0) and epoch % self.save_every == 0:
                 self._save_checkpoint(epoch)
+            if self.distributed and epoch % self.save_every == 0 and dist.is_initialized():
+                # no rank runs ahead of a half-written checkpoint (the reference has no
+                # barrier here, multigpu.py:118); one CPU barrier per save
+                dist.barrier()
         if torch.cuda.is_available() and next(self.model.parameters()).is_cuda:
             torch.cuda.synchronize()
