@@ -70,6 +70,10 @@ def parse():
     p.add_argument("--defer_gather", type=int, default=None,
                    help="1: ZeRO-1 all-gathers issued at the start of the next step and waited per chunk "
                         "inside the forward (default 1 with --shard_optimizer on the MLPs)")
+    p.add_argument("--comm_side_optimizer", type=int, default=None,
+                   help="1: ZeRO-1 shard updates on the RCCL stream behind each reduce-scatter (one join per "
+                        "step instead of one per bucket; default 1 with --shard_optimizer; measured 0.432-0.434 "
+                        "vs 0.436-0.438 ms/step at --ddp_single, profiles/r1_side)")
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
@@ -148,6 +152,8 @@ def resolve_defaults(args, world):
         # 4096-column layer), and the wide MLP measured 5.52 vs 4.32 ms/step with 64 MB chunks at world
         # size 1 (profiles/r1_chunk); the multi-GPU benefit is unmeasured here, so it stays opt-in
         args.chunk_mb = 0.0
+    if args.comm_side_optimizer is None:
+        args.comm_side_optimizer = int(bool(args.shard_optimizer))
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 
@@ -174,7 +180,8 @@ def build_ddpx(args, device, world):
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=bool(args.overlap_optimizer),
                                       shard_optimizer=bool(args.shard_optimizer), chunk_mb=args.chunk_mb or None,
-                                      defer_gather=bool(args.defer_gather))
+                                      defer_gather=bool(args.defer_gather),
+                                      comm_side_optimizer=bool(args.comm_side_optimizer))
         if args.overlap_optimizer or args.shard_optimizer:
             net.attach_optimizer(opt)
     sched = one_cycle(opt, resolve_steps_per_epoch("compat", 0, world > 1))
@@ -345,7 +352,8 @@ def main():
                        " fused-into-backward" if (args.impl == "ddpx" and not multi and not args.no_fused_optimizer)
                        else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "chunk_mb": args.chunk_mb or None,
-                   "defer_gather": bool(args.defer_gather) if multi else None, "final_loss": round(final_loss, 4),
+                   "defer_gather": bool(args.defer_gather) if multi else None,
+                   "comm_side_optimizer": bool(args.comm_side_optimizer) if multi else None, "final_loss": round(final_loss, 4),
                    "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
                    "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
                    "replicas_consistent": consistent,

@@ -375,6 +375,7 @@ DDPX_API int ddpx_reducer_wait_bucket(void* h, int i, hipStream_t s) {
   Reducer* r = static_cast<Reducer*>(h);
   Bucket& b = r->buckets[i];
   if (!b.launched) return -1;
+  if (s == r->comm->stream) return 0;  // already in stream order (and a captured self-wait is invalid)
   return (int)hipStreamWaitEvent(s, b.done, 0);
 }
 
@@ -430,10 +431,13 @@ DDPX_API int ddpx_reducer_gather(void* h, int i, hipStream_t compute) {
   Bucket& b = r->buckets[i];
   if (!b.gptr) return -2;
   Comm* c = r->comm;
-  hipError_t he = hipEventRecord(b.gready, compute);
-  if (he != hipSuccess) return (int)he;
-  he = hipStreamWaitEvent(c->stream, b.gready, 0);
-  if (he != hipSuccess) return (int)he;
+  hipError_t he;
+  if (compute != c->stream) {  // issued from the comm stream itself: stream order suffices
+    he = hipEventRecord(b.gready, compute);
+    if (he != hipSuccess) return (int)he;
+    he = hipStreamWaitEvent(c->stream, b.gready, 0);
+    if (he != hipSuccess) return (int)he;
+  }
   size_t shard = b.gcount / (size_t)c->nranks;
   const char* send = static_cast<const char*>(b.gptr) + (size_t)c->rank * shard * dtype_size(b.gdtype);
   int e = ddpx_comm_allgather(c, send, b.gptr, shard, b.gdtype, c->stream);
@@ -449,7 +453,7 @@ DDPX_API int ddpx_reducer_wait_gather(void* h, int i, hipStream_t s) {
   if (i < 0 || i >= (int)r->buckets.size()) return -1;
   Bucket& b = r->buckets[i];
   if (!b.gathering) return 0;
-  hipError_t he = hipStreamWaitEvent(s, b.gdone, 0);
+  hipError_t he = s == r->comm->stream ? hipSuccess : hipStreamWaitEvent(s, b.gdone, 0);
   b.gathering = false;
   return (int)he;
 }

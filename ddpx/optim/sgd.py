@@ -141,11 +141,30 @@ class SGD(Optimizer):
         if src is not None and getattr(src, "sharded", False):
             # ZeRO-1: each rank updates only its shard of every sharded bucket (gradients were
             # reduce-scattered), then the bucket's parameter copy is all-gathered in place
-            for b in src.bucket_order():
-                src.wait_bucket(b)
-                for (start, end) in src.update_ranges(b):
-                    self._update(start, end, g)
-                src.gather_bucket(b)
+            side = src.optimizer_stream() if hasattr(src, "optimizer_stream") else None
+            if side is None:
+                for b in src.bucket_order():
+                    src.wait_bucket(b)
+                    for (start, end) in src.update_ranges(b):
+                        self._update(start, end, g)
+                    src.gather_bucket(b)
+            else:
+                # shard updates on the communicator stream, in stream order behind each bucket's
+                # reduce-scatter: one compute -> comm edge (end of backward: nothing still reads the
+                # weights) and one comm -> compute join at the end instead of a join per bucket
+                cur = torch.cuda.current_stream()
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    for b in src.bucket_order():
+                        src.claim_bucket_on_comm_stream(b)
+                        for (start, end) in src.update_ranges(b):
+                            self._update(start, end, g)
+                        src.gather_bucket(b)
+                done = torch.cuda.Event()
+                done.record(side)
+                cur.wait_event(done)
             src.optimizer_done()
         elif any(self.flat.updated):
             # fused-backward parameters are already stepped; update the rest range by range

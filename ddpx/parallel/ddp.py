@@ -270,8 +270,9 @@ class DistributedDataParallel(nn.Module):
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
                  reduce_single: bool = False, shard_optimizer: bool = False, chunk_mb: float | None = None,
-                 defer_gather: bool = False):
+                 defer_gather: bool = False, comm_side_optimizer: bool = False):
         super().__init__()
+        self.comm_side_optimizer = comm_side_optimizer
         self.module = module
         dev = next(module.parameters()).device
         self.device = dev
@@ -444,6 +445,12 @@ class DistributedDataParallel(nn.Module):
         if b in self._gather_wait:  # the shard about to be updated must not race its pending gather
             self.reducer.wait_gather(b)
             self._gather_wait.discard(b)
+
+    def claim_bucket_on_comm_stream(self, b):
+        """wait_bucket() for an update issued ON the communicator stream: the reduce-scatter and any
+        pending gather of ``b`` precede it in stream order, so only the bookkeeping remains (a HIP graph
+        capture must not see an event waited on by the stream that recorded it)."""
+        self._gather_wait.discard(b)
 
     def update_ranges(self, b):
         s, e = self.bucket_ranges[b]
@@ -631,6 +638,15 @@ class DistributedDataParallel(nn.Module):
     def wait_range(self, start, end):
         b = self.bucket_ranges.index((start, end))
         self.reducer.wait_bucket(b)
+
+    def optimizer_stream(self):
+        """The stream the ZeRO-1 shard updates run on when ``comm_side_optimizer`` is set (the native
+        RCCL stream, right behind each bucket's reduce-scatter: no per-bucket join back into the compute
+        stream), else None."""
+        if (self.comm_side_optimizer and self.sharded and isinstance(self.reducer, _NativeReducer)
+                and getattr(self.comm, "stream", None) is not None):
+            return self.comm.stream
+        return None
 
     def optimizer_done(self):
         if self.sharded:

@@ -69,6 +69,9 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this (MB of gradient) into row-chunk DDP buckets")
+    p.add_argument("--comm_side_optimizer", action="store_true",
+                   help="with --shard_optimizer on the RCCL path: shard updates on the communicator stream behind "
+                        "each reduce-scatter (one join per step instead of one per bucket)")
     p.add_argument("--defer_gather", action="store_true",
                    help="with --shard_optimizer: all-gather updated shards at the start of the next forward, "
                         "overlapped with it (MLP native path)")
@@ -210,7 +213,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
                                       first_bucket_mb=args.first_bucket_mb,
                                       overlap_optimizer=args.overlap_optimizer,
                                       shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
-                                      defer_gather=args.defer_gather)
+                                      defer_gather=args.defer_gather,
+                                      comm_side_optimizer=args.comm_side_optimizer)
         if args.overlap_optimizer:
             net.attach_optimizer(optimizer)
     metrics = MetricsWriter(args.metrics, rank) if args.metrics else None

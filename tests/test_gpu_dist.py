@@ -48,8 +48,9 @@ def test_rccl_collectives(gpu, pg):
     c.close()
 
 
-@pytest.mark.parametrize("overlap,shard", [(False, False), (True, False), (False, True), (True, True)])
-def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard):
+@pytest.mark.parametrize("overlap,shard,side", [(False, False, False), (True, False, False), (False, True, False),
+                                               (True, True, False), (True, True, True)])
+def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard, side):
     import ddpx
     from ddpx.models import MLP
     from ddpx.optim.sgd import SGD
@@ -63,7 +64,7 @@ def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard):
     comm = RcclComm(gpu)
     oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
     da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
-                                 overlap_optimizer=overlap, shard_optimizer=shard)
+                                 overlap_optimizer=overlap, shard_optimizer=shard, comm_side_optimizer=side)
     assert len(da.bucket_ranges) >= 2
     if shard:  # native MLP weights are shadow-only: reduce-scatter + bf16 shadow gather, biases replicated
         assert da.sharded and da.gather_what == "shadow" and da.bucket_modes[-1] == 0
@@ -86,9 +87,10 @@ def test_native_reducer_ddp_matches_plain(gpu, pg, overlap, shard):
     comm.close()
 
 
-@pytest.mark.parametrize("shard,chunk_mb,defer", [(False, None, False), (True, None, False), (True, 0.25, True),
-                                                  (False, 0.25, False)])
-def test_graph_capture_with_rccl(gpu, pg, shard, chunk_mb, defer):
+@pytest.mark.parametrize("shard,chunk_mb,defer,side", [(False, None, False, False), (True, None, False, False),
+                                                       (True, 0.25, True, False), (False, 0.25, False, False),
+                                                       (True, None, True, True), (True, None, False, True)])
+def test_graph_capture_with_rccl(gpu, pg, shard, chunk_mb, defer, side):
     """Whole step (fwd, bwd with bucketed all-reduce on the comm stream, SGD) in one HIP graph."""
     import ddpx
     from ddpx.models import MLP
@@ -103,7 +105,9 @@ def test_graph_capture_with_rccl(gpu, pg, shard, chunk_mb, defer):
         ddpx.prepare_model(m, gpu)
     comm = RcclComm(gpu)
     da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
-                                 shard_optimizer=shard, chunk_mb=chunk_mb, defer_gather=defer)
+                                 shard_optimizer=shard, chunk_mb=chunk_mb, defer_gather=defer,
+                                 comm_side_optimizer=side)
+    assert (da.optimizer_stream() is not None) == side
     if chunk_mb:
         assert da.chunk_bucket
     assert da.defer_gather == defer
