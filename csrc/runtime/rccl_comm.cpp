@@ -132,6 +132,7 @@ struct Bucket {
 
 struct Reducer {
   Comm* comm = nullptr;
+  std::vector<int> lazy;  // buckets whose collective is not issued yet (lazy_comm)
   int op = ncclAvg;
   std::vector<Bucket> buckets;
   int launched = 0;
@@ -325,15 +326,48 @@ DDPX_API int ddpx_reducer_prepare(void* h) {
     b.pending = b.expected;
     b.launched = false;
   }
+  r->lazy.clear();
   r->launched = 0;
   return 0;
 }
 
+// Lazy issue (DDPX_LAZY_COMM=1): the bucket's ready event is recorded on the compute stream at once,
+// but the comm-stream wait + collective are issued at the reducer's next call, i.e. after the caller
+// has enqueued its next compute kernel.  Same dependencies and collective order; inside a HIP graph
+// capture the next compute node is then created before the collective node.
+static bool lazy_comm() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_LAZY_COMM");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static int issue_bucket(Reducer* r, Bucket& b);
+
+static int flush_lazy(Reducer* r) {
+  for (int i : r->lazy) {
+    int e = issue_bucket(r, r->buckets[i]);
+    if (e) return e;
+  }
+  r->lazy.clear();
+  return 0;
+}
+
 static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
-  Comm* c = r->comm;
   hipError_t he = hipEventRecord(b.ready, compute);
   if (he != hipSuccess) return (int)he;
-  he = hipStreamWaitEvent(c->stream, b.ready, 0);
+  b.launched = true;
+  if (lazy_comm()) {
+    r->lazy.push_back((int)(&b - r->buckets.data()));
+    return 0;
+  }
+  return issue_bucket(r, b);
+}
+
+static int issue_bucket(Reducer* r, Bucket& b) {
+  Comm* c = r->comm;
+  hipError_t he = hipStreamWaitEvent(c->stream, b.ready, 0);
   if (he != hipSuccess) return (int)he;
   if (r->launched == 0) hipEventRecord(r->t_first, c->stream);
   int e;
@@ -349,7 +383,6 @@ static int launch_bucket(Reducer* r, Bucket& b, hipStream_t compute) {
   if (he != hipSuccess) return (int)he;
   hipEventRecord(r->t_last, c->stream);
   r->timed = true;
-  b.launched = true;
   r->launched++;
   return 0;
 }
@@ -362,10 +395,12 @@ DDPX_API int ddpx_reducer_mark_ready(void* h, int i, int n, hipStream_t compute)
   if (i < 0 || i >= (int)r->buckets.size()) return -1;
   Bucket& b = r->buckets[i];
   if (b.launched) return -2;  // marked twice in one backward
+  int e = flush_lazy(r);
+  if (e) return e;
   b.pending -= n;
   if (b.pending > 0) return 0;
   if (b.pending < 0) return -3;
-  int e = launch_bucket(r, b, compute);
+  e = launch_bucket(r, b, compute);
   return e ? e : 1;
 }
 
@@ -375,6 +410,7 @@ DDPX_API int ddpx_reducer_wait_bucket(void* h, int i, hipStream_t s) {
   Reducer* r = static_cast<Reducer*>(h);
   Bucket& b = r->buckets[i];
   if (!b.launched) return -1;
+  if (int e = flush_lazy(r)) return e;
   if (s == r->comm->stream) return 0;  // already in stream order (and a captured self-wait is invalid)
   return (int)hipStreamWaitEvent(s, b.done, 0);
 }
@@ -386,6 +422,7 @@ DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
   Reducer* r = static_cast<Reducer*>(h);
   hipEventRecord(r->t_bwd, compute);
   r->bwd_marked = true;
+  if (int e = flush_lazy(r)) return -1000 - e;
   int forced = 0;
   for (auto& b : r->buckets) {
     if (!b.launched) {
@@ -394,6 +431,7 @@ DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
       forced++;
     }
   }
+  if (int e = flush_lazy(r)) return -1000 - e;
   for (auto& b : r->buckets) {
     hipError_t he = hipStreamWaitEvent(compute, b.done, 0);
     if (he != hipSuccess) return -(int)he;
@@ -405,7 +443,9 @@ DDPX_API int ddpx_reducer_finalize(void* h, hipStream_t compute) {
 DDPX_API int ddpx_reducer_mark_backward_end(void* h, hipStream_t compute) {
   Reducer* r = static_cast<Reducer*>(h);
   r->bwd_marked = true;
-  return (int)hipEventRecord(r->t_bwd, compute);
+  hipError_t he = hipEventRecord(r->t_bwd, compute);
+  if (int e = flush_lazy(r)) return e;
+  return (int)he;
 }
 
 // Communication time of the last completed iteration and the part of it after backward ended
@@ -430,6 +470,7 @@ DDPX_API int ddpx_reducer_gather(void* h, int i, hipStream_t compute) {
   if (i < 0 || i >= (int)r->buckets.size()) return -1;
   Bucket& b = r->buckets[i];
   if (!b.gptr) return -2;
+  if (int e = flush_lazy(r)) return e;
   Comm* c = r->comm;
   hipError_t he;
   if (compute != c->stream) {  // issued from the comm stream itself: stream order suffices
