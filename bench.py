@@ -108,6 +108,9 @@ def setup_dist(args):
     if args.comm == "host":
         local = local % torch.cuda.device_count()  # ranks may share a device
     torch.cuda.set_device(local)
+    if n == 1 and args.ddp_single and world == 1:
+        # time the DDP machinery, not RCCL's one-rank in-place copy kernels (identity at world size 1)
+        os.environ.setdefault("DDPX_COMM_SKIP_IDENTITY", "1")
     if world > 1 or (n == 1 and args.ddp_single):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1 and "MASTER_PORT" not in os.environ:
