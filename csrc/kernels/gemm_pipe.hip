@@ -163,7 +163,15 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
     return e && e[0] == '1' ? 1 : 0;
   }();
   p.sgd_plain = sgd_plain;
-  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  // Weight gradients stored to a buffer (DDP path: bf16 / fp32 gradient output, no fused optimizer):
+  // the 256x256 8-wave tile moves a quarter of the 64x128 tile's L2->LDS operand bytes and is faster
+  // once it fills half the chip (MI355X, K = 512: 35.4 vs 46.1 us on 4096x4096, 30.9 vs 38.6 us on
+  // 4096x3072, fp32 out; benchmarks/wgrad_probe.py, profiles/r1_wgrad).  The fused-SGD epilogue keeps
+  // 64x128 (its HBM stream wants two resident workgroups per CU: 78.9 vs 72.8 us).
+  if (tile_cfg < 0 && !a_kcontig && !b_kcontig && epi != pipe::EPI_SGD && !colsum &&
+      ((M + 255) / 256) * ((N + 255) / 256) >= 128)
+    cfg = 13;
   // Master/momentum LDS prefetch for the fused-SGD tiles: opt-in (DDPX_SGD_PREFETCH=1).  Measured
   // slower on MI355X (toy fc1 64x128: 112 vs 77 us; profiles/r1_epi): the 64 KiB side buffer halves
   // occupancy and the prefetch lands on the critical path of short (K = 512) main loops.

@@ -17,7 +17,7 @@ def _rand_bf16(*shape, dev):
                          [("pipe", t) for t in range(-1, 14)])
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
-                                 (200, 136, 1000)])
+                                 (200, 136, 1000), (2048, 4096, 512)])
 def test_gemm_layouts(gpu, impl_tile, layout, MNK):
     impl, tile = impl_tile
     from ddpx.ops.gemm import matmul
