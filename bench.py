@@ -108,6 +108,9 @@ def setup_dist(args):
     if args.comm == "host":
         local = local % torch.cuda.device_count()  # ranks may share a device
     torch.cuda.set_device(local)
+    # a hung collective aborts the communicator with a per-rank message after this long instead of
+    # stalling the benchmark indefinitely (RcclComm watchdog; eager steps are tracked)
+    os.environ.setdefault("DDPX_COMM_TIMEOUT", "300")
     if n == 1 and args.ddp_single and world == 1:
         # time the DDP machinery, not RCCL's one-rank in-place copy kernels (identity at world size 1)
         os.environ.setdefault("DDPX_COMM_SKIP_IDENTITY", "1")
