@@ -30,20 +30,22 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
   const float lr = lr_ptr ? *lr_ptr : lr_host;
   const int64_t nv = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // read-once / write-once streams (master, momentum, gradient): non-temporal, so the optimizer does
+  // not leave hundreds of MB of dirty lines in L2 / MALL for the next forward's GEMMs to write back
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-    f32x4 pv = reinterpret_cast<const f32x4*>(p)[i];
+    f32x4 pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
     f32x4 gv;
     if constexpr (GBF16) {
-      u32x2 raw = reinterpret_cast<const u32x2*>(g)[i];
+      u32x2 raw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g) + i);
       gv[0] = __uint_as_float(raw[0] << 16);
       gv[1] = __uint_as_float(raw[0] & 0xffff0000u);
       gv[2] = __uint_as_float(raw[1] << 16);
       gv[3] = __uint_as_float(raw[1] & 0xffff0000u);
     } else {
-      gv = reinterpret_cast<const f32x4*>(g)[i];
+      gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
     }
     // same fma sequence as sgd_apply() (fused-backward epilogues): bitwise-identical updates
-    f32x4 b = reinterpret_cast<const f32x4*>(buf)[i];
+    f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf) + i);
     f32x4 po, bo;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -55,9 +57,9 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
       }
       po[q] = fmaf(-lr, d, pv[q]);
     }
-    if (mom != 0.f) reinterpret_cast<f32x4*>(buf)[i] = bo;
+    if (mom != 0.f) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(buf) + i);
     pv = po;
-    reinterpret_cast<f32x4*>(p)[i] = pv;
+    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4*>(p) + i);
     if (shadow) {
       u32x2 s = {pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3])};
       reinterpret_cast<u32x2*>(shadow)[i] = s;
