@@ -60,9 +60,13 @@ def parse():
     p.add_argument("--shard_optimizer", type=int, default=None,
                    help="1: ZeRO-1 reduce-scatter / shard update / bf16 all-gather (default 1 for N>1)")
     p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
+    p.add_argument("--fused_optimizer", type=int, default=None,
+                   help="N=1: 1 = SGD inside the weight-gradient GEMM epilogues, 0 = fp32 gradients then one "
+                        "non-temporal flat SGD pass.  Default 0 for the toy MLP (0.290 vs 0.306 ms/step, same "
+                        "numerics: profiles/r1_n1alt), 1 for the others (wide MLP 2.82 vs 2.97 ms/step)")
     p.add_argument("--grad_dtype", default="auto", choices=["auto", "fp32", "bf16"],
                    help="gradient buffer / reduction dtype (bf16 = values of the bf16 MFMA wgrads, as under "
-                        "autocast); auto: fp32 at N=1 (grads never leave the fused kernels), bf16 for N>1")
+                        "autocast); auto: fp32 at N=1 (same numerics as the fused optimizer), bf16 for N>1")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this into row-chunk buckets, each reduced as soon as its "
@@ -158,6 +162,10 @@ def resolve_defaults(args, world):
         # 4096-column layer), and the wide MLP measured 5.52 vs 4.32 ms/step with 64 MB chunks at world
         # size 1 (profiles/r1_chunk); the multi-GPU benefit is unmeasured here, so it stays opt-in
         args.chunk_mb = 0.0
+    if args.fused_optimizer is None:
+        args.fused_optimizer = 0 if args.model == "mlp" else 1
+    if args.no_fused_optimizer:
+        args.fused_optimizer = 0
     if args.comm_side_optimizer is None:
         args.comm_side_optimizer = int(bool(args.shard_optimizer))
     if args.defer_gather is None:
@@ -177,7 +185,7 @@ def build_ddpx(args, device, world):
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update is fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
-              fused_backward=(world == 1 and not args.ddp_single and not args.no_fused_optimizer))
+              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer)))
     net = model
     if world > 1 or args.ddp_single:
         comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
@@ -355,7 +363,7 @@ def main():
                    "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
                    "graph_steps": (args.graph_steps if args.impl == "ddpx" and not args.no_graph else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
-                       " fused-into-backward" if (args.impl == "ddpx" and not multi and not args.no_fused_optimizer)
+                       " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer)
                        else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "chunk_mb": args.chunk_mb or None,
                    "defer_gather": bool(args.defer_gather) if multi else None,
