@@ -68,15 +68,17 @@ struct SgdArgs {
   float mom, wd;
 };
 
+// Master and momentum are read-once / write-once streams: non-temporal, so the update leaves no
+// dirty L2 / MALL lines for the next forward's GEMMs to write back (profiles/r1_sgdnt).
 __device__ __forceinline__ void sgd_apply(const SgdArgs& s, size_t i, float g, float lr) {
-  float p = s.p[i];
+  float p = __builtin_nontemporal_load(s.p + i);
   float d = fmaf(s.wd, p, g);
   if (s.mom != 0.f) {
-    d = fmaf(s.mom, s.buf[i], d);
-    s.buf[i] = d;
+    d = fmaf(s.mom, __builtin_nontemporal_load(s.buf + i), d);
+    __builtin_nontemporal_store(d, s.buf + i);
   }
   p = fmaf(-lr, d, p);
-  s.p[i] = p;
+  __builtin_nontemporal_store(p, s.p + i);
   if (s.shadow) s.shadow[i] = f2bf(p);
 }
 
