@@ -32,8 +32,7 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   // read-once / write-once streams (master, momentum, gradient): non-temporal, so the optimizer does
   // not leave hundreds of MB of dirty lines in L2 / MALL for the next forward's GEMMs to write back
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-    f32x4 pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
+  auto load_g = [&](int64_t i) -> f32x4 {
     f32x4 gv;
     if constexpr (GBF16) {
       u32x2 raw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g) + i);
@@ -44,8 +43,10 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
     } else {
       gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
     }
+    return gv;
+  };
+  auto update = [&](int64_t i, f32x4 pv, f32x4 gv, f32x4 b) {
     // same fma sequence as sgd_apply() (fused-backward epilogues): bitwise-identical updates
-    f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf) + i);
     f32x4 po, bo;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -58,12 +59,28 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
       po[q] = fmaf(-lr, d, pv[q]);
     }
     if (mom != 0.f) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(buf) + i);
-    pv = po;
-    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4*>(p) + i);
+    __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(p) + i);
     if (shadow) {
-      u32x2 s = {pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3])};
-      reinterpret_cast<u32x2*>(shadow)[i] = s;
+      u32x2 sh = {pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      reinterpret_cast<u32x2*>(shadow)[i] = sh;
     }
+  };
+  // two vectors per thread per iteration, all six loads issued before either update: twice the
+  // bytes in flight per wave of the one-vector loop
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += 2 * stride) {
+    const int64_t j = i + stride;
+    const bool two = j < nv;
+    const f32x4 p0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
+    const f32x4 g0 = load_g(i);
+    const f32x4 b0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf) + i);
+    f32x4 p1 = p0, g1 = g0, b1 = b0;
+    if (two) {
+      p1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + j);
+      g1 = load_g(j);
+      b1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf) + j);
+    }
+    update(i, p0, g0, b0);
+    if (two) update(j, p1, g1, b1);
   }
   // scalar tail (n not a multiple of 4)
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
