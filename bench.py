@@ -6,78 +6,77 @@ at 1/2/4/8 MI355X".  Config: MLP 3072→4096→4096→10 on CIFAR
 synthetic data (uint8 images resident on the GPU, RandomCrop+Flip augmentation
 each step as in the reference), batch 512 per GPU (the reference's default
 ``--batch_size``), SGD lr 0.4 / momentum 0.9 / wd 5e-4 with the reference's
-one-cycle schedule, fp32 master weights and gradients, bf16 MFMA compute.
+one-cycle schedule, fp32 master weights, fp32 gradients, bf16 MFMA compute.
 Weak scaling: per-GPU batch fixed as N grows.
 
     python bench.py --gpus 1 --steps 200 --warmup 30
-    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+    python bench.py --gpus 8                     # self-launches 8 ranks (torch.distributed.run child)
+    torchrun --nproc-per-node 8 bench.py --gpus 8  # or under an external launcher
+    python bench.py --gpus 2 --comm host         # 2 ranks sharing ONE GPU (logic rehearsal, not perf)
+    python bench.py --device cpu [--gpus 2]      # BASELINE config 1 (CPU, gloo for N > 1)
 
-Every timed step does the whole job: batch gather+augment, forward, loss,
-backward, bucketed gradient all-reduce (N>1), optimizer step and LR update.
-``--impl torch`` runs the stock PyTorch-ROCm recipe (nn.Linear + autocast,
-torch DDP over RCCL, foreach SGD) on the same data for the baseline number.
+N > 1 runs the stock DDP algorithm (reference ``multigpu.py:89``): every rank keeps the full fp32
+replica, gradients are averaged with an fp32 RCCL all-reduce (``ncclAvg``) bucket by bucket while
+backward runs, and each bucket's SGD update starts as soon as its all-reduce lands.  bf16 gradient
+communication (``--grad_dtype bf16``) and ZeRO-1 (``--shard_optimizer 1``) are opt-in and are labelled
+in the output line.
+
+Every timed step does the whole job: batch gather+augment, forward, loss, backward, bucketed gradient
+all-reduce (N > 1), optimizer step and LR update.  ``--impl torch`` runs the stock PyTorch-ROCm recipe
+(nn.Linear + autocast, torch DDP over RCCL, foreach SGD) on the same data; at N = 1 the ddpx line also
+carries that recipe measured in the same process (``stock_same_run``).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 BASELINE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
-# The reference publishes no numbers (BASELINE.md): vs_baseline stays null.  For context the line also
-# carries the ratio to the stock PyTorch-ROCm recipe measured on one MI355X with this same data
-# (--impl torch; profiles/r1_first, profiles/r1_gemm, profiles/r1_tune), samples/s at batch 512.
-STOCK_MEASURED_1GPU = {"mlp": 706_000.0, "mlp_wide": 100_040.0, "vgg": 26_400.0, "deepnn": 118_494.0}
+LAUNCHER_ENV = "DDPX_BENCH_LAUNCHER"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1, help="ranks (GPUs; CPU processes with --device cpu)")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch_size", type=int, default=512, help="per-GPU batch")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: BASELINE config 1 (torch CPU kernels under the ddpx engine, gloo for N > 1)")
+    p.add_argument("--batch_size", type=int, default=512, help="per-rank batch")
     p.add_argument("--hidden", type=int, default=None, help="MLP hidden width (default 4096 toy, 16384 wide)")
     p.add_argument("--layers", type=int, default=3)
     p.add_argument("--model", default="mlp", choices=["mlp", "mlp_wide", "vgg", "deepnn"])
     p.add_argument("--impl", default="ddpx", choices=["ddpx", "torch"])
-    p.add_argument("--fp8", type=int, default=0,
-                   help="1: MX-FP8 hidden-layer forward/wgrad GEMMs (mlp models).  Off by default: on MI355X the "
-                        "wide MLP is optimizer-stream bound and bf16 measured faster (2.69 vs 3.07 ms/step)")
+    p.add_argument("--fp8", type=int, default=None,
+                   help="1: MX-FP8 hidden-layer forward / weight-gradient GEMMs (MLP models; default 0)")
     p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--graph_steps", type=int, default=1,
                    help="training steps per captured HIP graph (the launch gap between replays is paid once "
-                        "per graph); the timed region still runs exactly --steps steps.  Measured: 4 steps "
-                        "0.299 vs 0.304 ms/step single-GPU (within run-to-run noise) but 0.70 vs 0.43 ms/step "
-                        "with the DDP reducer (cross-queue comm-stream edges inside one graph), so default 1")
+                        "per graph); the timed region still runs exactly --steps steps")
     p.add_argument("--overlap_optimizer", type=int, default=None,
                    help="1: per-bucket optimizer as each collective lands (default 1 for N>1)")
     p.add_argument("--shard_optimizer", type=int, default=None,
-                   help="1: ZeRO-1 reduce-scatter / shard update / bf16 all-gather (default 1 for N>1)")
+                   help="1: ZeRO-1 reduce-scatter / shard update / all-gather (opt-in, default 0)")
     p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
     p.add_argument("--fused_optimizer", type=int, default=None,
                    help="N=1: 1 = SGD inside the weight-gradient GEMM epilogues, 0 = fp32 gradients then one "
-                        "non-temporal flat SGD pass.  Default 0 for the toy MLP (0.290 vs 0.306 ms/step, same "
-                        "numerics: profiles/r1_n1alt), 1 for the others (wide MLP 2.82 vs 2.97 ms/step)")
+                        "non-temporal flat SGD pass.  Default 0 for the toy MLP (profiles/r1_n1alt), 1 for the others")
     p.add_argument("--grad_dtype", default="auto", choices=["auto", "fp32", "bf16"],
-                   help="gradient buffer / reduction dtype (bf16 = values of the bf16 MFMA wgrads, as under "
-                        "autocast); auto: fp32 at N=1 (same numerics as the fused optimizer), bf16 for N>1")
+                   help="gradient buffer / all-reduce dtype; auto = fp32 at every N (stock DDP precision)")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this into row-chunk buckets, each reduced as soon as its "
                         "slice of the weight gradient is written (opt-in; default off)")
     p.add_argument("--defer_gather", type=int, default=None,
-                   help="1: ZeRO-1 all-gathers issued at the start of the next step and waited per chunk "
-                        "inside the forward (default 1 with --shard_optimizer on the MLPs)")
+                   help="ZeRO-1 only: all-gathers issued at the start of the next step, waited per chunk")
     p.add_argument("--comm_side_optimizer", type=int, default=None,
-                   help="1: ZeRO-1 shard updates on the RCCL stream behind each reduce-scatter (one join per "
-                        "step instead of one per bucket; default 1 with --shard_optimizer; measured 0.432-0.434 "
-                        "vs 0.436-0.438 ms/step at --ddp_single, profiles/r1_side)")
+                   help="ZeRO-1 only: shard updates on the RCCL stream behind each reduce-scatter")
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
@@ -86,34 +85,75 @@ def parse():
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="host: gloo-staged collectives so several ranks can share one GPU (logic rehearsal on a "
                         "1-GPU box; not graph-capturable, not a performance path)")
+    p.add_argument("--stock_ref", type=int, default=None,
+                   help="1: also time the stock PyTorch recipe in this process (default 1 at N=1 on the GPU)")
+    p.add_argument("--stock_steps", type=int, default=30)
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def needs_self_launch(args, env=None) -> bool:
+    env = os.environ if env is None else env
+    return args.gpus > 1 and "WORLD_SIZE" not in env and "RANK" not in env
+
+
+def self_launch_cmd(args, argv, port: int):
+    """torch.distributed.run child command for ``--gpus N`` without an external launcher."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def self_launch(args, argv) -> int:
+    """Run N ranks as a torch.distributed.run child (reference: ``mp.spawn`` at multigpu.py:262-263).
+
+    This process never initialises HIP (no torch.cuda call), so starting the ranks is safe.  Their output is
+    forwarded line by line; rank 0 prints the one JSON line (with ``config.launcher`` set)."""
+    env = dict(os.environ)
+    env[LAUNCHER_ENV] = "self:torch.distributed.run"
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    proc = subprocess.Popen(self_launch_cmd(args, argv, _free_port()), env=env, stdout=subprocess.PIPE, text=True,
+                            bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
 
 
 def baseline_value(metric_key: str):
     try:
         with open(BASELINE_FILE) as f:
             b = json.load(f)
-        v = b.get("published", {}).get(metric_key) or b.get("measured_stock_pytorch", {}).get(metric_key)
+        v = b.get("published", {}).get(metric_key)
         return float(v) if v else None
     except Exception:
         return None
 
 
+# ------------------------------------------------------------------------------------------ setup
 def setup_dist(args):
+    import torch
+    import torch.distributed as dist
     n, impl = args.gpus, args.impl
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n:
-        if n > 1 and world == 1:
-            print(f"bench.py: --gpus {n} needs a launcher (torchrun --nproc-per-node {n})", file=sys.stderr)
-            sys.exit(2)
-    if args.comm == "host":
-        local = local % torch.cuda.device_count()  # ranks may share a device
-    torch.cuda.set_device(local)
-    # a hung collective aborts the communicator with a per-rank message after this long instead of
-    # stalling the benchmark indefinitely (RcclComm watchdog; eager steps are tracked)
+        print(f"bench.py: --gpus {n} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    cpu = args.device == "cpu"
+    if not cpu:
+        if args.comm == "host":
+            local = local % torch.cuda.device_count()  # ranks may share a device
+        torch.cuda.set_device(local)
+    # a hung collective is reported per rank after this long (RcclComm watchdog, eager steps and graph replays)
     os.environ.setdefault("DDPX_COMM_TIMEOUT", "300")
     if n == 1 and args.ddp_single and world == 1:
         # time the DDP machinery, not RCCL's one-rank in-place copy kernels (identity at world size 1)
@@ -121,13 +161,11 @@ def setup_dist(args):
     if world > 1 or (n == 1 and args.ddp_single):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1 and "MASTER_PORT" not in os.environ:
-            import socket
-            with socket.socket() as sk:
-                sk.bind(("127.0.0.1", 0))
-                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ["MASTER_PORT"] = str(_free_port())
         # ddpx: GPU collectives go through its own RCCL communicator; the c10d group only
         # bootstraps it (TCPStore) and carries CPU barriers/timing -> gloo.  torch: stock RCCL PG.
-        dist.init_process_group(backend="gloo" if impl == "ddpx" else "nccl", rank=rank, world_size=world)
+        backend = "gloo" if (impl == "ddpx" or cpu) else "nccl"
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
 
 
@@ -141,6 +179,8 @@ def make_data(args, device, rank, world, layout=None):
         layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
         if args.impl == "ddpx" and args.model in ("vgg", "deepnn"):
             layout = "nhwc8_bf16"
+        if device.type == "cpu":
+            layout = "nchw_f32"
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
 
 
@@ -148,19 +188,16 @@ def resolve_defaults(args, world):
     if args.hidden is None:
         args.hidden = 16384 if args.model == "mlp_wide" else 4096
     multi = world > 1 or args.ddp_single
+    if args.fp8 is None:
+        args.fp8 = 0
     if args.grad_dtype == "auto":
-        args.grad_dtype = "bf16" if multi else "fp32"
+        # stock DDP precision at every N: fp32 gradients, fp32 all-reduce (bf16 is opt-in)
+        args.grad_dtype = "fp32"
     if args.overlap_optimizer is None:
         args.overlap_optimizer = int(multi)
     if args.shard_optimizer is None:
-        # ZeRO-1 pays off where only the bf16 shadow must be all-gathered (MLP weights); the native
-        # VGG reads fp32 masters (per-step weight repack), so it keeps the replicated all-reduce
-        args.shard_optimizer = int(multi and args.model.startswith("mlp"))
+        args.shard_optimizer = 0  # ZeRO-1 is opt-in: the default is the replicated (stock DDP) optimizer
     if args.chunk_mb is None:
-        # row-chunk buckets: off by default.  At the toy MLP's M = 512 rows a quarter-width forward /
-        # wgrad GEMM is launch- and fill-bound (36 vs 34 us for a 1024-column chunk vs the whole
-        # 4096-column layer), and the wide MLP measured 5.52 vs 4.32 ms/step with 64 MB chunks at world
-        # size 1 (profiles/r1_chunk); the multi-GPU benefit is unmeasured here, so it stays opt-in
         args.chunk_mb = 0.0
     if args.fused_optimizer is None:
         args.fused_optimizer = 0 if args.model == "mlp" else 1
@@ -170,25 +207,34 @@ def resolve_defaults(args, world):
         args.comm_side_optimizer = int(bool(args.shard_optimizer))
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
+    if args.stock_ref is None:
+        args.stock_ref = int(world == 1 and args.impl == "ddpx" and args.device == "cuda" and not args.ddp_single
+                             and args.comm == "rccl")
 
 
 def build_ddpx(args, device, world):
+    import torch
     from ddpx.models import build_model
     from ddpx.optim.schedule import one_cycle, resolve_steps_per_epoch
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import HostStagedComm, RcclComm
+    from ddpx.parallel.comm import HostStagedComm, RcclComm, TorchComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
-    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="bf16", device=device,
-                        fp8=bool(args.fp8))
+    cpu = device.type == "cpu"
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="fp32" if cpu else "bf16",
+                        device=device, fp8=bool(args.fp8))
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
-    # single process: the SGD update is fused into the kernels that produce each gradient
-    opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, capturable=not args.no_graph,
-              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer)))
+    # single process: the SGD update may be fused into the kernels that produce each gradient
+    opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4,
+              capturable=not (args.no_graph or cpu),
+              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not cpu))
     net = model
     if world > 1 or args.ddp_single:
-        comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
+        if cpu:
+            comm = TorchComm()
+        else:
+            comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
@@ -204,6 +250,7 @@ def build_ddpx(args, device, world):
 
 def build_torch(args, device, world):
     """Stock PyTorch-ROCm recipe (the baseline to beat)."""
+    import torch
     import torch.nn as nn
     from torch.nn.parallel import DistributedDataParallel as TDDP
     from ddpx.optim.schedule import OneCycleLambda, resolve_steps_per_epoch
@@ -221,26 +268,83 @@ def build_torch(args, device, world):
             if i < args.layers - 1:
                 layers.append(nn.ReLU())
         model = nn.Sequential(nn.Flatten(), *layers).to(device)
-    net = TDDP(model, device_ids=[device.index]) if world > 1 else model
+    net = TDDP(model, device_ids=[device.index] if device.type == "cuda" else None) if world > 1 else model
     opt = torch.optim.SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, OneCycleLambda(resolve_steps_per_epoch("compat", 0, world > 1)))
     return model, net, opt, sched
 
 
-def main():
-    args = parse()
+def torch_runner(args, device, world, loader, idx_all, full):
+    """Eager step loop of the stock recipe (and of the ddpx engine on the CPU)."""
+    import torch
+    bs = args.batch_size
+    amp = device.type == "cuda" and (args.model not in ("vgg", "deepnn") or args.torch_amp)
+    model, net, opt, sched = build_torch(args, device, world)
+
+    def one_step(k):
+        b = full[k % len(full)]
+        x, y = loader.make_batch(idx_all[b * bs:(b + 1) * bs], k)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = net(x)
+        loss = torch.nn.functional.cross_entropy(out.float(), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        return loss
+
+    def run(k, n):
+        loss = None
+        for i in range(n):
+            loss = one_step(k + i)
+        return loss
+
+    return model, net, opt, sched, run
+
+
+def measure_stock_same_run(args, device, loader, idx_all, full):
+    """Stock PyTorch-ROCm recipe (nn.Linear + bf16 autocast + foreach SGD), same data, same process."""
+    import torch
+    a = argparse.Namespace(**vars(args))
+    a.impl, a.torch_amp = "torch", True
+    _, _, _, _, run = torch_runner(a, device, 1, loader, idx_all, full)
+    run(0, 5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(5, args.stock_steps)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.stock_steps
+    return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(args.batch_size / dt, 2),
+            "recipe": "torch.nn + bf16 autocast + foreach SGD", "steps": args.stock_steps}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if needs_self_launch(args):
+        sys.exit(self_launch(args, argv))
+
+    import torch
+    import torch.distributed as dist
+
     rank, world, local = setup_dist(args)
     resolve_defaults(args, world)
-    if args.comm == "host":
+    cpu = args.device == "cpu"
+    if args.comm == "host" or cpu:
         args.no_graph = True
-    device = torch.device("cuda", local)
+    device = torch.device("cpu") if cpu else torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
     idx_all = loader._epoch_indices()
     nb = len(loader)
     full = [i for i in range(nb) if (i + 1) * args.batch_size <= idx_all.numel()]
     bs = args.batch_size
 
-    if args.impl == "ddpx":
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    net = model = None
+    if args.impl == "ddpx" and not cpu:
         from ddpx.runtime.graphs import CapturedStep
         model, net, opt, sched = build_ddpx(args, device, world)
         static_x, static_y = loader.make_batch(idx_all[:bs], 0)
@@ -278,10 +382,11 @@ def main():
                 loss = step_body(x, y)
             return loss
 
+        comm_obj = getattr(net, "comm", None)
+
         def run(k, n):
             """Steps k .. k+n-1: eager for the first two (allocator / lazy-init warm-up), then replays of
-            an S-step graph (one launch per S steps: the replay-to-replay launch gap is paid once per S
-            steps) and of a 1-step graph for the remainder."""
+            an S-step graph and of a 1-step graph for the remainder."""
             loss = None
             while n > 0:
                 if not use_graph or k < 2:
@@ -289,9 +394,11 @@ def main():
                     m = 1
                 else:
                     if not graphs:
-                        graphs[1] = CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True)
+                        graphs[1] = CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True,
+                                                 comm=comm_obj)
                         if S > 1:
-                            graphs[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True)
+                            graphs[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True,
+                                                     comm=comm_obj)
                     m = S if n >= S else 1
                     loss = graphs[m]()
                 for _ in range(m):
@@ -299,16 +406,14 @@ def main():
                 k += m
                 n -= m
             return loss
-    else:
-        model, net, opt, sched = build_torch(args, device, world)
+    elif args.impl == "ddpx":  # CPU: the ddpx engine (flat store, flat SGD, DDP over gloo) on torch CPU kernels
+        model, net, opt, sched = build_ddpx(args, device, world)
 
         def one_step(k):
             b = full[k % len(full)]
             x, y = loader.make_batch(idx_all[b * bs:(b + 1) * bs], k)
-            opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.model not in ("vgg", "deepnn") or args.torch_amp):
-                out = net(x)
-            loss = torch.nn.functional.cross_entropy(out.float(), y)
+            opt.zero_grad()
+            loss, _ = net.forward_loss(x, y)
             loss.backward()
             opt.step()
             sched.step()
@@ -319,62 +424,93 @@ def main():
             for i in range(n):
                 loss = one_step(k + i)
             return loss
+    else:
+        model, net, opt, sched, run = torch_runner(args, device, world, loader, idx_all, full)
 
     # warmup (includes graph capture for ddpx)
     loss = run(0, args.warmup) if args.warmup else None
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     loss = run(args.warmup, args.steps)
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.impl == "ddpx" else device)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if (args.impl == "ddpx" or cpu) else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     multi = world > 1 or args.ddp_single
-    comm = net.comm_stats() if (multi and args.impl == "ddpx" and hasattr(net, "comm_stats")) else None
+    ddpx_ddp = multi and args.impl == "ddpx"
+    comm = net.comm_stats() if (ddpx_ddp and hasattr(net, "comm_stats")) else None
     consistent = None
-    if multi and args.impl == "ddpx":
+    buckets_mb = None
+    if ddpx_ddp:
         # outside the timed region: replicas must hold identical weights after K steps
         net.consolidate()
         ck = [float(net.flat.master.double().sum().item()), float(net.flat.master.double().abs().sum().item())]
         allck = [None] * world
         dist.all_gather_object(allck, ck)
         consistent = all(c == allck[0] for c in allck)
+        esz = net.flat.grad.element_size()
+        buckets_mb = [round((e - s) * esz / 2 ** 20, 3) for s, e in net.bucket_ranges]
+    stock = None
+    if args.stock_ref and rank == 0 and not cpu:
+        stock = measure_stock_same_run(args, device, loader, idx_all, full)
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
-    model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}", "mlp_wide": f"wide-mlp-3072x{args.hidden}x{args.layers}",
+    model_name = {"mlp": f"toy-mlp-3072x{args.hidden}x{args.layers}",
+                  "mlp_wide": f"wide-mlp-3072x{args.hidden}x{args.layers}",
                   "vgg": "vgg11-cifar", "deepnn": "deepnn-cifar"}[args.model]
     base = baseline_value(f"{args.model}_x{world}") if args.impl == "ddpx" else None
+    if cpu:
+        dtype = "fp32"
+    elif args.model.startswith("mlp"):
+        dtype = "mxfp8/bf16" if (args.fp8 and args.impl == "ddpx") else "bf16"
+    else:
+        dtype = "bf16" if (args.impl == "ddpx" or args.torch_amp) else "fp32"
+    if ddpx_ddp:
+        grad_comm = f"{args.grad_dtype} {'reduce-scatter+all-gather (ZeRO-1)' if args.shard_optimizer else 'all-reduce'} avg"
+    elif multi:
+        grad_comm = "fp32 all-reduce avg (torch DDP)"
+    else:
+        grad_comm = None
     rec = {
         "metric": metric, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": (round(value / base, 4) if base else None), "dtype": ("mxfp8/bf16" if args.fp8 else "bf16") if (args.model not in ("vgg", "deepnn") or args.impl == "ddpx" or args.torch_amp) else "fp32",
-        "data": "synthetic (CIFAR-shaped uint8, GPU-resident, crop+flip augment per step; random-init weights)",
+        "vs_baseline": (round(value / base, 4) if base else None), "dtype": dtype,
+        "data": ("synthetic (CIFAR-shaped uint8, " + ("host" if cpu else "GPU") +
+                 "-resident, crop+flip augment per step; random-init weights)"),
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
-                   "parallelism": f"dp{world}", "impl": args.impl, "graph": (args.impl == "ddpx" and not args.no_graph),
+                   "parallelism": f"dp{world}", "device": args.device, "impl": args.impl,
+                   "launcher": os.environ.get(LAUNCHER_ENV, "torchrun/external" if world > 1 else "none"),
+                   "comm": (args.comm if ddpx_ddp else None),
+                   "graph": (args.impl == "ddpx" and not args.no_graph),
                    "graph_steps": (args.graph_steps if args.impl == "ddpx" and not args.no_graph else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
-                       " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer)
-                       else ""), "grad_comm": args.grad_dtype if args.impl == "ddpx" else "fp32",
-                   "bucket_cap_mb": args.bucket_cap_mb, "chunk_mb": args.chunk_mb or None,
-                   "defer_gather": bool(args.defer_gather) if multi else None,
-                   "comm_side_optimizer": bool(args.comm_side_optimizer) if multi else None, "final_loss": round(final_loss, 4),
-                   "ddp": bool(multi), "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
-                   "sharded_optimizer": bool(args.shard_optimizer) if multi and args.impl == "ddpx" else None,
+                       " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer
+                                                  and not cpu) else ""),
+                   "grad_comm": grad_comm, "grad_dtype": args.grad_dtype if args.impl == "ddpx" else "fp32",
+                   "bucket_cap_mb": args.bucket_cap_mb, "first_bucket_mb": args.first_bucket_mb,
+                   "buckets_mb": buckets_mb, "chunk_mb": args.chunk_mb or None,
+                   "sharded_optimizer": bool(args.shard_optimizer) if ddpx_ddp else None,
+                   "defer_gather": bool(args.defer_gather) if (ddpx_ddp and args.shard_optimizer) else None,
+                   "comm_side_optimizer": (bool(args.comm_side_optimizer)
+                                           if (ddpx_ddp and args.shard_optimizer) else None),
+                   "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
+                   "final_loss": round(final_loss, 4), "ddp": bool(multi),
                    "replicas_consistent": consistent,
-                   "vs_stock_pytorch_1gpu": (round(value / (STOCK_MEASURED_1GPU[args.model] * world), 4)
-                                             if args.impl == "ddpx" and args.model in STOCK_MEASURED_1GPU else None),
                    "comm_ms_per_step": round(comm["comm_ms"], 4) if comm else None,
-                   "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None},
+                   "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None,
+                   "stock_same_run": stock,
+                   "vs_stock_same_run": (round(value / stock["samples_per_sec"], 4) if stock else None)},
     }
     if rank == 0:
         line = json.dumps(rec)

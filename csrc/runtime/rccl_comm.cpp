@@ -40,12 +40,25 @@ struct Pending {
   const char* what;
 };
 
+// What the watchdog does when a tracked operation exceeds the timeout or RCCL reports an asynchronous
+// error (DDPX_COMM_TIMEOUT_ACTION; ProcessGroupNCCL's TORCH_NCCL_ASYNC_ERROR_HANDLING analogue):
+//   raise  - set the error flag only; the owning thread's next comm.check() / collective call fails
+//   abort  - also ncclCommAbort (serialised against collective issue, see Comm::issue_mu)
+//   exit   - raise, then terminate the process with exit code 3 after a grace period
+//            (DDPX_COMM_EXIT_GRACE_S, default 10 s) unless the owning thread exited first (default)
+enum TimeoutAction : int { ACT_RAISE = 0, ACT_ABORT = 1, ACT_EXIT = 2 };
+
 struct Comm {
+  // The RCCL handle is written only under issue_mu (creation, abort, destroy).  Every collective
+  // issue holds issue_mu for the duration of the enqueue and checks `aborted` first, so an abort can
+  // never free the communicator underneath an ncclAllReduce call on the owning thread.
   ncclComm_t nccl = nullptr;
+  std::mutex issue_mu;
+  std::atomic<bool> aborted{false};
   int rank = 0, nranks = 1, device = 0;
   hipStream_t stream = nullptr;  // dedicated comm stream (high priority)
   // watchdog
-  std::mutex mu;
+  std::mutex mu;  // guards pending / free_events
   std::deque<Pending> pending;
   std::vector<hipEvent_t> free_events;
   std::thread watchdog;
@@ -53,46 +66,92 @@ struct Comm {
   std::atomic<int> error{0};  // 0 ok, 1 async nccl error, 2 timeout, 3 aborted
   double timeout_s = 0.0;
   bool track = false;
+  int action = ACT_EXIT;
+  double exit_grace_s = 10.0;
+  std::atomic<long long> tracked{0};  // operations / graph replays registered with the watchdog
 };
 
 int check(ncclResult_t r) { return r == ncclSuccess ? 0 : 1000 + (int)r; }
 
-void watchdog_loop(Comm* c) {
-  while (!c->stop.load()) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(50));
-    if (c->error.load()) continue;
-    ncclResult_t ae = ncclSuccess;
-    if (c->nccl && ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
-        ae != ncclInProgress) {
-      fprintf(stderr, "[ddpx rank %d] RCCL async error %d (%s); aborting communicator\n", c->rank, (int)ae,
-              ncclGetErrorString(ae));
-      c->error.store(1);
-      ncclCommAbort(c->nccl);
-      c->nccl = nullptr;
-      continue;
-    }
-    std::lock_guard<std::mutex> g(c->mu);
-    while (!c->pending.empty()) {
-      Pending& p = c->pending.front();
-      hipError_t q = hipEventQuery(p.ev);
-      if (q == hipSuccess) {
-        c->free_events.push_back(p.ev);
-        c->pending.pop_front();
-        continue;
-      }
-      const double age = std::chrono::duration<double>(Clock::now() - p.t0).count();
-      if (c->timeout_s > 0 && age > c->timeout_s) {
-        fprintf(stderr, "[ddpx rank %d] collective '%s' exceeded timeout %.1fs; aborting communicator\n",
-                c->rank, p.what, c->timeout_s);
-        c->error.store(2);
-        if (c->nccl) ncclCommAbort(c->nccl);
-        c->nccl = nullptr;
-      }
-      break;
+// Abort the communicator from the watchdog thread.  Waits (bounded) for an in-flight issue call to
+// return; a call stuck inside RCCL (e.g. a connection handshake with a dead peer) is exactly what
+// ncclCommAbort exists to unblock, so after the bound the abort proceeds without the lock.  The handle
+// itself is never cleared without the lock: issuers test `aborted` under issue_mu instead.
+void abort_comm(Comm* c) {
+  bool locked = false;
+  for (int i = 0; i < 200 && !locked; ++i) {  // ~2 s
+    locked = c->issue_mu.try_lock();
+    if (!locked) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  if (!c->aborted.exchange(true) && c->nccl) ncclCommAbort(c->nccl);
+  if (locked) c->issue_mu.unlock();
+}
+
+void on_failure(Comm* c, int code, const char* what) {
+  c->error.store(code);
+  if (c->action == ACT_ABORT) {
+    abort_comm(c);
+  } else if (c->action == ACT_EXIT) {
+    fprintf(stderr, "[ddpx rank %d] %s: process exits in %.1fs unless it terminates first\n", c->rank, what,
+            c->exit_grace_s);
+    fflush(stderr);
+    const auto t_end = Clock::now() + std::chrono::duration<double>(c->exit_grace_s);
+    while (!c->stop.load() && Clock::now() < t_end) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    if (!c->stop.load()) {
+      fprintf(stderr, "[ddpx rank %d] %s: terminating (exit code 3)\n", c->rank, what);
+      fflush(stderr);
+      std::_Exit(3);
     }
   }
 }
 
+void watchdog_loop(Comm* c) {
+  while (!c->stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (c->error.load() || c->aborted.load()) continue;
+    ncclResult_t ae = ncclSuccess;
+    // ncclCommGetAsyncError is documented as callable concurrently with operations on the comm;
+    // the handle is stable until abort/destroy, which only this thread (abort) or the owner after
+    // joining this thread (destroy) perform.
+    if (c->nccl && ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress) {
+      fprintf(stderr, "[ddpx rank %d] RCCL async error %d (%s)\n", c->rank, (int)ae, ncclGetErrorString(ae));
+      fflush(stderr);
+      on_failure(c, 1, "RCCL async error");
+      continue;
+    }
+    const char* late = nullptr;
+    double late_age = 0.0;
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      while (!c->pending.empty()) {
+        Pending& p = c->pending.front();
+        hipError_t q = hipEventQuery(p.ev);
+        if (q == hipSuccess) {
+          c->free_events.push_back(p.ev);
+          c->pending.pop_front();
+          continue;
+        }
+        const double age = std::chrono::duration<double>(Clock::now() - p.t0).count();
+        if (c->timeout_s > 0 && age > c->timeout_s) {
+          late = p.what;
+          late_age = age;
+        }
+        break;
+      }
+    }
+    if (late) {
+      fprintf(stderr, "[ddpx rank %d] collective '%s' timed out: not complete after %.1fs (timeout %.1fs)\n",
+              c->rank, late, late_age, c->timeout_s);
+      fflush(stderr);
+      on_failure(c, 2, "collective timed out");
+    }
+  }
+}
+
+// Register "everything enqueued on s so far" with the watchdog: an event recorded now must complete
+// within the timeout.  Collectives issued eagerly are tracked one by one; collectives inside a HIP graph
+// are tracked per replay (ddpx_comm_track after hipGraphLaunch), since at capture time nothing runs.
 void track_op(Comm* c, hipStream_t s, const char* what) {
   if (!c->track) return;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -105,9 +164,21 @@ void track_op(Comm* c, hipStream_t s, const char* what) {
   } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
     return;
   }
-  hipEventRecord(ev, s);
+  if (hipEventRecord(ev, s) != hipSuccess) {
+    c->free_events.push_back(ev);
+    return;
+  }
   c->pending.push_back({ev, Clock::now(), what});
+  c->tracked.fetch_add(1);
 }
+
+// Issue guard: holds issue_mu while a collective is enqueued; fails if the communicator is gone.
+struct IssueGuard {
+  Comm* c;
+  std::lock_guard<std::mutex> g;
+  explicit IssueGuard(Comm* c_) : c(c_), g(c_->issue_mu) {}
+  bool ok() const { return c->nccl && !c->aborted.load() && c->error.load() == 0; }
+};
 
 // ---------------------------------------------------------------------------
 // Reducer: gradient buckets -> all-reduce on the comm stream.
@@ -192,8 +263,31 @@ DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int devic
   }
   c->timeout_s = timeout_s;
   c->track = timeout_s > 0;
+  if (const char* a = getenv("DDPX_COMM_TIMEOUT_ACTION")) {
+    if (!strcmp(a, "raise")) c->action = ACT_RAISE;
+    else if (!strcmp(a, "abort")) c->action = ACT_ABORT;
+    else c->action = ACT_EXIT;
+  }
+  if (const char* g = getenv("DDPX_COMM_EXIT_GRACE_S")) c->exit_grace_s = atof(g);
   c->watchdog = std::thread(watchdog_loop, c);
   return c;
+}
+
+// Track a graph replay (or any stream position): call right after hipGraphLaunch on `s`.
+DDPX_API int ddpx_comm_track(void* h, hipStream_t s, const char* what) {
+  Comm* c = static_cast<Comm*>(h);
+  if (c->error.load()) return 3;
+  track_op(c, s, what ? what : "graph replay");
+  return 0;
+}
+
+DDPX_API long long ddpx_comm_tracked(void* h) { return static_cast<Comm*>(h)->tracked.load(); }
+DDPX_API int ddpx_comm_set_timeout(void* h, double timeout_s, int action) {
+  Comm* c = static_cast<Comm*>(h);
+  c->timeout_s = timeout_s;
+  c->track = timeout_s > 0;
+  if (action >= 0) c->action = action;
+  return 0;
 }
 
 DDPX_API void* ddpx_comm_stream(void* h) { return static_cast<Comm*>(h)->stream; }
@@ -204,13 +298,15 @@ DDPX_API int ddpx_comm_destroy(void* h, int abort) {
   c->stop.store(true);
   if (c->watchdog.joinable()) c->watchdog.join();
   int e = 0;
-  if (c->nccl) {
-    if (abort) e = check(ncclCommAbort(c->nccl));
+  std::lock_guard<std::mutex> g(c->issue_mu);
+  if (c->nccl && !c->aborted.load()) {
+    if (abort || c->error.load()) e = check(ncclCommAbort(c->nccl));
     else {
       hipStreamSynchronize(c->stream);
       e = check(ncclCommDestroy(c->nccl));
     }
   }
+  c->nccl = nullptr;
   for (auto& p : c->pending) hipEventDestroy(p.ev);
   for (auto ev : c->free_events) hipEventDestroy(ev);
   hipStreamDestroy(c->stream);
@@ -244,7 +340,8 @@ static bool skip_identity(const Comm* c, const void* send, const void* recv) {
 DDPX_API int ddpx_comm_allreduce(void* h, const void* send, void* recv, size_t count, int dtype, int op,
                                  hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
-  if (!c->nccl) return 3;
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
   if (skip_identity(c, send, recv)) return 0;
   s = pick_stream(c, s);
   int e = check(ncclAllReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, c->nccl, s));
@@ -255,7 +352,8 @@ DDPX_API int ddpx_comm_allreduce(void* h, const void* send, void* recv, size_t c
 DDPX_API int ddpx_comm_broadcast(void* h, const void* send, void* recv, size_t count, int dtype, int root,
                                  hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
-  if (!c->nccl) return 3;
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
   if (skip_identity(c, send, recv)) return 0;
   s = pick_stream(c, s);
   int e = check(ncclBroadcast(send, recv, count, (ncclDataType_t)dtype, root, c->nccl, s));
@@ -266,7 +364,8 @@ DDPX_API int ddpx_comm_broadcast(void* h, const void* send, void* recv, size_t c
 DDPX_API int ddpx_comm_reduce_scatter(void* h, const void* send, void* recv, size_t recvcount, int dtype, int op,
                                       hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
-  if (!c->nccl) return 3;
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
   if (skip_identity(c, send, recv)) return 0;
   s = pick_stream(c, s);
   int e = check(ncclReduceScatter(send, recv, recvcount, (ncclDataType_t)dtype, (ncclRedOp_t)op, c->nccl, s));
@@ -277,7 +376,8 @@ DDPX_API int ddpx_comm_reduce_scatter(void* h, const void* send, void* recv, siz
 DDPX_API int ddpx_comm_allgather(void* h, const void* send, void* recv, size_t sendcount, int dtype,
                                  hipStream_t s) {
   Comm* c = static_cast<Comm*>(h);
-  if (!c->nccl) return 3;
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
   if (skip_identity(c, send, recv)) return 0;
   s = pick_stream(c, s);
   int e = check(ncclAllGather(send, recv, sendcount, (ncclDataType_t)dtype, c->nccl, s));
@@ -529,3 +629,26 @@ DDPX_API int ddpx_reducer_destroy(void* h) {
   delete r;
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Host-mapped int32 flag (fault injection / watchdog tests): pinned host memory the device can read
+// through PCIe; the host flips it with a plain store.
+DDPX_API int ddpx_hostflag_create(void** host, void** dev) {
+  int* p = nullptr;
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  *p = 0;
+  e = hipHostGetDevicePointer(dev, p, 0);
+  if (e != hipSuccess) {
+    hipHostFree(p);
+    return (int)e;
+  }
+  *host = p;
+  return 0;
+}
+
+DDPX_API void ddpx_hostflag_set(void* host, int v) {
+  __atomic_store_n(static_cast<int*>(host), v, __ATOMIC_SEQ_CST);
+}
+
+DDPX_API int ddpx_hostflag_destroy(void* host) { return (int)hipHostFree(host); }

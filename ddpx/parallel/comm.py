@@ -37,6 +37,10 @@ NCCL_OP = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 _uid_counter = itertools.count()
 
 
+class CommError(RuntimeError):
+    """A collective failed or timed out (watchdog), reported on the owning thread."""
+
+
 class Comm:
     rank: int = 0
     world_size: int = 1
@@ -67,6 +71,9 @@ class Comm:
         return out
 
     def check(self):
+        pass
+
+    def track(self, stream=None, what: str = "graph replay"):
         pass
 
     def close(self, abort=False):
@@ -249,11 +256,27 @@ class RcclComm(Comm):
                                           self._s(stream))
         native.check(rc, "ncclAllGather")
 
+    TIMEOUT_ACTIONS = {"raise": 0, "abort": 1, "exit": 2}
+
     def check(self):
         e = self._rt.ddpx_comm_error(self.handle)
         if e:
-            raise RuntimeError({1: "RCCL asynchronous error", 2: "RCCL collective timed out",
-                                3: "RCCL communicator aborted"}.get(e, f"RCCL error {e}"))
+            raise CommError(f"[rank {self.rank}] " + {1: "RCCL asynchronous error", 2: "RCCL collective timed out",
+                                                      3: "RCCL communicator aborted"}.get(e, f"RCCL error {e}"))
+
+    def track(self, stream=None, what: str = "graph replay"):
+        """Register everything enqueued on ``stream`` so far with the watchdog (call after each graph
+        replay: collectives captured in a graph are invisible to per-collective tracking)."""
+        rc = self._rt.ddpx_comm_track(self.handle, self._s(stream), what.encode())
+        if rc:
+            self.check()
+
+    def tracked(self) -> int:
+        return int(self._rt.ddpx_comm_tracked(self.handle))
+
+    def set_timeout(self, timeout_s: float, action: str | None = None):
+        self._rt.ddpx_comm_set_timeout(self.handle, float(timeout_s),
+                                       -1 if action is None else self.TIMEOUT_ACTIONS[action])
 
     def close(self, abort=False):
         if getattr(self, "handle", None):

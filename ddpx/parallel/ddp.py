@@ -270,8 +270,13 @@ class DistributedDataParallel(nn.Module):
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
                  reduce_single: bool = False, shard_optimizer: bool = False, chunk_mb: float | None = None,
-                 defer_gather: bool = False, comm_side_optimizer: bool = False):
+                 defer_gather: bool = False, comm_side_optimizer: bool = False,
+                 find_unused_parameters: bool = False):
         super().__init__()
+        # torch DDP semantics: False (default) -> a parameter without gradient on some rank is an error at
+        # world size > 1 (its bucket would otherwise be issued in a different order on different ranks);
+        # True -> buckets are issued at the end of backward in bucket order, unused gradients as zeros
+        self.find_unused_parameters = bool(find_unused_parameters)
         self.comm_side_optimizer = comm_side_optimizer
         self.module = module
         dev = next(module.parameters()).device
@@ -590,7 +595,8 @@ class DistributedDataParallel(nn.Module):
             bs = [self.bucket_of[i]]
         for b in bs:
             self._marks[b] += 1
-            self.reducer.mark_ready(b, 1)
+            if not self.find_unused_parameters:
+                self.reducer.mark_ready(b, 1)
             if self._marks[b] == self.bucket_expected[b]:
                 self._completion_order.append(b)
 
@@ -600,9 +606,29 @@ class DistributedDataParallel(nn.Module):
     def _marks_complete(self, b):
         return self._marks[b] == self.bucket_expected[b]
 
+    def _unused_names(self):
+        f = self.flat
+        return [f.names.get(id(f.params[i]), str(i)) for i, w in enumerate(f.written) if not w and not f.updated[i]]
+
     def _finalize(self):
         if self.reducer is None:
             return
+        if self.find_unused_parameters:
+            # every bucket is issued here, in bucket order (identical on every rank); gradients of
+            # parameters this rank did not use are zeros
+            self.flat.fix_unwritten(mark_written=True)
+            for b in range(len(self.bucket_ranges)):
+                self.reducer.mark_ready(b, self.bucket_expected[b])
+            self._completion_order = list(range(len(self.bucket_ranges)))
+        elif len(self._completion_order) < len(self.bucket_ranges):
+            unused = self._unused_names()
+            if self.world_size > 1:
+                raise RuntimeError(
+                    f"DDP (rank {self.rank}): parameters {unused} received no gradient in this backward; their "
+                    "buckets cannot be reduced in the same order on every rank.  Pass find_unused_parameters=True "
+                    "(torch DDP's flag) if the model skips parameters.")
+            # world size 1 (reduce_single): no ordering hazard; stale gradients must not be reduced
+            self.flat.fix_unwritten(mark_written=True)
         if self.debug and self.world_size > 1:
             # TORCH_DISTRIBUTED_DEBUG=DETAIL-style check: identical bucket completion order on every rank
             order = list(self._completion_order)

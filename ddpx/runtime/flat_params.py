@@ -270,8 +270,11 @@ class FlatParams:
         for p in self.params:
             p.grad = None
 
-    def fix_unwritten(self):
-        """Zero gradients nobody produced this iteration (stale values would otherwise be applied)."""
+    def fix_unwritten(self, mark_written: bool = False):
+        """Zero gradients nobody produced this iteration (stale values would otherwise be applied).
+
+        ``mark_written``: the zeros are this iteration's gradient (DDP reduces them next), so later
+        callers (``SGD.step``) must not zero the reduced result again."""
         missing = [i for i, w in enumerate(self.written) if not w and not self.updated[i]]
         if missing:
             if not self._warned_unused:
@@ -280,6 +283,8 @@ class FlatParams:
                 self._warned_unused = True
             for i in missing:
                 self.grad[self.slice(i)].zero_()
+                if mark_written:
+                    self.written[i] = True
         return missing
 
     def remove_hooks(self):

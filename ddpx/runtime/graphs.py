@@ -22,12 +22,16 @@ class CapturedStep:
     """Capture ``fn(x, y) -> loss`` into a graph; ``__call__`` replays it."""
 
     def __init__(self, fn, example_x: torch.Tensor, example_y: torch.Tensor, warmup: int = 0, pre_replay=None,
-                 use_inputs_as_static: bool = False):
+                 use_inputs_as_static: bool = False, comm=None):
         """``warmup`` extra eager calls run on a side stream first (they execute ``fn`` for real:
         in training they are real optimizer steps, so callers normally warm up with their own
         eager steps and pass 0).  Capture itself records without executing: call the object
         to run the captured step for the example batch."""
         self.fn = fn
+        # communicator whose collectives the graph contains: its watchdog tracks every replay (a
+        # collective captured in the graph is not seen by per-collective tracking) and its error state
+        # is checked before each replay, so a timed-out step fails on the owning thread
+        self.comm = comm
         # use_inputs_as_static: the caller writes every batch straight into these buffers
         self.static_x = example_x if use_inputs_as_static else example_x.clone()
         self.static_y = example_y if use_inputs_as_static else example_y.clone()
@@ -60,5 +64,9 @@ class CapturedStep:
             self.load(x, y)
         if self.pre_replay is not None:
             self.pre_replay()
+        if self.comm is not None:
+            self.comm.check()
         self.graph.replay()
+        if self.comm is not None:
+            self.comm.track(what="graph replay")
         return self.static_loss

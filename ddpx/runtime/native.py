@@ -84,6 +84,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_dropout_fwd", I, P, P, I64, F, P, P, P)
     _sig(lib, "ddpx_avgpool", I, P, I, I, I, P, P)
     _sig(lib, "ddpx_avgpool_bwd", I, P, I, I, I, P, P)
+    _sig(lib, "ddpx_debug_spin_wait", I, P, I, c_double, P, P)
     for extra in _EXTRA_KERNEL_SIGS:
         if hasattr(lib, extra[0]):
             _sig(lib, *extra)
@@ -111,6 +112,12 @@ def _declare_rt(lib):
     _sig(lib, "ddpx_comm_broadcast", I, P, P, P, S, I, I, P)
     _sig(lib, "ddpx_comm_reduce_scatter", I, P, P, P, S, I, I, P)
     _sig(lib, "ddpx_comm_allgather", I, P, P, P, S, I, P)
+    _sig(lib, "ddpx_comm_track", I, P, P, c_char_p)
+    _sig(lib, "ddpx_comm_tracked", c_int64, P)
+    _sig(lib, "ddpx_comm_set_timeout", I, P, D, I)
+    _sig(lib, "ddpx_hostflag_create", I, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p))
+    _sig(lib, "ddpx_hostflag_set", None, P, I)
+    _sig(lib, "ddpx_hostflag_destroy", I, P)
     _sig(lib, "ddpx_comm_group_start", I)
     _sig(lib, "ddpx_comm_group_end", I)
     _sig(lib, "ddpx_reducer_create", P, P, I, I)

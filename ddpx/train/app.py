@@ -153,13 +153,42 @@ def input_layout(model, device, dtype):
     return "nchw_f32"
 
 
-def load_train_objs(args, device, distributed: bool, world_size: int, loader_len_hint: int, comm=None):
+_CONFIG = None  # module-level run configuration the reference-signature helpers default to
+
+
+def set_config(args) -> None:
+    """Make ``args`` the configuration ``load_train_objs()`` / ``prepare_dataloader(ds, bs)`` use."""
+    global _CONFIG
+    _CONFIG = args
+
+
+def current_config():
+    """The active configuration: the one ``run()`` / ``set_config`` installed, else the reference's defaults
+    (``TOTAL_EPOCHS=20 SAVE_EVERY=5``, VGG, lr 0.4, batch 512)."""
+    global _CONFIG
+    if _CONFIG is None:
+        _CONFIG = build_parser("ddpx").parse_args(["20", "5"])
+    return _CONFIG
+
+
+def load_train_objs(args=None, device=None, distributed: bool = False, world_size: int = 1,
+                    loader_len_hint: int | None = None, comm=None):
     """(train_set, model, optimizer, test_set, scheduler) — the reference's factory, ddpx engine underneath.
+
+    Callable exactly as the reference does, ``load_train_objs()`` (``/root/reference/singlegpu.py:132``):
+    every argument defaults from :func:`current_config` (device: the first GPU, else the CPU).
 
     ``--sync_bn`` (reference: the commented-out ``convert_sync_batchnorm`` at
     ``/root/reference/multigpu.py:127``) swaps every BatchNorm2d for :class:`SyncBatchNorm2d` on ``comm``
     before the flat parameter store is built; the VGG then runs on the torch-op path.
     """
+    if args is None:
+        args = current_config()
+    if device is None:
+        device = resolve_device(args)
+    if loader_len_hint is None:
+        train_n = args.train_size if resolve_data(args) == "synthetic" else 50000
+        loader_len_hint = _loader_len(train_n, args.batch_size, world_size)
     kind = resolve_data(args)
     train_set, test_set = get_datasets(kind, args.data_root, seed=0, train_size=args.train_size,
                                        test_size=args.test_size)
@@ -180,7 +209,13 @@ def load_train_objs(args, device, distributed: bool, world_size: int, loader_len
     return train_set, model, optimizer, test_set, scheduler
 
 
-def prepare_dataloader(dataset, batch_size, device, layout, rank=0, world_size=1, seed=0):
+def prepare_dataloader(dataset, batch_size: int, device=None, layout: str = "nchw_f32", rank: int = 0,
+                       world_size: int = 1, seed: int = 0):
+    """Shuffled training batches (``/root/reference/singlegpu.py:174``: ``DataLoader(dataset, batch_size,
+    pin_memory=True, shuffle=True)``) produced on ``device`` by the GPU-resident loader.  Callable as
+    ``prepare_dataloader(dataset, batch_size)``: NCHW fp32 batches on the configured device."""
+    if device is None:
+        device = resolve_device(current_config())
     sampler = DistributedIndexSampler(len(dataset), world_size, rank, shuffle=True, seed=seed)
     return DeviceLoader(dataset, batch_size, device, sampler=sampler, train=True, layout=layout, seed=seed + rank)
 
@@ -191,6 +226,7 @@ def _loader_len(n, batch_size, world_size):
 
 
 def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distributed: bool = False):
+    set_config(args)
     device = resolve_device(args, local_rank)
     if device.type == "cuda":
         torch.cuda.set_device(device)

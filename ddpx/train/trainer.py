@@ -91,7 +91,7 @@ class Trainer:
         if self.use_graph and self._graph_batch == bs:
             if self._graph is None:
                 self.optimizer.sync_lr()
-                self._graph = CapturedStep(self._step_body, source, targets)
+                self._graph = CapturedStep(self._step_body, source, targets, comm=getattr(self.model, "comm", None))
             else:
                 self._graph.load(source, targets)
             self.optimizer.sync_lr()

@@ -1,14 +1,18 @@
 """bench.py flag resolution (CPU): the defaults the driver's 1/2/4/8-GPU runs get.
 
-N = 1 toy MLP: fp32 gradients + flat SGD pass (profiles/r1_n1alt); N > 1: bf16 gradient buckets,
-ZeRO-1 with comm-stream shard updates and deferred gathers; other models keep their own defaults.
+N = 1 toy MLP: fp32 gradients + flat SGD pass (profiles/r1_n1alt); N > 1: the stock DDP algorithm
+(fp32 gradients, fp32 all-reduce, replicated optimizer overlapped per bucket); bf16 gradient comm and
+ZeRO-1 are opt-in.  Also: the self-launch and CPU modes end to end (BASELINE config 1).
 """
+import json
+import subprocess
 import os
 import sys
 
 import pytest
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def _args(argv):
@@ -38,9 +42,15 @@ def test_single_gpu_toy_mlp_defaults():
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_multi_gpu_toy_mlp_defaults(world):
     a = _resolved(["--gpus", str(world)], world)
-    assert a.grad_dtype == "bf16"
-    assert a.shard_optimizer == 1 and a.overlap_optimizer == 1
-    assert a.comm_side_optimizer == 1 and a.defer_gather == 1 and a.chunk_mb == 0.0
+    assert a.grad_dtype == "fp32"
+    assert a.shard_optimizer == 0 and a.overlap_optimizer == 1
+    assert a.comm_side_optimizer == 0 and a.defer_gather == 0 and a.chunk_mb == 0.0
+    assert a.stock_ref == 0 and a.fp8 == 0
+
+
+def test_zero1_opt_in():
+    a = _resolved(["--gpus", "8", "--shard_optimizer", "1"], 8)
+    assert a.shard_optimizer == 1 and a.comm_side_optimizer == 1 and a.defer_gather == 1
 
 
 def test_other_models_keep_fused_optimizer():
@@ -58,3 +68,46 @@ def test_explicit_flags_win():
     assert _resolved(["--model", "vgg", "--no_fused_optimizer"], 1).fused_optimizer == 0
     b = _resolved(["--gpus", "8", "--comm_side_optimizer", "0", "--shard_optimizer", "0"], 8)
     assert b.comm_side_optimizer == 0 and b.shard_optimizer == 0 and b.defer_gather == 0
+
+
+def test_self_launch_command_needs_no_launcher():
+    import bench
+    a = _args(["--gpus", "4", "--steps", "5"])
+    assert bench.needs_self_launch(a, env={})
+    assert not bench.needs_self_launch(a, env={"WORLD_SIZE": "4", "RANK": "0"})
+    assert not bench.needs_self_launch(_args([]), env={})
+    cmd = bench.self_launch_cmd(a, ["--gpus", "4", "--steps", "5"], 12345)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "5"]
+
+
+def _bench(argv, timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], cwd=ROOT, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--batch_size", "64", "--hidden", "256", "--train_size", "1024"]
+
+
+def test_bench_cpu_single_process():
+    rec = _bench(["--device", "cpu", *SMALL])
+    assert rec["n_gpus"] == 1 and rec["dtype"] == "fp32" and rec["value"] > 0
+    assert rec["config"]["device"] == "cpu" and rec["config"]["ddp"] is False
+
+
+def test_bench_cpu_two_ranks_self_launched():
+    """``bench.py --gpus 2 --device cpu`` with no launcher: N ranks are started by bench.py itself."""
+    rec = _bench(["--gpus", "2", "--device", "cpu", *SMALL])
+    c = rec["config"]
+    assert rec["n_gpus"] == 2 and c["global_batch"] == 128 and c["parallelism"] == "dp2"
+    assert c["launcher"] == "self:torch.distributed.run"
+    assert c["grad_dtype"] == "fp32" and c["grad_comm"].startswith("fp32 all-reduce")
+    assert c["replicas_consistent"] is True and c["sharded_optimizer"] is False
+    assert c["buckets_mb"] and rec["value"] > 0
