@@ -37,7 +37,7 @@ using Clock = std::chrono::steady_clock;
 struct Pending {
   hipEvent_t ev;
   Clock::time_point t0;
-  const char* what;
+  char what[64];  // copied: callers (ctypes) pass temporaries
 };
 
 // What the watchdog does when a tracked operation exceeds the timeout or RCCL reports an asynchronous
@@ -120,7 +120,7 @@ void watchdog_loop(Comm* c) {
       on_failure(c, 1, "RCCL async error");
       continue;
     }
-    const char* late = nullptr;
+    char late[64] = {0};
     double late_age = 0.0;
     {
       std::lock_guard<std::mutex> g(c->mu);
@@ -134,13 +134,13 @@ void watchdog_loop(Comm* c) {
         }
         const double age = std::chrono::duration<double>(Clock::now() - p.t0).count();
         if (c->timeout_s > 0 && age > c->timeout_s) {
-          late = p.what;
+          memcpy(late, p.what, sizeof(late));
           late_age = age;
         }
         break;
       }
     }
-    if (late) {
+    if (late[0]) {
       fprintf(stderr, "[ddpx rank %d] collective '%s' timed out: not complete after %.1fs (timeout %.1fs)\n",
               c->rank, late, late_age, c->timeout_s);
       fflush(stderr);
@@ -168,7 +168,9 @@ void track_op(Comm* c, hipStream_t s, const char* what) {
     c->free_events.push_back(ev);
     return;
   }
-  c->pending.push_back({ev, Clock::now(), what});
+  Pending p{ev, Clock::now(), {0}};
+  snprintf(p.what, sizeof(p.what), "%s", what ? what : "?");
+  c->pending.push_back(p);
   c->tracked.fetch_add(1);
 }
 

@@ -56,13 +56,17 @@ def test_multigpu_single_rank_rccl_sharded(gpu, tmp_path):
     assert any("loss_mean_ranks" in r for r in recs)  # all-reduced over the (single-rank) group
 
 
-def test_bench_ddp_single_comm_stats(gpu, tmp_path):
-    """bench.py --ddp_single: the RCCL reducer at world size 1 reports per-step comm / exposed time."""
-    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3", "--ddp_single"],
+@pytest.mark.parametrize("shard", [0, 1])
+def test_bench_ddp_single_comm_stats(gpu, tmp_path, shard):
+    """bench.py --ddp_single: the RCCL reducer at world size 1 reports per-step comm / exposed time
+    (replicated optimizer by default, ZeRO-1 when asked)."""
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3", "--ddp_single",
+                "--shard_optimizer", str(shard)],
                tmp_path, extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()),
                                     "DDPX_COMM_SKIP_IDENTITY": "0"})  # real RCCL calls at world size 1
     rec = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][0])
-    assert rec["config"]["ddp"] and rec["config"]["sharded_optimizer"] and rec["config"]["replicas_consistent"]
+    assert rec["config"]["ddp"] and rec["config"]["replicas_consistent"]
+    assert rec["config"]["sharded_optimizer"] is bool(shard)
     assert rec["config"]["comm_ms_per_step"] > 0
 
 

@@ -154,7 +154,7 @@ def test_watchdog_terminates_process_on_timeout(gpu):
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), PYTHONPATH=ROOT)
     t0 = time.time()
     r = subprocess.run([sys.executable, "-c", _EXIT_SCRIPT.format(root=ROOT)], env=env, stdout=subprocess.PIPE,
-                       stderr=subprocess.PIPE, text=True, timeout=90)
+                       stderr=subprocess.PIPE, text=True, errors="replace", timeout=90)
     dt = time.time() - t0
     assert r.returncode == 3, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "replayed" in r.stdout and "still alive" not in r.stdout
