@@ -49,11 +49,8 @@ def main():
         kind, tile = c.split("_t")
         tile = int(tile)
         if kind == "fwd1":
-            if tile == 8:
-                G.SPLITK = True
-                fn = lambda: G.linear_fwd(x, w, b, relu=True)  # noqa: E731
-            else:
-                fn = lambda: G.linear_fwd(x, w, b, relu=True, tile=tile)  # noqa: E731
+            # tile -1: the default plan (in-launch split-K on 128x128 tiles for this shape)
+            fn = lambda: G.linear_fwd(x, w, b, relu=True, tile=tile)  # noqa: E731
         elif kind == "dgrad1":
             fn = lambda: G.linear_dgrad(dy, w, relu_mask_of=x, tile=tile)  # noqa: E731
         elif kind == "wgrad1":

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Forward / dgrad GEMMs of the toy MLP at batch 512: split-K 8-wave path vs single-pass tiles (µs)."""
+"""Forward / dgrad GEMMs of the toy MLP at batch 512: default plan (in-launch split-K) vs fixed tiles (µs)."""
 import argparse
 import json
 import os
@@ -25,11 +25,8 @@ def main():
         b = torch.randn(N, device=dev)
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
         row = {}
-        for sk in (True, False):
-            G.SPLITK = sk
-            row[f"fwd_auto_split{int(sk)}"] = timeit(lambda: G.linear_fwd(x, w, b, relu=True))
-            row[f"dgrad_auto_split{int(sk)}"] = timeit(lambda: G.linear_dgrad(dy, w, relu_mask_of=x))
-        G.SPLITK = True
+        row["fwd_auto"] = timeit(lambda: G.linear_fwd(x, w, b, relu=True))
+        row["dgrad_auto"] = timeit(lambda: G.linear_dgrad(dy, w, relu_mask_of=x))
         for t in range(14):
             row[f"fwd_t{t}"] = timeit(lambda: G.linear_fwd(x, w, b, relu=True, tile=t))
             row[f"dgrad_t{t}"] = timeit(lambda: G.linear_dgrad(dy, w, relu_mask_of=x, tile=t))

@@ -101,6 +101,12 @@ struct Params {
   int klen;        // split-K: K elements per split (0: no split)
   long long split_stride;  // elements between the output slabs of consecutive splits
   int sgd_plain;           // fused-SGD epilogue: 1 = ordinary (cached) loads/stores instead of non-temporal
+  // In-launch split-K (gridDim.y = splits, klen set): each split's fp32 accumulators go write-through
+  // (sc1) into slab[split][tile] in register layout, then the tile's ticket; the last split to arrive adds
+  // every slab in split order and runs the epilogue (one launch, no partial-sum kernel).
+  float* slab;
+  unsigned slab_bytes;
+  int* tcnt;               // per-tile tickets, zero between launches (the last arriver resets its own)
 };
 
 constexpr unsigned kOOB = 0x80000000u;
@@ -370,7 +376,7 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 // SGDPF (fused-SGD wgrad only): the tile's fp32 master / momentum rows are LDS-DMA'd into a side
 // buffer during the main loop, so the optimizer epilogue only streams writes.
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
-          bool SGDPF = false>
+          bool SGDPF = false, bool SK = false>
 __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
@@ -415,7 +421,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   const int kbeg = p.klen ? split * p.klen : 0;
   const int kend = p.klen ? min(p.K, kbeg + p.klen) : p.K;
   void* Cbase = p.C;
-  if (p.klen) Cbase = reinterpret_cast<char*>(p.C) + (size_t)split * p.split_stride * (p.epi == EPI_F32 ? 4 : 2);
+  if (p.klen && !SK) Cbase = reinterpret_cast<char*>(p.C) + (size_t)split * p.split_stride * (p.epi == EPI_F32 ? 4 : 2);
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, p.b_bytes, 0x00020000);
@@ -492,6 +498,47 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+  }
+
+  // ---- in-launch split-K combine (cdna_hip_programming §5 "Projection GEMM" item 2, sc1 form) ----
+  if constexpr (SK) {
+    constexpr int NF = FM * FN;
+    const int S = gridDim.y;
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc((void*)p.slab, 0, p.slab_bytes, 0x00020000);
+    // slab (split, tile): NF blocks of NT x 16 B, lane-linear -> every store / load is a whole 1 KiB per wave
+    auto slab_off = [&](int sp, int f) -> unsigned {
+      return (unsigned)((((size_t)(sp * ntiles + wg) * NF + f) * NT + tid) * 16);
+    };
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsl, slab_off(split, i * FN + j),
+                                               0, 16 /* sc1: write-through */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the ticket
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(p.tcnt + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != S - 1) return;  // not the last split of this tile
+    if (tid == 0) __hip_atomic_store(p.tcnt + wg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // sum in split order (own partial from registers): the same bits whichever split arrives last
+    f32x4 tot[FM][FN];
+    for (int sp = 0; sp < S; ++sp) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const f32x4 v = sp == split ? acc[i][j]
+                                      : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                      rsl, slab_off(sp, i * FN + j), 0, 16 /* sc1 */));
+          tot[i][j] = sp == 0 ? v : tot[i][j] + v;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j];
   }
 
   // ---- stage the accumulator tile through LDS (all DMA has landed: last wait was vmcnt(0)) ----
@@ -585,10 +632,10 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
 }
 
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
-          bool SGDPF = false>
+          bool SGDPF = false, bool SK = false>
 static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB, SGDPF>),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB, SGDPF, SK>),
                      dim3(tiles, splits), dim3(NW * 64), 0, s, p);
   return hipGetLastError();
 }
@@ -597,9 +644,10 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
 static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {
-  static const int t[14][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
-                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256}};
-  const int c = (cfg >= 0 && cfg <= 13) ? cfg : 7;
+  static const int t[16][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
+                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
+                               {128, 128}, {128, 128}};
+  const int c = (cfg >= 0 && cfg <= 15) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
 }
@@ -613,6 +661,8 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 11: return launch<128, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s); // BK 128, 96 KiB
     case 12: return launch<64, 64, 2, AK, BKc, AMODE, BMODE, 4, 2>(p, splits, s);  // BK 128, 64 KiB (2 WG/CU)
     case 13: return launch<256, 256, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 64x128 each, 128 KiB
+    case 14: return launch<128, 128, 3, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 96 KiB
+    case 15: return launch<128, 128, 4, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 128 KiB
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
     case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
@@ -621,6 +671,21 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 5: return launch<64, 128, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
     case 6: return launch<128, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  72 KiB, 2 WG/CU
     default: return launch<64, 64, 3, AK, BKc, AMODE, BMODE>(p, splits, s);   //  48 KiB, 3 WG/CU
+  }
+}
+
+// In-launch split-K variants (Params.slab / tcnt / klen set, gridDim.y = splits >= 2).
+template <bool AK, bool BKc>
+static hipError_t dispatch_sk(const Params& p, int cfg, int splits, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch<128, 128, 4, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, false, true>(p, splits, s);
+    case 5: return launch<64, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, false, true>(p, splits, s);
+    case 6: return launch<128, 64, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, false, true>(p, splits, s);
+    case 10: return launch<64, 128, 2, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 2, false, true>(p, splits, s);
+    case 8: return launch<256, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
+    case 14: return launch<128, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
+    case 15: return launch<128, 128, 4, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
+    default: return hipErrorInvalidValue;
   }
 }
 

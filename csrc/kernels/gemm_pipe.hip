@@ -50,74 +50,6 @@ __global__ void __launch_bounds__(256) reduce_partials_kernel(const float* __res
   }
 }
 
-// Split-K finish: out = epi( sum_s part[s] ) in fixed split order (deterministic), plus per-4-row-block
-// column sums of the stored values (colsum [ceil(M/4)][N], the fused bias gradient of dgrad).
-// Block = 64 column quads x 4 rows; one f32x4 per thread per slab: a pure stream with >2k blocks.
-template <int E>
-__global__ void __launch_bounds__(256) splitk_finish_kernel(Params p, const float* __restrict__ part, int S) {
-  const int cq = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int n = blockIdx.x * 256 + cq * 4;
-  const int m = blockIdx.y * 4 + ty;
-  const size_t slab = (size_t)p.M * p.N;
-  float st[4] = {0.f, 0.f, 0.f, 0.f};
-  if (n < p.N && m < p.M) {
-    f32x4 v[8];
-    const int S8 = S < 8 ? S : 8;
-#pragma unroll
-    for (int sp = 0; sp < 8; ++sp)
-      if (sp < S8) v[sp] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + sp * slab + (size_t)m * p.N + n));
-    f32x4 acc = v[0];
-#pragma unroll
-    for (int sp = 1; sp < 8; ++sp)
-      if (sp < S8) { acc[0] += v[sp][0]; acc[1] += v[sp][1]; acc[2] += v[sp][2]; acc[3] += v[sp][3]; }
-    for (int sp = 8; sp < S; ++sp) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(part + sp * slab + (size_t)m * p.N + n);
-      acc[0] += w[0]; acc[1] += w[1]; acc[2] += w[2]; acc[3] += w[3];
-    }
-    const size_t off = (size_t)m * p.ldc + n;
-    float cin[4] = {0.f, 0.f, 0.f, 0.f};
-    unsigned short av[4] = {0, 0, 0, 0};
-    if constexpr (E == EPI_F32) {
-      if (p.accumulate) for (int q = 0; q < 4; ++q) cin[q] = reinterpret_cast<const float*>(p.C)[off + q];
-    } else if constexpr (E == EPI_BF16) {
-      if (p.accumulate) for (int q = 0; q < 4; ++q) cin[q] = bf2f(reinterpret_cast<const unsigned short*>(p.C)[off + q]);
-    } else if constexpr (E == EPI_RELUMASK_BF16) {
-      const u32x2 a = *reinterpret_cast<const u32x2*>(p.aux + (size_t)m * p.ldaux + n);
-      av[0] = a[0] & 0xffffu; av[1] = a[0] >> 16; av[2] = a[1] & 0xffffu; av[3] = a[1] >> 16;
-    }
-    for (int q = 0; q < 4; ++q) {
-      float po, bo;
-      st[q] = epi_one<E>(p, p.C, off + q, n + q, acc[q], 0.f, cin[q], av[q], 0.f, 0.f, &po, &bo);
-    }
-    if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
-      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.C) + off) = (f32x4){st[0], st[1], st[2], st[3]};
-    } else {
-      *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(p.C) + off) =
-          (u32x2){pack_bf2(st[0], st[1]), pack_bf2(st[2], st[3])};
-    }
-  }
-  if (!p.colsum) return;
-  __shared__ float red[4][256];
-  for (int q = 0; q < 4; ++q) red[ty][cq * 4 + q] = st[q];
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (blockIdx.x * 256 + t < p.N)
-    p.colsum[(size_t)blockIdx.y * p.N + blockIdx.x * 256 + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-}
-
-// Split-K plan for the M = 512-row products (forward, dgrad): 256x128 tiles on 8 waves (2x the
-// arithmetic intensity of 128x128: the 64x64-tile kernel is bound by L2->LDS operand traffic, not
-// MFMA), K split so that ~256 workgroups fill the CUs.  Returns splits (1 = no split-K).
-static int splitk_plan(int M, int N, int K, bool ak, bool bk) {
-  if (!ak || M > 2048 || K < 1024) return 1;  // wgrad-shaped / large-M / short-K: regular tiles
-  const int tiles = ((M + 255) / 256) * ((N + 127) / 128);
-  if (tiles >= 192) return 1;
-  int s = (256 + tiles - 1) / tiles;
-  const int kb = K / 64;
-  while (s > 1 && kb / s < 8) --s;  // keep >= 8 K-steps per split
-  return s < 1 ? 1 : s;
-}
-
 // Default tile per operand-layout class, from the MI355X sweep of the MLP shapes
 // (benchmarks/mlp_gemm_bench.py, benchmarks/sgd_bw.py; profiles/r1_gemm2): the M=512-row products
 // want 64x64 tiles with 128-wide K stages (fwd 27.1 vs 29.1 us, dgrad 36.5 vs 45.1 us at H=4096),
@@ -129,6 +61,42 @@ static int pick(int M, int N, int K, bool ak, bool bk) {
   return 12;  // M=512-row forward / dgrad: 64x64, BK=128 (one barrier per 128 of K), 2 WG/CU
 }
 
+// In-launch split-K plan for the M = 512-row products (forward, dgrad: A K-contiguous).  Their 64x64
+// tiles are bound by L2 -> LDS operand traffic (each CU streams 2 MB of A/B panels for fc1 at ~78 GB/s;
+// profiles/r1_pmc, r2_ab): 128x128 tiles halve the bytes per FLOP, and splitting K two ways keeps all 256
+// CUs busy (128 tiles x 2), with the partial sums combined inside the same launch by the last split of
+// each tile (64 KiB write-through slab per split, register layout).  The 128x128 tile needs 8 waves
+// issuing LDS-DMA (4 waves at one workgroup per CU measured 28.9 / 32.3 / 46.2 us vs 21.8 / 26.8 / 34.8
+// for the 64x64 tiles on fc0 fwd / fc1 fwd / fc1 dgrad).  Returns splits (1: no split), sets *cfg.
+// Measured on MI355X in one process (benchmarks/mlp_step_kernels.py, profiles/r2_splitk): every split
+// tile so far is slower than the 64x64 single-pass tile at M = 512 (fc1 fwd 26.7 us single-pass vs
+// 28.9 on 8-wave 128x128 / 27.5 on 64x128 at 2 per CU / 37.3 on 256x128 split 4), so the plan is OFF by
+// default.  DDPX_SPLITK=<cfg> enables it with that tile; DDPX_SPLITK_MAX caps the splits (default 2).
+static int plan(int M, int N, int K, bool ak, bool bk, int epi, int* cfg) {
+  *cfg = pick(M, N, K, ak, bk);
+  static const int sk_cfg = [] {  // DDPX_SPLITK: 0 = off, else the split tile config (default 14)
+    const char* e = getenv("DDPX_SPLITK");
+    return e ? atoi(e) : 0;
+  }();
+  static const int sk_max = [] {
+    const char* e = getenv("DDPX_SPLITK_MAX");
+    return e ? atoi(e) : 2;
+  }();
+  if (sk_cfg <= 0 || !ak || epi == EPI_SGD || epi == EPI_BNSTAT_BF16 || K < 1024) return 1;
+  int bm, bn;
+  tile_of(sk_cfg, &bm, &bn);
+  // workgroups that fill the chip: 2 per CU for the 4-wave tiles whose LDS ring fits twice per CU
+  const int target = (sk_cfg == 5 || sk_cfg == 6 || sk_cfg == 7) ? 512 : 256;
+  const int t = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (t * 4 >= target * 3) return 1;
+  int s = target / t;
+  if (s > sk_max) s = sk_max;
+  while (s > 1 && (K / 64) / s < 8) --s;  // >= 8 K-steps of 64 per split
+  if (s < 2) return 1;
+  *cfg = sk_cfg;
+  return s;
+}
+
 }  // namespace pipe
 }  // namespace ddpx
 
@@ -136,16 +104,33 @@ using namespace ddpx;
 
 // Number of row tiles (M direction) the kernel will use for cfg (for sizing colsum partials).
 DDPX_API int ddpx_gemm_pipe_tiles_m(int M, int N, int K, int a_kcontig, int b_kcontig, int tile_cfg) {
-  const int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  int cfg = tile_cfg;
+  if (cfg < 0) pipe::plan(M, N, K, a_kcontig, b_kcontig, pipe::EPI_BF16, &cfg);
   int bm, bn;
   pipe::tile_of(cfg, &bm, &bn);
   return (M + bm - 1) / bm;
 }
 
+DDPX_API void ddpx_gemm_tile_dims(int cfg, int* bm, int* bn) { pipe::tile_of(cfg, bm, bn); }
+
+// Launch plan for ddpx_gemm_pipe with tile_cfg = -1: splits (> 1: in-launch split-K, needing a slab of
+// *slab_floats floats and *tickets zeroed ints), and the tile config.
+DDPX_API int ddpx_gemm_pipe_plan(int M, int N, int K, int a_kcontig, int b_kcontig, int epi, int* cfg,
+                                 long long* slab_floats, int* tickets) {
+  const int s = pipe::plan(M, N, K, a_kcontig, b_kcontig, epi, cfg);
+  int bm, bn;
+  pipe::tile_of(*cfg, &bm, &bn);
+  const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  *slab_floats = s > 1 ? (long long)s * tiles * bm * bn : 0;
+  *tickets = s > 1 ? (int)tiles : 0;
+  return s;
+}
+
 DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* bias, const void* aux, float* colsum,
                             int M, int N, int K, int lda, int ldb, int ldc, int ldaux, int a_kcontig, int b_kcontig,
                             int epi, int accumulate, float alpha, int tile_cfg, float* sgd_p, float* sgd_buf,
-                            void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd, hipStream_t stream) {
+                            void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd, int splits,
+                            float* slab, long long slab_floats, int* tcnt, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (a_kcontig ? (K % 8 || lda % 8) : (M % 8 || lda % 8)) return -1;
   if (b_kcontig ? (K % 8 || ldb % 8) : (N % 8 || ldb % 8)) return -2;
@@ -156,7 +141,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   pipe::Params p{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
                  M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes,
                  SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
-                 pipe::make_geom(0, 0, 0, 0), 0, 0};
+                 pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr};
   if (epi == pipe::EPI_SGD && (!sgd_p || !sgd_lr || (sgd_mom != 0.f && !sgd_buf))) return -5;
   static const int sgd_plain = [] {
     const char* e = getenv("DDPX_SGD_PLAIN");
@@ -164,6 +149,21 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   p.sgd_plain = sgd_plain;
   int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  if (splits > 1) {  // in-launch split-K (ddpx_gemm_pipe_plan): the caller's cfg, slab and zeroed tickets
+    if (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || !slab || !tcnt || tile_cfg < 0 || !a_kcontig)
+      return -7;
+    int bm, bn;
+    pipe::tile_of(cfg, &bm, &bn);
+    const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    if (slab_floats < (long long)splits * tiles * bm * bn || slab_floats * 4 >= 0x80000000ll) return -8;
+    int klen = (K + splits - 1) / splits;
+    klen = (klen + 63) / 64 * 64;
+    if ((K + klen - 1) / klen != splits) return -9;
+    p.klen = klen;
+    p.slab = slab;
+    p.slab_bytes = (unsigned)(slab_floats * 4);
+    p.tcnt = tcnt;
+  }
   // Weight gradients stored to a buffer (DDP path: bf16 / fp32 gradient output, no fused optimizer):
   // the 256x256 8-wave tile moves a quarter of the 64x128 tile's L2->LDS operand bytes and is faster
   // once it fills half the chip (MI355X, K = 512: 35.4 vs 46.1 us on 4096x4096, 30.9 vs 38.6 us on
@@ -184,63 +184,17 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
     return (int)pipe::dispatch_sgd_prefetch<false, false>(p, cfg, stream);
   }
   hipError_t e;
-  if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
-  else if (a_kcontig) e = pipe::dispatch<true, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
-  else if (b_kcontig) e = pipe::dispatch<false, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
-  else e = pipe::dispatch<false, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, 1, stream);
-  return (int)e;
-}
-
-// Split-K plan query: splits (>1 means ddpx_gemm_pipe_splitk applies), scratch floats, colsum rows.
-DDPX_API int ddpx_gemm_splitk_plan(int M, int N, int K, int a_kcontig, int b_kcontig, long long* scratch_floats,
-                                   int* colsum_rows) {
-  const int s = pipe::splitk_plan(M, N, K, a_kcontig, b_kcontig);
-  *scratch_floats = s > 1 ? (long long)s * M * N : 0;
-  *colsum_rows = (M + 3) / 4;
-  return s;
-}
-
-// C = epi(A.B) via split-K on the 8-wave 256x128 tile: fp32 partial slabs in `scratch`, then a
-// fixed-order reduction kernel that applies the epilogue (and per-64-row column sums).
-DDPX_API int ddpx_gemm_pipe_splitk(const void* A, const void* B, void* C, const float* bias, const void* aux,
-                                   float* colsum, int M, int N, int K, int lda, int ldb, int ldc, int ldaux,
-                                   int a_kcontig, int b_kcontig, int epi, int accumulate, float alpha, int splits,
-                                   float* scratch, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (splits < 1 || !scratch) return -7;
-  if (!a_kcontig || (K % 8) || (lda % 8)) return -1;
-  if (b_kcontig ? (K % 8 || ldb % 8) : (N % 8 || ldb % 8)) return -2;
-  if (N % 4 || ldc % 4) return -8;
-  if (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16) return -6;
-  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -3;
-  const size_t a_bytes = ((size_t)(M - 1) * lda + K) * 2;
-  const size_t b_bytes = (size_t)(b_kcontig ? (size_t)(N - 1) * ldb + K : (size_t)(K - 1) * ldb + N) * 2;
-  if (a_bytes >= 0x80000000ull || b_bytes >= 0x80000000ull) return -4;
-  int klen = (K + splits - 1) / splits;
-  klen = (klen + 63) / 64 * 64;
-  const int S = (K + klen - 1) / klen;
-  pipe::Params pp{(const unsigned short*)A, (const unsigned short*)B, scratch, nullptr, nullptr, nullptr,
-                  M, N, K, lda, ldb, N, 0, pipe::EPI_F32, 0, 1.f, (unsigned)a_bytes, (unsigned)b_bytes,
-                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::make_geom(0, 0, 0, 0), klen,
-                  (long long)M * N};
-  hipError_t e = b_kcontig
-                     ? pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(pp, 8, S, stream)
-                     : pipe::dispatch<true, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(pp, 8, S, stream);
-  if (e != hipSuccess) return (int)e;
-  pipe::Params fp{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
-                  M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, 0u, 0u,
-                  SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, pipe::make_geom(0, 0, 0, 0), 0, 0};
-  const dim3 grid((N + 255) / 256, (M + 3) / 4);
-  switch (epi) {
-    case pipe::EPI_F32: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_F32>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    case pipe::EPI_BF16: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_BF16>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    case pipe::EPI_BIAS_BF16: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_BIAS_BF16>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    case pipe::EPI_BIAS_RELU_BF16: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_BIAS_RELU_BF16>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    case pipe::EPI_BIAS_F32: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_BIAS_F32>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    case pipe::EPI_RELUMASK_BF16: hipLaunchKernelGGL(pipe::splitk_finish_kernel<pipe::EPI_RELUMASK_BF16>, grid, dim3(256), 0, stream, fp, scratch, S); break;
-    default: return -6;
+  if (splits > 1) {
+    e = b_kcontig ? pipe::dispatch_sk<true, true>(p, cfg, splits, stream)
+                  : pipe::dispatch_sk<true, false>(p, cfg, splits, stream);
+    return (int)e;
   }
-  return (int)hipGetLastError();
+  const int S = 1;
+  if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
+  else if (a_kcontig) e = pipe::dispatch<true, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
+  else if (b_kcontig) e = pipe::dispatch<false, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
+  else e = pipe::dispatch<false, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
+  return (int)e;
 }
 
 DDPX_API int ddpx_reduce_partials(const float* part, int T, int N, void* out, int out_bf16, int accumulate,

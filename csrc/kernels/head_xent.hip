@@ -1,62 +1,28 @@
 // ddpx — fused classifier head: Linear(K -> C<=16) + softmax cross-entropy
 // (forward), and its backward fused with the preceding ReLU's mask and bias
-// gradient.
+// gradient.  ONE launch each way.
 //
 // Reference ops replaced:
 //   classifier Linear  /root/reference/singlegpu.py:73,81 (`self.classifier(x)`)
 //   F.cross_entropy    /root/reference/singlegpu.py:105
 //   argmax/eq/sum eval /root/reference/singlegpu.py:200-206
 //
-// With C = 10 classes the head is skinny (N = 10): the work is a few MFLOP
-// and a few MB of streaming, so the design goal is PARALLELISM and no long
-// dependent chains:
-//   forward  = split-K MFMA partial logits (16 rows x 16 padded classes per
-//              workgroup slice, 4 waves split the slice's K) + a row-parallel
-//              finalize (bias, log-softmax, NLL, dlogits, argmax) + a
-//              deterministic mean;
-//   backward = row-split x column-tile workgroups (>= 256 of them) that
-//              each produce dH for their tile and partial dW / bias sums,
-//              followed by a fixed-order reduction of the partials
-//              (bitwise reproducible, no float atomics).
+// With C = 10 classes the head is skinny: a few MFLOP and a few MB of traffic, so what costs time
+// is kernel boundaries, serial cross-workgroup reductions and idle CUs, not arithmetic (the r1
+// split-K design took four launches and 28.5 us at M = 512, K = 4096):
+//   forward  = (16-row block x K slice) workgroups; the last slice of a row block to arrive sums
+//              the slices' partial logits and finishes its rows (bias, log-softmax, NLL, dlogits,
+//              argmax), and the last row block sums the batch-mean loss (write-through partials +
+//              agent-scope tickets, fixed summation orders);
+//   backward = one workgroup per 16-column slab over ALL rows: dH for the slab, and the slab's
+//              complete dW / previous-layer bias sums (reduced in registers + LDS in a fixed order),
+//              stored or applied (fused SGD) directly.  Head bias gradient by workgroup 0.
 #include "ddpx_common.h"
 
 namespace ddpx {
 
-constexpr int kHeadC = 16;  // classes padded to one MFMA tile
-
-// partial[ks][m][16] = sum_{k in slice ks} H[m][k] * W[c][k]   (c >= C -> 0)
-__global__ void __launch_bounds__(256)
-head_logits_partial_kernel(const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M,
-                           int K, int C, int ldh, int kslice, float* __restrict__ partial) {
-  __shared__ float red[4][16][17];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * 16, ks = blockIdx.y;
-  const int kbeg = ks * kslice;
-  const int kend = min(K, kbeg + kslice);
-  const int wlen = (kslice + 3) / 4;
-  const int wb = kbeg + wave * wlen;
-  const int we = min(kend, wb + wlen);
-  const int row = m0 + (lane & 15);
-  const int cls = lane & 15;
-  const int ko = 8 * (lane >> 4);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k = wb; k < we; k += 32) {
-    const int kk = k + ko;
-    u32x4 av = {0u, 0u, 0u, 0u}, bv = {0u, 0u, 0u, 0u};
-    if (row < M && kk < we) av = *reinterpret_cast<const u32x4*>(H + (size_t)row * ldh + kk);
-    if (cls < C && kk < we) bv = *reinterpret_cast<const u32x4*>(W + (size_t)cls * K + kk);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
-                                                  acc, 0, 0, 0);
-  }
-  // C/D map: col (class) = lane&15, row = 4*(lane>>4) + r
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
-  __syncthreads();
-  const int t = threadIdx.x;
-  const int rr = t >> 4, cc = t & 15;
-  const float s = (red[0][rr][cc] + red[1][rr][cc]) + (red[2][rr][cc] + red[3][rr][cc]);
-  if (m0 + rr < M) partial[((size_t)ks * M + m0 + rr) * kHeadC + cc] = s;
-}
+constexpr int kHeadC = 16;      // classes padded to one MFMA tile
+constexpr int kHeadCols = 16;   // backward: columns per workgroup
 
 // Per row, given the summed logits z (bias not yet added): log-softmax, NLL, dlogits, argmax.
 // Returns the row loss (0 for no target).
@@ -91,239 +57,269 @@ __device__ __forceinline__ float head_finish(float (&z)[kHeadC], const float* __
   return lse - zt;
 }
 
-// Partial-logit slices ks = k0, k0 + kstep, ... of row m summed into z.
-__device__ __forceinline__ void head_sum(const float* __restrict__ partial, int KS, int M, int m, int k0, int kstep,
-                                         float (&z)[kHeadC]) {
-#pragma unroll
-  for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
-  for (int ks = k0; ks < KS; ks += kstep) {
-    const f32x4* pp = reinterpret_cast<const f32x4*>(partial + ((size_t)ks * M + m) * kHeadC);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = pp[q];
-      z[4 * q] += v[0];
-      z[4 * q + 1] += v[1];
-      z[4 * q + 2] += v[2];
-      z[4 * q + 3] += v[3];
-    }
-  }
-}
-
-__device__ __forceinline__ float head_row(const float* __restrict__ partial, int KS, const float* __restrict__ b,
-                                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, int m,
-                                          float* __restrict__ logits, float* __restrict__ dlogits, int* hit) {
-  float z[kHeadC];
-  head_sum(partial, KS, M, m, 0, 1, z);
-  return head_finish(z, b, tgt, C, inv_m, m, logits, dlogits, hit);
-}
-
-// One thread per row.
+// Forward.  Workgroup (rb, ks) = 16 rows x one K slice (256 workgroups at M = 512: a 32-workgroup
+// row-only split left 7/8 of the chip idle and ran 14.6 us); its 4 waves split the slice, issue all
+// their loads first, and multiply on v_mfma_f32_16x16x32_bf16 (A = 16 rows of H, B = the 16 padded
+// classes of W).  The [16][16] partial goes out write-through (sc1) and the workgroup takes the row
+// block's agent-scope ticket; the last of the KS slices to arrive sums the partials in slice order
+// (deterministic), finishes the 16 rows (bias, log-softmax, NLL, dlogits, argmax), stores their losses
+// write-through and takes the batch ticket; the last row block sums every row loss in row order.
+// Both hand-offs follow MI355X_MICROARCH.md "Valid forms", row 1 (sc1 stores drained before the
+// ticket, sc1 loads after it): no release or acquire fence.  Each last arriver resets its ticket.
 __global__ void __launch_bounds__(256)
-head_finalize_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
-                     const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
-                     float* __restrict__ loss_rows, float* __restrict__ dlogits, int* __restrict__ correct) {
-  const int m = blockIdx.x * 256 + threadIdx.x;
-  int hit = 0;
-  if (m < M) {
-    const float l = head_row(partial, KS, b, tgt, M, C, inv_m, m, logits, dlogits, &hit);
-    if (loss_rows) loss_rows[m] = l;
-  }
-  if (correct) {
-    const unsigned long long bal = __ballot(hit);
-    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(correct, __popcll(bal));  // integer: deterministic
-  }
-}
-
-// Single workgroup (M <= 8192): every row plus the mean loss in one launch.  TL lanes share a row
-// (each sums every TL-th partial-logit slice, so the slice loads of a row are in flight together
-// instead of in one thread's serial chain), a butterfly combines them, and the group's first lane
-// finishes the row.  Rows are assigned in a fixed pattern and reduced in a fixed order: deterministic.
-template <int TL>
-__global__ void __launch_bounds__(1024)
-head_finalize_mean_kernel(const float* __restrict__ partial, int KS, const float* __restrict__ b,
-                          const int64_t* __restrict__ tgt, int M, int C, float inv_m, float* __restrict__ logits,
-                          float* __restrict__ loss_rows, float* __restrict__ dlogits, int* __restrict__ correct,
-                          float* __restrict__ loss_mean) {
-  __shared__ float red[16];
-  constexpr int RPP = 1024 / TL;  // rows per pass
-  const int sub = threadIdx.x % TL, r = threadIdx.x / TL;
-  float acc = 0.f;
-  int hits = 0;
-  for (int m0 = 0; m0 < M; m0 += RPP) {
-    const int m = m0 + r;
-    float z[kHeadC];
-    if (m < M) head_sum(partial, KS, M, m, sub, TL, z);
-    else {
+head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __restrict__ W,
+                const float* __restrict__ b, const int64_t* __restrict__ tgt, int M, int K, int C, int ldh, int KS,
+                int kslice, float inv_m, float* __restrict__ logits, float* __restrict__ dlogits,
+                int* __restrict__ correct, float* part, float* loss_rows, int* tickets, float* __restrict__ loss_mean) {
+  // one LDS object (cdna_hip_programming §5 item 4a): [4 waves][16][17] partials + [16][17] sums + flags
+  __shared__ float lds[4 * 16 * 17 + 16 * 17 + 4];
+  float* zs = lds + 4 * 16 * 17;
+  int* flag = reinterpret_cast<int*>(zs + 16 * 17);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rb = blockIdx.x / KS, ks = blockIdx.x - rb * KS;
+  const int nrb = gridDim.x / KS;
+  const int m0 = rb * 16;
+  const int kw = kslice / 4;  // multiple of 32
+  const int kb = ks * kslice + wave * kw;
+  const int ke = min(K, kb + kw);
+  const int row = m0 + (lane & 15);
+  const int cls = lane & 15;
+  const int ko = 8 * (lane >> 4);
+  const bool rok = row < M, cok = cls < C;
+  const unsigned short* hp = H + (size_t)(rok ? row : 0) * ldh;
+  const unsigned short* wp = W + (size_t)(cok ? cls : 0) * K;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int KST = 4;  // MFMA steps whose loads are in flight together
+  for (int k = kb; k < ke; k += 32 * KST) {
+    u32x4 av[KST], bv[KST];
 #pragma unroll
-      for (int c = 0; c < kHeadC; ++c) z[c] = 0.f;
+    for (int i = 0; i < KST; ++i) {
+      const int kk = k + 32 * i + ko;
+      av[i] = bv[i] = (u32x4){0u, 0u, 0u, 0u};
+      if (rok && kk < ke) av[i] = *reinterpret_cast<const u32x4*>(hp + kk);
+      if (cok && kk < ke) bv[i] = *reinterpret_cast<const u32x4*>(wp + kk);
     }
 #pragma unroll
-    for (int o = 1; o < TL; o <<= 1)
-#pragma unroll
-      for (int c = 0; c < kHeadC; ++c) z[c] += __shfl_xor(z[c], o, 64);
-    if (m < M && sub == 0) {
-      int hit = 0;
-      const float l = head_finish(z, b, tgt, C, inv_m, m, logits, dlogits, &hit);
-      if (loss_rows) loss_rows[m] = l;
-      acc += l;
-      hits += hit;
-    }
+    for (int i = 0; i < KST; ++i)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[i]),
+                                                    __builtin_bit_cast(bf16x8, bv[i]), acc, 0, 0, 0);
   }
-  if (correct) {
-    int hsum = hits;
+  // C/D map: col (class) = lane&15, row = 4*(lane>>4) + r
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) hsum += __shfl_xor(hsum, o, 64);
-    if ((threadIdx.x & 63) == 0 && hsum) atomicAdd(correct, hsum);
-  }
-  acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  for (int r = 0; r < 4; ++r) lds[(wave * 16 + 4 * (lane >> 4) + r) * 17 + (lane & 15)] = acc[r];
   __syncthreads();
-  if (threadIdx.x < 64) {
-    float t = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
-    t = wave_sum(t);
-    if (threadIdx.x == 0) *loss_mean = t / (float)M;
+  const int t = threadIdx.x;
+  const int rr = t >> 4, cc = t & 15;
+  float z = (lds[rr * 17 + cc] + lds[(16 + rr) * 17 + cc]) + (lds[(32 + rr) * 17 + cc] + lds[(48 + rr) * 17 + cc]);
+  if (KS > 1) {
+    __hip_atomic_store(part + (size_t)blockIdx.x * 256 + t, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) *flag = __hip_atomic_fetch_add(tickets + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+    __syncthreads();
+    if (!*flag) return;
+    // sc1 buffer loads, all in flight together (relaxed atomic loads were each waited for: 8 serial
+    // round trips); summed in slice order, whichever slice arrived last
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(part + (size_t)rb * KS * 256), 0,
+                                                                          (unsigned)(KS * 256 * 4), 0x00020000);
+    z = 0.f;
+    for (int s0 = 0; s0 < KS; s0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        v[q] = s0 + q < KS ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, ((s0 + q) * 256 + t) * 4, 0, 16))
+                           : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) z += v[q];
+    }
+    if (t == 0) __hip_atomic_store(tickets + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// Deterministic mean of loss_rows (single workgroup).
-__global__ void __launch_bounds__(1024) mean_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
-  __shared__ float red[16];
+  zs[rr * 17 + cc] = z;
+  __syncthreads();
+  if (wave == 0) {
+    int hit = 0;
+    if (lane < 16 && m0 + lane < M) {
+      const int m = m0 + lane;
+      float zr[kHeadC];
+#pragma unroll
+      for (int c = 0; c < kHeadC; ++c) zr[c] = zs[lane * 17 + c];
+      const float l = head_finish(zr, b, tgt, C, inv_m, m, logits, dlogits, &hit);
+      if (loss_mean) __hip_atomic_store(loss_rows + m, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (correct) {
+      const unsigned long long bal = __ballot(hit);
+      if (lane == 0 && bal) atomicAdd(correct, __popcll(bal));  // integer: deterministic
+    }
+  }
+  if (!loss_mean) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains its sc1 stores
+  __syncthreads();
+  if (t == 0) flag[1] = __hip_atomic_fetch_add(tickets + nrb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nrb - 1;
+  __syncthreads();
+  if (!flag[1] || wave != 0) return;
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)loss_rows, 0, (unsigned)(M * 4), 0x00020000);
   float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float t = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
-    t = wave_sum(t);
-    if (threadIdx.x == 0) *out = t / (float)n;
+  for (int i0 = 0; i0 < M; i0 += 64 * 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)  // out-of-range lanes read zeros (buffer bounds check)
+      v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rl, (i0 + q * 64 + lane) * 4, 0, 16));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  s = wave_sum(s);  // fixed butterfly: the same order whichever row block is last
+  if (lane == 0) {
+    *loss_mean = s / (float)M;
+    __hip_atomic_store(tickets + nrb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// Backward partials.  Workgroup (column tile ct of 64, row split rs):
+// Sum over the 32 lanes of each half-wave (every lane of the half gets it): DPP within 16-lane rows
+// (quad xor 1, quad xor 2, row rotate 4, row rotate 8: plain VALU), then one swap across the row pair.
+// The DPP adds run in a fixed pattern, so the result does not depend on timing.
+__device__ __forceinline__ float half_wave_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  return v + __shfl_xor(v, 16, 64);
+}
+
+// Backward.  Workgroup = a 16-column slab [k0, k0+16) over all M rows (256 workgroups at K = 4096);
+// thread (cg = half-wave, r0 = wave * 32 + lane % 32) owns 8 columns of rows r0, r0+256, ... (the two
+// 16-B halves of a row come from lanes l and l+32 of one wave instruction) and issues the loads of
+// RPT such rows before computing any of them (the 32-column, one-row-in-flight version was latency
+// bound: 15.5 us at M = 512):
 //   g[m][k]  = go * sum_c dlogits[m][c] * W[c][k]
 //   dH[m][k] = hscale * (relu_mask ? g * (H[m][k] > 0) : g)             (bf16, stored)
 //   (hscale = 1/(1-p) when H is the output of an inverted Dropout(p) after a ReLU: H > 0 is then
 //    exactly "kept and positive", so the dropout + ReLU backward costs nothing extra)
-//   pdw[rs][c][k]  = go * sum_{m in split} dlogits[m][c] * H[m][k]
-//   pdb[rs][k]     = sum_{m in split} dH[m][k]     (bias grad of the layer that produced H)
-// 8 lanes x 8 columns per row, 32 rows per pass, ROWS_PER_SPLIT/32 passes.
+//   dW[c][k]    = go * sum_m dlogits[m][c] * H[m][k]
+//   dprev[k]    = sum_m dH[m][k]                  (bias gradient of the layer that produced H)
+//   db[c]       = go * sum_m dlogits[m][c]        (workgroup 0)
+// Column sums: registers over the thread's rows, then the 32 lanes of a half-wave (DPP row reduction +
+// one cross-row swap; a 5-step ds_bpermute butterfly over 88 values per lane was LDS-issue bound),
+// then the 8 waves in order through LDS — a fixed order, so the result is bitwise reproducible.
+// Outputs are stored (fp32 / bf16, written or accumulated) or, with SgdArgs.p set, applied as an SGD
+// update: each workgroup reads only its own columns of W, all before it updates them.
 template <int C>
-__global__ void __launch_bounds__(256)
-head_bwd_partial_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
-                        const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K,
-                        int ldh, int rows_per_split, unsigned short* __restrict__ dH, float* __restrict__ pdw,
-                        float* __restrict__ pdb, float* __restrict__ pdbh, int relu_mask, float hscale) {
-  __shared__ float red[4][64][C + 1];
-  __shared__ float redh[16][C];
+__global__ void __launch_bounds__(512)
+head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
+                const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K, int ldh,
+                unsigned short* __restrict__ dH, int relu_mask, float hscale, void* __restrict__ dW,
+                void* __restrict__ db, void* __restrict__ dbprev, int out_bf16, int accumulate, SgdArgs sW,
+                SgdArgs sB, SgdArgs sP) {
+  constexpr int NT = 512, NWV = NT / 64;
+  constexpr int TPR = kHeadCols / 8;  // threads per row
+  constexpr int RL = NT / TPR;        // rows per pass (256)
+  constexpr int RPT = 2;              // passes whose loads are in flight together
+  static_assert(C % 2 == 0, "dlogits rows are read as float2");
+  __shared__ float lds[NWV * kHeadCols * (C + 1) + NWV * C];
+  float* redh = lds + NWV * kHeadCols * (C + 1);
   const float go = go_ptr ? *go_ptr : 1.f;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int cg = tid & 7, r0 = tid >> 3;
-  const int k = blockIdx.x * 64 + cg * 8;
-  const int rs = blockIdx.y;
-  const int mbeg = rs * rows_per_split;
-  const int mend = min(M, mbeg + rows_per_split);
-  float wv[C][8];
+  static_assert(TPR == 2, "half-wave column groups");
+  const int cg = lane >> 5, r0 = w * 32 + (lane & 31);
+  const int k0 = blockIdx.x * kHeadCols;
+  const int k = k0 + cg * 8;
+  // W packed bf16, widened at each use
+  u32x4 wraw[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(W + (size_t)c * K + k);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      wv[c][2 * j] = __uint_as_float(v[j] << 16);
-      wv[c][2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
-    }
-  }
-  float dw[C][8], dbp[8];
+  for (int c = 0; c < C; ++c) wraw[c] = *reinterpret_cast<const u32x4*>(W + (size_t)c * K + k);
+  auto wv = [&](int c, int j) -> float {
+    return (j & 1) ? __uint_as_float(wraw[c][j >> 1] & 0xffff0000u) : __uint_as_float(wraw[c][j >> 1] << 16);
+  };
+  float dw[C][8], dbp[8], hb[C];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     dbp[j] = 0.f;
 #pragma unroll
     for (int c = 0; c < C; ++c) dw[c][j] = 0.f;
   }
-  for (int m = mbeg + r0; m < mend; m += 32) {
-    float dl[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) dl[c] = dlogits[(size_t)m * C + c] * go;
-    const u32x4 hv = *reinterpret_cast<const u32x4*>(H + (size_t)m * ldh + k);
-    float h[8];
+  for (int c = 0; c < C; ++c) hb[c] = 0.f;
+  const bool head_bias = blockIdx.x == 0 && cg == 0;  // one thread per row sums dlogits for the head bias
+  for (int mb = r0; mb < M; mb += RL * RPT) {
+    float2 dn[RPT][C / 2];
+    u32x4 hn[RPT];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      h[2 * j] = __uint_as_float(hv[j] << 16);
-      h[2 * j + 1] = __uint_as_float(hv[j] & 0xffff0000u);
+    for (int q = 0; q < RPT; ++q) {
+      const int m = mb + q * RL;
+      const int mm = m < M ? m : mb;  // rows past M re-read row mb and are skipped below
+      const float2* dp = reinterpret_cast<const float2*>(dlogits + (size_t)mm * C);  // 8-B aligned rows
+#pragma unroll
+      for (int c = 0; c < C / 2; ++c) dn[q][c] = dp[c];
+      hn[q] = *reinterpret_cast<const u32x4*>(H + (size_t)mm * ldh + k);
     }
-    float g[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = 0.f;
+    for (int q = 0; q < RPT; ++q) {
+      const int m = mb + q * RL;
+      if (m >= M) break;
+      float dl[C];
 #pragma unroll
-      for (int c = 0; c < C; ++c) s = fmaf(dl[c], wv[c][j], s);
-      if (relu_mask && !(h[j] > 0.f)) s = 0.f;
-      g[j] = s * hscale;
+      for (int c = 0; c < C / 2; ++c) {
+        dl[2 * c] = dn[q][c].x * go;
+        dl[2 * c + 1] = dn[q][c].y * go;
+      }
+      if (head_bias) {
 #pragma unroll
-      for (int c = 0; c < C; ++c) dw[c][j] = fmaf(dl[c], h[j], dw[c][j]);
-    }
-    u32x4 o;
+        for (int c = 0; c < C; ++c) hb[c] += dl[c];
+      }
+      float h[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = pack_bf2(g[2 * j], g[2 * j + 1]);
-    if (dH) *reinterpret_cast<u32x4*>(dH + (size_t)m * ldh + k) = o;
+      for (int j = 0; j < 4; ++j) {
+        h[2 * j] = __uint_as_float(hn[q][j] << 16);
+        h[2 * j + 1] = __uint_as_float(hn[q][j] & 0xffff0000u);
+      }
+      float g[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      dbp[2 * j] += __uint_as_float(o[j] << 16);
-      dbp[2 * j + 1] += __uint_as_float(o[j] & 0xffff0000u);
+      for (int j = 0; j < 8; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) s = fmaf(dl[c], wv(c, j), s);
+        if (relu_mask && !(h[j] > 0.f)) s = 0.f;
+        g[j] = s * hscale;
+#pragma unroll
+        for (int c = 0; c < C; ++c) dw[c][j] = fmaf(dl[c], h[j], dw[c][j]);
+      }
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf2(g[2 * j], g[2 * j + 1]);
+      if (dH) *reinterpret_cast<u32x4*>(dH + (size_t)m * ldh + k) = o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // bias gradient of the stored (bf16-rounded) dH
+        dbp[2 * j] += __uint_as_float(o[j] << 16);
+        dbp[2 * j + 1] += __uint_as_float(o[j] & 0xffff0000u);
+      }
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    dbp[j] = half_wave_sum(dbp[j]);
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {
-      dbp[j] += __shfl_xor(dbp[j], o, 64);
-#pragma unroll
-      for (int c = 0; c < C; ++c) dw[c][j] += __shfl_xor(dw[c][j], o, 64);
-    }
-  }
-  if (lane < 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[w][lane * 8 + j][C] = dbp[j];
-#pragma unroll
-      for (int c = 0; c < C; ++c) red[w][lane * 8 + j][c] = dw[c][j];
-    }
+    for (int c = 0; c < C; ++c) dw[c][j] = half_wave_sum(dw[c][j]);
   }
   if (blockIdx.x == 0) {
-    // head bias partial for this row split: pdbh[rs][c] = go * sum_m dlogits[m][c]
-    const int c = tid & 15, rg = tid >> 4;
-    float sh = 0.f;
-    if (c < C)
-      for (int m = mbeg + rg; m < mend; m += 16) sh += dlogits[(size_t)m * C + c];
-    if (c < C) redh[rg][c] = sh * go;
+#pragma unroll
+    for (int c = 0; c < C; ++c) hb[c] = half_wave_sum(hb[c]);  // cg 1 lanes hold zeros
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) redh[w * C + c] = hb[c];
+    }
+  }
+  if ((lane & 31) == 0) {  // lane 0: cg 0, lane 32: cg 1
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lds[(w * kHeadCols + cg * 8 + j) * (C + 1) + C] = dbp[j];
+#pragma unroll
+      for (int c = 0; c < C; ++c) lds[(w * kHeadCols + cg * 8 + j) * (C + 1) + c] = dw[c][j];
+    }
   }
   __syncthreads();
-  if (blockIdx.x == 0 && tid < C) {
-    float sh = 0.f;
-    for (int rg = 0; rg < 16; ++rg) sh += redh[rg][tid];
-    pdbh[(size_t)rs * C + tid] = sh;
-  }
-  for (int i = tid; i < 64 * (C + 1); i += 256) {
-    const int col = i % 64, c = i / 64;
-    const float s = (red[0][col][c] + red[1][col][c]) + (red[2][col][c] + red[3][col][c]);
-    const int kk = blockIdx.x * 64 + col;
-    if (c < C) pdw[((size_t)rs * C + c) * K + kk] = s;
-    else pdb[(size_t)rs * K + kk] = s;
-  }
-}
-
-// Fixed-order reduction of the row-split partials into the gradient buffers
-// (fp32 or bf16, write or accumulate) + the head bias gradient (workgroup 0).
-template <int C>
-__global__ void __launch_bounds__(256)
-head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict__ pdb,
-                         const float* __restrict__ pdbh, int RS, int K, void* __restrict__ dW,
-                         void* __restrict__ db, void* __restrict__ dbprev, int out_bf16, int accumulate,
-                         SgdArgs sW, SgdArgs sB, SgdArgs sP) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over (C+1)*K + C
-  auto put = [&](const SgdArgs* sg, void* base, size_t idx, float v) {
-    if (sg->p) {  // fused optimizer: update the parameter instead of storing its gradient
-      sgd_apply(*sg, idx, v, *sg->lr);
+  const float lr = sW.p ? *sW.lr : 0.f;
+  auto put = [&](const SgdArgs& sg, void* base, size_t idx, float v) {
+    if (sg.p) {  // fused optimizer: update the parameter instead of storing its gradient
+      sgd_apply(sg, idx, v, lr);
     } else if (out_bf16) {
       unsigned short* o = reinterpret_cast<unsigned short*>(base) + idx;
       *o = f2bf(accumulate ? v + bf2f(*o) : v);
@@ -332,22 +328,23 @@ head_bwd_finalize_kernel(const float* __restrict__ pdw, const float* __restrict_
       *o = accumulate ? v + *o : v;
     }
   };
-  if (i < C * K) {
+  if (tid < kHeadCols * (C + 1)) {
+    const int col = tid % kHeadCols, c = tid / kHeadCols;
     float s = 0.f;
-    for (int r = 0; r < RS; ++r) s += pdw[(size_t)r * C * K + i];
-    put(&sW, dW, i, s);
-  } else if (i < (C + 1) * K) {
-    if (!dbprev && !sP.p) return;
-    const int kk = i - C * K;
-    float s = 0.f;
-    for (int r = 0; r < RS; ++r) s += pdb[(size_t)r * K + kk];
-    put(&sP, dbprev, kk, s);
-  } else if (i < (C + 1) * K + C) {
-    if (!db && !sB.p) return;
-    const int c = i - (C + 1) * K;
-    float s = 0.f;
-    for (int r = 0; r < RS; ++r) s += pdbh[(size_t)r * C + c];
-    put(&sB, db, c, s);
+#pragma unroll
+    for (int ww = 0; ww < NWV; ++ww) s += lds[(ww * kHeadCols + col) * (C + 1) + c];
+    const int kk = k0 + col;
+    if (c < C) {
+      if (dW || sW.p) put(sW, dW, (size_t)c * K + kk, s);
+    } else if (dbprev || sP.p) {
+      put(sP, dbprev, kk, s);
+    }
+  }
+  if (blockIdx.x == 0 && tid < C && (db || sB.p)) {  // head bias: db[c] = go * sum_m dlogits[m][c]
+    float sh = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NWV; ++ww) sh += redh[ww * C + tid];
+    put(sB, db, tid, sh);
   }
 }
 
@@ -368,113 +365,56 @@ accuracy_kernel(const float* __restrict__ logits, const int64_t* __restrict__ tg
   if ((threadIdx.x & 63) == 0 && bal) atomicAdd(correct, __popcll(bal));
 }
 
-static int head_ksplit(int M, int K) {
-  const int row_tiles = (M + 15) / 16;
-  int ks = (256 + row_tiles - 1) / row_tiles;
-  const int maxks = max(1, K / 128);
-  if (ks > maxks) ks = maxks;
-  if (ks < 1) ks = 1;
-  return ks;
-}
-
-static int head_row_splits(int M, int K) {
-  const int ctiles = K / 64;
-  int rs = (256 + ctiles - 1) / ctiles;
-  const int maxrs = max(1, M / 32);
-  if (rs > maxrs) rs = maxrs;
-  return max(rs, 1);
-}
-
 }  // namespace ddpx
 
 using namespace ddpx;
 
-// Scratch sizes (floats) the host must provide for the head kernels.
-DDPX_API int64_t ddpx_head_fwd_scratch(int M, int K) { return (int64_t)head_ksplit(M, K) * M * kHeadC; }
-DDPX_API int64_t ddpx_head_bwd_scratch(int M, int K, int C) {
-  const int64_t rs = head_row_splits(M, K);
-  return rs * (C + 1) * K + rs * C;
+static int head_ksplit(int M, int K) {
+  const int rbs = (M + 15) / 16;
+  int ks = (256 + rbs - 1) / rbs;
+  const int maxks = max(1, K / 128);  // >= one 32-wide MFMA step per wave
+  return max(1, min(ks, maxks));
 }
 
-// loss_mean (optional): mean row loss written by the same launch (M <= 8192) or by a follow-up
-// single-workgroup reduction (larger M); loss_rows may then be null for M <= 8192.
+// Forward scratch (floats): slice partials [row blocks * KS][16][16] + row losses [M]; tickets (ints):
+// row blocks + 1, zero before the first launch (every launch leaves them zero).
+DDPX_API int64_t ddpx_head_fwd_scratch(int M, int K) {
+  const int64_t rbs = (M + 15) / 16;
+  return rbs * head_ksplit(M, K) * 256 + M;
+}
+DDPX_API int64_t ddpx_head_fwd_tickets(int M) { return (M + 15) / 16 + 1; }
+
 DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K, int C,
-                           int ldh, float inv_m, float* logits, float* loss_rows, float* dlogits, int* correct,
-                           float* scratch, float* loss_mean, hipStream_t s) {
+                           int ldh, float inv_m, float* logits, float* dlogits, int* correct, float* scratch,
+                           int* tickets, float* loss_mean, hipStream_t s) {
   if (M <= 0) return 0;
   if (C < 1 || C > kHeadC) return -1;
   if (K % 8 || ldh % 8) return -2;
+  if (!scratch || !tickets) return -3;
+  if (loss_mean && !tgt) return -4;
+  const int rbs = (M + 15) / 16;
   const int ks = head_ksplit(M, K);
   int kslice = (K + ks - 1) / ks;
-  kslice = (kslice + 127) / 128 * 128;  // whole 32-k MFMA steps for each of the 4 waves
-  hipLaunchKernelGGL(head_logits_partial_kernel, dim3((M + 15) / 16, ks), dim3(256), 0, s, (const unsigned short*)H,
-                     (const unsigned short*)W, M, K, C, ldh, kslice, scratch);
-  if (loss_mean && tgt && M <= 8192) {
-    // lanes per row: as many as keep every row in ONE pass of the 1024 threads (M <= 1024 / TL), at most
-    // one per partial-logit slice — more passes would each pay the load latency again
-    int tl = 1;
-    while (tl < 16 && tl < ks && M * tl * 2 <= 1024) tl *= 2;
-    if (tl == 1)
-      hipLaunchKernelGGL(head_finalize_mean_kernel<1>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                         logits, loss_rows, dlogits, correct, loss_mean);
-    else if (tl == 2)
-      hipLaunchKernelGGL(head_finalize_mean_kernel<2>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                         logits, loss_rows, dlogits, correct, loss_mean);
-    else if (tl == 4)
-      hipLaunchKernelGGL(head_finalize_mean_kernel<4>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                         logits, loss_rows, dlogits, correct, loss_mean);
-    else if (tl == 8)
-      hipLaunchKernelGGL(head_finalize_mean_kernel<8>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                         logits, loss_rows, dlogits, correct, loss_mean);
-    else
-      hipLaunchKernelGGL(head_finalize_mean_kernel<16>, dim3(1), dim3(1024), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                         logits, loss_rows, dlogits, correct, loss_mean);
-    return (int)hipGetLastError();
-  }
-  if (loss_mean && !loss_rows) return -3;
-  hipLaunchKernelGGL(head_finalize_kernel, dim3((M + 255) / 256), dim3(256), 0, s, scratch, ks, b, tgt, M, C, inv_m,
-                     logits, loss_rows, dlogits, correct);
-  if (loss_mean && tgt) hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, s, loss_rows, M, loss_mean);
+  kslice = (kslice + 127) / 128 * 128;  // whole 32-wide MFMA steps for each of the 4 waves
+  float* part = scratch;
+  float* loss_rows = scratch + (size_t)rbs * ks * 256;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(rbs * ks), dim3(256), 0, s, (const unsigned short*)H,
+                     (const unsigned short*)W, b, tgt, M, K, C, ldh, ks, kslice, inv_m, logits, dlogits, correct, part,
+                     loss_rows, tickets, loss_mean);
   return (int)hipGetLastError();
 }
 
-DDPX_API int ddpx_mean(const float* x, int n, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, s, x, n, out);
-  return (int)hipGetLastError();
-}
-
-// Backward in two launches: the partials (dH for every row + per-row-split dW / bias partials) and
-// the fixed-order finalize that stores or applies (fused SGD) the parameter gradients.  The finalize
-// is tiny (a separate entry point so a caller can time or reorder it).
-DDPX_API int ddpx_head_bwd_partial(const float* dlogits, const float* go, const void* H, const void* W, int M, int K,
-                                   int C, int ldh, void* dH, int relu_mask, float hscale, float* scratch,
-                                   hipStream_t s) {
+DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H, const void* W, int M, int K, int C,
+                           int ldh, void* dH, int relu_mask, float hscale, void* dW, void* db, void* dbprev,
+                           int out_bf16, int accumulate, float* sw_p, float* sw_buf, void* sw_sh, float* sb_p,
+                           float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh, const float* lr,
+                           float mom, float wd, hipStream_t s) {
   if (M <= 0) return 0;
   if (C != 10) return -1;
-  if (K % 64 || ldh % 8) return -2;
-  const int rs = head_row_splits(M, K);
-  const int rps = (M + rs - 1) / rs;
-  float* pdw = scratch;
-  float* pdb = scratch + (size_t)rs * C * K;
-  float* pdbh = pdb + (size_t)rs * K;
-  hipLaunchKernelGGL(head_bwd_partial_kernel<10>, dim3(K / 64, rs), dim3(256), 0, s, dlogits, go,
-                     (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, rps, (unsigned short*)dH, pdw, pdb,
-                     pdbh, relu_mask, hscale);
-  return (int)hipGetLastError();
-}
-
-DDPX_API int ddpx_head_bwd_finalize(int M, int K, int C, void* dW, void* db, void* dbprev, int out_bf16,
-                                    int accumulate, const float* scratch, float* sw_p, float* sw_buf, void* sw_sh,
-                                    float* sb_p, float* sb_buf, void* sb_sh, float* sp_p, float* sp_buf, void* sp_sh,
-                                    const float* lr, float mom, float wd, hipStream_t s) {
-  if (M <= 0) return 0;
-  if (C != 10) return -1;
-  const int rs = head_row_splits(M, K);
-  const float* pdw = scratch;
-  const float* pdb = scratch + (size_t)rs * C * K;
-  const float* pdbh = pdb + (size_t)rs * K;
-  hipLaunchKernelGGL(head_bwd_finalize_kernel<10>, dim3(((C + 1) * K + C + 255) / 256), dim3(256), 0, s, pdw, pdb,
-                     pdbh, rs, K, dW, db, dbprev, out_bf16, accumulate,
+  if (K % kHeadCols || ldh % 8) return -2;
+  hipLaunchKernelGGL(head_bwd_kernel<10>, dim3(K / kHeadCols), dim3(512), 0, s, dlogits, go,
+                     (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, (unsigned short*)dH, relu_mask,
+                     hscale, dW, db, dbprev, out_bf16, accumulate,
                      SgdArgs{sw_p, sw_buf, (unsigned short*)sw_sh, lr, mom, wd},
                      SgdArgs{sb_p, sb_buf, (unsigned short*)sb_sh, lr, mom, wd},
                      SgdArgs{sp_p, sp_buf, (unsigned short*)sp_sh, lr, mom, wd});

@@ -23,10 +23,9 @@ from ..runtime import native
 
 # "pipe" (LDS-DMA multi-stage ring, default) or "v1" (register-staged, 2 LDS buffers)
 GEMM_IMPL = os.environ.get("DDPX_GEMM", "pipe")
-# split-K on the 8-wave 256x128 tile for the M=512-row products (forward / dgrad).  Off by default:
-# on MI355X the partial-slab round trip (S x 8 MiB fp32) costs more than the larger tile saves for the
-# toy MLP (bench: 0.352 vs 0.295 ms/step, profiles/r1_gemm); DDPX_SPLITK=1 enables it.
-SPLITK = os.environ.get("DDPX_SPLITK", "0") == "1"
+# In-launch split-K for the M=512-row products (forward / dgrad): 128x128 tiles, K split over 2-4
+# workgroups whose fp32 partials are combined by the last split of each tile inside the same launch
+# (``csrc/include/ddpx_pipe.h``).  Planned by the native side; DDPX_SPLITK=0 turns it off there.
 
 EPI_F32 = 0
 EPI_BF16 = 1
@@ -60,31 +59,42 @@ def _check_bf16_2d(t, name):
     _req(t.data_ptr() % 16 == 0, f"{name} must be 16-byte aligned")
 
 
-def splitk_plan(M, N, K, a_kcontig, b_kcontig, tile=-1, impl=None, epi=None):
-    """(splits, scratch_floats, colsum_rows) — splits == 1 means the regular single-pass kernel."""
-    if not SPLITK or tile != -1 or (impl or GEMM_IMPL) != "pipe" or epi == EPI_SGD or N % 4:
-        return 1, 0, 0
+def plan(M, N, K, a_kcontig, b_kcontig, epi):
+    """(splits, cfg, slab_floats, tickets) of the default launch; splits > 1 = in-launch split-K."""
+    cfg = native.c_int(0)
     sf = native.c_int64(0)
-    rows = native.c_int(0)
-    s = native.kernels().ddpx_gemm_splitk_plan(M, N, K, int(a_kcontig), int(b_kcontig), native.ctypes.byref(sf),
-                                               native.ctypes.byref(rows))
-    return s, sf.value, rows.value
+    nt = native.c_int(0)
+    s = native.kernels().ddpx_gemm_pipe_plan(M, N, K, int(a_kcontig), int(b_kcontig), int(epi),
+                                             native.ctypes.byref(cfg), native.ctypes.byref(sf), native.ctypes.byref(nt))
+    return s, cfg.value, sf.value, nt.value
+
+
+_TICKETS: dict = {}
+
+
+def _tickets(dev, n):
+    """Per-device tile tickets of the in-launch split-K (zero between launches: each tile's last split
+    resets its own).  GEMMs on one device run in stream order, so one buffer serves every launch."""
+    t = _TICKETS.get(dev)
+    if t is None or t.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("split-K GEMM: first launch of this size must happen outside graph capture")
+        t = _TICKETS[dev] = torch.zeros((max(n, 4096),), dtype=torch.int32, device=dev)
+    return t
+
+
+def tile_dims(cfg):
+    bm, bn = native.c_int(0), native.c_int(0)
+    native.kernels().ddpx_gemm_tile_dims(int(cfg), native.ctypes.byref(bm), native.ctypes.byref(bn))
+    return bm.value, bn.value
 
 
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
-             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None):
+             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None, splits=None):
+    """``splits`` (with an explicit ``tile``): force the in-launch split-K on that tile config."""
     lib = native.kernels()
     impl = impl or GEMM_IMPL
     s = native.stream_handle(stream)
-    splits, sfl, _ = splitk_plan(M, N, K, a_kcontig, b_kcontig, tile, impl, epi) if sgd is None else (1, 0, 0)
-    if splits > 1 and ldc % 4 == 0:
-        scratch = torch.empty(sfl, dtype=torch.float32, device=a.device)
-        rc = lib.ddpx_gemm_pipe_splitk(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
-                                       native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig),
-                                       int(b_kcontig), epi, int(accumulate), float(alpha), splits, scratch.data_ptr(),
-                                       s)
-        native.check(rc, f"ddpx_gemm_pipe_splitk(M={M},N={N},K={K},epi={epi},splits={splits})")
-        return c
     if impl == "v1":
         if colsum is not None or sgd is not None:
             raise ValueError("v1 GEMM has no fused column sum / optimizer epilogue")
@@ -92,18 +102,32 @@ def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias
                                 lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate),
                                 float(alpha), tile, s)
     else:
+        slab, sf, tk = None, 0, None
+        nt = 0
+        if splits is not None and splits > 1:
+            _req(tile >= 0 and sgd is None, "forced split-K needs an explicit tile and no fused optimizer")
+            bm, bn = tile_dims(tile)
+            nt = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+            sf = splits * nt * bm * bn
+        else:
+            splits = 1
+            if tile < 0 and sgd is None:
+                splits, cfg, sf, nt = plan(M, N, K, a_kcontig, b_kcontig, epi)
+                if splits > 1:
+                    tile = cfg
+        if splits > 1:
+            slab = torch.empty(sf, dtype=torch.float32, device=a.device)
+            tk = _tickets(a.device, nt)
         rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
                                 native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
-                                int(accumulate), float(alpha), tile, *native.sgd_args(sgd), s)
+                                int(accumulate), float(alpha), tile, *native.sgd_args(sgd), splits, native.ptr(slab), sf,
+                                native.ptr(tk), s)
     native.check(rc, f"ddpx_gemm_{impl}(M={M},N={N},K={K},epi={epi})")
     return c
 
 
 def tiles_m(M, N, K, a_kcontig, b_kcontig, tile=-1):
     """Rows of per-tile column-sum partials the kernel chosen for this shape writes."""
-    splits, _, rows = splitk_plan(M, N, K, a_kcontig, b_kcontig, tile)
-    if splits > 1:
-        return rows
     return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, K, int(a_kcontig), int(b_kcontig), tile)
 
 
@@ -115,7 +139,7 @@ def reduce_partials(part, T, N, out, accumulate=False, sgd=None):
     return out
 
 
-def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, tile=-1):
+def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, tile=-1, splits=None):
     """Y = act(X Wᵀ + b).  X [M,K] bf16, W [N,K] bf16, b [N] fp32."""
     _check_bf16_2d(x, "x")
     _check_bf16_2d(w, "w")
@@ -136,11 +160,11 @@ def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, 
     _req(tuple(out.shape) == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0
          and out.data_ptr() % 16 == 0 and out.dtype == _OUT_DTYPE[epi], "bad out tensor")
     return gemm_raw(x, w, out, M=M, N=N, K=K, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), a_kcontig=True,
-                    b_kcontig=True, epi=epi, bias=bias, tile=tile)
+                    b_kcontig=True, epi=epi, bias=bias, tile=tile, splits=splits)
 
 
 def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bias_grad_accumulate=False,
-                 bias_sgd=None):
+                 bias_sgd=None, splits=None):
     """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below.
 
     ``bias_grad`` ([K] fp32 or bf16): also produce Σ_m dX[m, :] — the bias gradient of the layer that
@@ -169,7 +193,7 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
     gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
              b_kcontig=False, epi=epi, aux=relu_mask_of,
              ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
-             impl=None if part is None else "pipe")
+             impl=None if part is None else "pipe", splits=splits)
     if part is not None:
         reduce_partials(part, part.shape[0], K, bias_grad, accumulate=bias_grad_accumulate, sgd=bias_sgd)
     return out

@@ -43,18 +43,31 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
     dev = h.device
     logits = torch.empty((M, C), dtype=torch.float32, device=dev) if want_logits else None
     have_t = targets is not None
-    # M <= 8192: logits, loss rows, dlogits and the mean loss come out of one finalize launch
-    loss_rows = torch.empty((M,), dtype=torch.float32, device=dev) if (have_t and M > 8192) else None
     dl = torch.empty((M, C), dtype=torch.float32, device=dev) if (want_grad and have_t) else None
     loss = torch.empty((), dtype=torch.float32, device=dev) if have_t else None
     lib = native.kernels()
+    # slice partials of the logits + row losses of the batch mean (combined in-launch by last arrivers)
     scratch = torch.empty((int(lib.ddpx_head_fwd_scratch(M, K)),), dtype=torch.float32, device=dev)
-    s = native.stream_handle()
     rc = lib.ddpx_head_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, C, h.stride(0),
-                           1.0 / M, native.ptr(logits), native.ptr(loss_rows), native.ptr(dl), native.ptr(correct),
-                           scratch.data_ptr(), native.ptr(loss), s)
+                           1.0 / M, native.ptr(logits), native.ptr(dl), native.ptr(correct), scratch.data_ptr(),
+                           _tickets(dev, int(lib.ddpx_head_fwd_tickets(M))).data_ptr(), native.ptr(loss),
+                           native.stream_handle())
     native.check(rc, "ddpx_head_fwd")
     return loss, logits, dl
+
+
+_TICKETS: dict = {}
+
+
+def _tickets(dev, n):
+    """Per-device arrival counters of the forward's in-launch reductions: zero between launches (each last
+    arriver resets its counter).  Head forwards on one device are ordered on its compute stream."""
+    t = _TICKETS.get(dev)
+    if t is None or t.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("head_forward: first call for this batch size must happen outside graph capture")
+        t = _TICKETS[dev] = torch.zeros((max(n, 1025),), dtype=torch.int32, device=dev)
+    return t
 
 
 def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_mask=True, accumulate=False,
@@ -91,10 +104,12 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
                 dbprev.add_(s) if accumulate else dbprev.copy_(s)
         return dH
     _check(h, w, None, None)
-    if K % 64:
-        raise ValueError("head_backward: K must be a multiple of 64")
+    if K % 32:
+        raise ValueError("head_backward: K must be a multiple of 32")
     if dH is not None and (dH.shape != h.shape or dH.dtype != torch.bfloat16 or dH.stride(0) != h.stride(0)):
         raise ValueError("head_backward: dH must match h")
+    if dlogits.dtype != torch.float32 or not dlogits.is_contiguous() or tuple(dlogits.shape) != (M, C):
+        raise ValueError("head_backward: dlogits must be contiguous fp32 [M, C]")
     fused = sgd_w is not None
     if fused:
         if sgd_b is None or (dbprev is not None) or sgd_w[0].numel() != C * K or sgd_b[0].numel() != C:
@@ -110,18 +125,14 @@ def head_backward(dlogits, grad_out, h, w, dW, db, dH=None, dbprev=None, relu_ma
     go = grad_out if torch.is_tensor(grad_out) else None
     if go is not None:
         go = go.to(torch.float32).contiguous()
-    scratch = torch.empty((int(lib.ddpx_head_bwd_scratch(M, K, C)),), dtype=torch.float32, device=h.device)
     sw, sb, sp = (native.sgd_args(x) for x in (sgd_w, sgd_b, sgd_prev))
     lr_ptr = sw[3] if fused else None
     mom, wd = (sw[4], sw[5]) if fused else (0.0, 0.0)
-    rc = lib.ddpx_head_bwd_partial(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C,
-                                   h.stride(0), native.ptr(dH), int(relu_mask), float(dh_scale), scratch.data_ptr(),
-                                   native.stream_handle())
-    native.check(rc, "ddpx_head_bwd_partial")
-    rc = lib.ddpx_head_bwd_finalize(M, K, C, native.ptr(dW), native.ptr(db), native.ptr(dbprev),
-                                    int(gdt == torch.bfloat16), int(accumulate), scratch.data_ptr(), *sw[:3], *sb[:3],
-                                    *sp[:3], lr_ptr, mom, wd, native.stream_handle())
-    native.check(rc, "ddpx_head_bwd_finalize")
+    rc = lib.ddpx_head_bwd(dlogits.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, C, h.stride(0),
+                           native.ptr(dH), int(relu_mask), float(dh_scale), native.ptr(dW), native.ptr(db),
+                           native.ptr(dbprev), int(gdt == torch.bfloat16), int(accumulate), *sw[:3], *sb[:3], *sp[:3],
+                           lr_ptr, mom, wd, native.stream_handle())
+    native.check(rc, "ddpx_head_bwd")
     return dH
 
 
