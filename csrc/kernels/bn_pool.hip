@@ -61,7 +61,8 @@ __global__ void __launch_bounds__(256)
 finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, const float* __restrict__ gamma,
                 const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
                 int64_t* __restrict__ nbt, float momentum, float eps, int training, float* __restrict__ a_out,
-                float* __restrict__ b_out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+                float* __restrict__ b_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                float* __restrict__ merged_out) {
   __shared__ float wres[4][3];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = blockIdx.x;
@@ -88,6 +89,11 @@ finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, co
     if (tid != 0) return;
     n = wres[0][0]; mu = wres[0][1]; m2 = wres[0][2];
     for (int q = 1; q < 4; ++q) chan_merge(n, mu, m2, wres[q][0], wres[q][1], wres[q][2]);
+    if (merged_out) {  // SyncBN: this rank's (mean, M2) in the tile-stats layout [2][C]; merged across ranks next
+      merged_out[c] = mu;
+      merged_out[C + c] = m2;
+      return;
+    }
     mean = mu;
     var = m2 / (float)M;  // biased, for normalisation
     const float unbiased = M > 1 ? m2 / (float)(M - 1) : m2;
@@ -447,7 +453,18 @@ DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, c
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
                               float* a, float* b, float* mean, float* rstd, hipStream_t s) {
   hipLaunchKernelGGL(bn::finalize_kernel, dim3(C), dim3(256), 0, s, stats, T, BM, M, C, gamma, beta, rmean,
-                     rvar, nbt, momentum, eps, training, a, b, mean, rstd);
+                     rvar, nbt, momentum, eps, training, a, b, mean, rstd, (float*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// SyncBatchNorm, forward: this rank's per-channel (mean, M2) over its M rows, merged from the conv
+// epilogue's tile statistics, written as ONE tile [2][C].  The ranks' tiles are all-gathered into
+// [ws][2][C] and ddpx_bn_finalize(gathered, T = ws, BM = M, M = ws * M) merges them in rank order — the
+// same Chan merge on every rank, so every rank normalises with bitwise-identical statistics.
+DDPX_API int ddpx_bn_local_stats(const float* stats, int T, int BM, int M, int C, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(bn::finalize_kernel, dim3(C), dim3(256), 0, s, stats, T, BM, M, C, (const float*)nullptr,
+                     (const float*)nullptr, (float*)nullptr, (float*)nullptr, (int64_t*)nullptr, 0.f, 0.f, 1,
+                     (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, out);
   return (int)hipGetLastError();
 }
 
@@ -491,6 +508,33 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
 // no BatchNorm: the reference's DeepNN blocks (/root/reference/singlegpu.py:21-31).  Same two
 // passes as BatchNorm with a = 1, b = bias, mean = 0, rstd = 1: pass 1 yields dbias = sum gz
 // (fixed-order, deterministic), pass 2 writes dy = gz for the conv dgrad / wgrad GEMMs.
+// SyncBatchNorm, backward in two halves around an all-reduce of sums[2][C] = (sum dy, sum dy*xhat):
+// ddpx_bn_bwd_sums stores this rank's sums and the LOCAL dgamma / dbeta (DDP averages those, as torch's
+// SyncBatchNorm does); after the all-reduce and a 1/M_global scale, ddpx_bn_bwd_apply forms dy.
+DDPX_API int ddpx_bn_bwd_sums(const void* gout, const void* y, const float* a, const float* b, const float* mean,
+                              const float* rstd, int N, int H, int W, int C, int pool, int relu, float* part,
+                              float* sums, void* dgamma, void* dbeta, int out_bf16, int accumulate, hipStream_t s) {
+  if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
+  const int B = ddpx_bn_bwd_blocks(N, H, W, C);
+  hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
+  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, 1, sums, sums + C,
+                     dgamma, dbeta, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                     SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_bn_bwd_apply(const void* gout, const void* y, const float* a, const float* b, const float* mean,
+                               const float* rstd, const float* c1, const float* c2, int N, int H, int W, int C,
+                               int pool, int relu, void* dy, hipStream_t s) {
+  if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
+  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
+  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu, 1,
+                     (unsigned short*)dy);
+  return (int)hipGetLastError();
+}
+
 DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bias, const float* ones,
                                const float* zeros, int N, int H, int W, int C, int pool, int relu, float* part,
                                float* c1, float* c2, void* dbias, int out_bf16, int accumulate, void* dy,

@@ -94,6 +94,49 @@ def bn_finalize(stats, T, BM, M, bn_mod, training, a, b, mean, rstd):
                                       rstd.data_ptr(), native.stream_handle()), "ddpx_bn_finalize")
 
 
+def bn_finalize_sync(stats, T, BM, M, bn_mod, a, b, mean, rstd, comm):
+    """SyncBatchNorm forward statistics (training): this rank's (mean, M2) from the tile statistics, one
+    all-gather of [2][C] per rank on the current stream (RCCL: graph-capturable), then the rank-ordered
+    Chan merge + running-stat update + affine coefficients in ``ddpx_bn_finalize``.  Every rank must hold
+    the same number of rows M (equal DistributedSampler shards)."""
+    C = bn_mod.num_features
+    lib = native.kernels()
+    dev = a.device
+    local = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    native.check(lib.ddpx_bn_local_stats(stats.data_ptr(), T, BM, M, C, local.data_ptr(), native.stream_handle()),
+                 "ddpx_bn_local_stats")
+    ws = comm.world_size
+    gathered = torch.empty(ws * 2 * C, dtype=torch.float32, device=dev)
+    comm.allgather(gathered, local)
+    bn_finalize(gathered, ws, M, ws * M, bn_mod, True, a, b, mean, rstd)
+
+
+def bn_backward_sync(gout, y, a, b, mean, rstd, N, H, W, C, pool, comm, dgamma=None, dbeta=None,
+                     accumulate=False):
+    """SyncBatchNorm backward: local (sum dy, sum dy*xhat) -> all-reduce -> dy with the global means;
+    dgamma / dbeta stay local (DDP averages them, as torch's SyncBatchNorm)."""
+    _nhwc(gout, "gout", C)
+    _nhwc(y, "y", C)
+    lib = native.kernels()
+    dev = y.device
+    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
+    part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
+    sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    gdt = dgamma.dtype if dgamma is not None else torch.float32
+    s = native.stream_handle()
+    native.check(lib.ddpx_bn_bwd_sums(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                      rstd.data_ptr(), N, H, W, C, int(pool), 1, part.data_ptr(), sums.data_ptr(),
+                                      native.ptr(dgamma), native.ptr(dbeta), int(gdt == torch.bfloat16),
+                                      int(accumulate), s), "ddpx_bn_bwd_sums")
+    comm.allreduce_(sums, op="sum")
+    native.check(lib.ddpx_scale_f32(sums.data_ptr(), 2 * C, 1.0 / (comm.world_size * N * H * W), s), "ddpx_scale_f32")
+    dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)
+    native.check(lib.ddpx_bn_bwd_apply(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                       rstd.data_ptr(), sums.data_ptr(), sums[C:].data_ptr(), N, H, W, C, int(pool),
+                                       1, dy.data_ptr(), s), "ddpx_bn_bwd_apply")
+    return dy
+
+
 def bn_apply(y, a, b, N, H, W, C, relu=True, pool=False):
     _nhwc(y, "y", C)
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)

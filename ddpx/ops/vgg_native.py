@@ -10,6 +10,10 @@ Per conv block (``/root/reference/singlegpu.py:60-70``):
               g   = dgrad(dy, W)                 (skipped for the first block)
 
 then ``x.mean([2,3])`` (global average pool) and the classifier + cross-entropy on the fused head.
+``model.sync_bn_comm`` (native SyncBatchNorm, ``--sync_bn``; reference: the commented-out
+``convert_sync_batchnorm`` at ``/root/reference/multigpu.py:127``) merges the BatchNorm statistics across
+ranks: an all-gather of each rank's [2][C] (mean, M2) in the forward, an all-reduce of (Σdy, Σdy·x̂) in the
+backward, both on the compute stream between the same native kernels.
 Weight gradients land straight in the DDP bucket storage (grad-ready order: classifier, bn7, conv7,
 ..., as torch DDP's rebuilt buckets) or — single process with ``SGD(fused_backward=True)`` — are
 applied in the reduce kernels without ever being stored.  The forward reads bf16 copies of the conv
@@ -49,6 +53,15 @@ class _Plan:
             self.wd.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
 
 
+def _sync_comm(model, training):
+    """The communicator of native SyncBatchNorm (``--sync_bn`` under DDP), or None: batch statistics are
+    then merged across ranks inside the forward and the backward (``ops/conv.py`` bn_*_sync)."""
+    comm = getattr(model, "sync_bn_comm", None)
+    if training and comm is not None and comm.world_size > 1:
+        return comm
+    return None
+
+
 def plan_of(model):
     p = getattr(model, "_ddpx_plan", None)
     if p is None:
@@ -71,7 +84,11 @@ def _forward(model, x, targets, want_logits, want_grad, training):
         b = torch.empty_like(a)
         mean = torch.empty_like(a)
         rstd = torch.empty_like(a)
-        K.bn_finalize(st, T, BM, N * H * W, bn, training, a, b, mean, rstd)
+        comm = _sync_comm(model, training)
+        if comm is not None:
+            K.bn_finalize_sync(st, T, BM, N * H * W, bn, a, b, mean, rstd, comm)
+        else:
+            K.bn_finalize(st, T, BM, N * H * W, bn, training, a, b, mean, rstd)
         xn = K.bn_apply(y, a, b, N, H, W, Co, relu=True, pool=pool)
         saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
         x = xn
@@ -107,7 +124,17 @@ def _backward(model, saved, last, dl, grad_out):
         conv, bn, pool = plan.blocks[bi]
         x, y, a, b, mean, rstd, (N, H, W, C, Co), _ = saved[bi]
         sg, sbeta = flat.fused_spec(bn.weight), flat.fused_spec(bn.bias)
-        if sg is not None:
+        comm = _sync_comm(model, True)
+        if comm is not None:
+            if sg is not None:
+                raise RuntimeError("SyncBatchNorm runs under DDP; the fused single-process optimizer does not apply")
+            dgam, accg = flat.grad_target(bn.weight)
+            dbet, _ = flat.grad_target(bn.bias)
+            dy = K.bn_backward_sync(g, y, a, b, mean, rstd, N, H, W, Co, pool, comm, dgamma=dgam, dbeta=dbet,
+                                    accumulate=accg)
+            flat.grad_done(bn.weight)
+            flat.grad_done(bn.bias)
+        elif sg is not None:
             dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, sgd_gamma=sg, sgd_beta=sbeta)
             flat.mark_updated(bn.weight)
             flat.mark_updated(bn.bias)

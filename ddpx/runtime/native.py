@@ -79,6 +79,9 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_bn_finalize", I, P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P)
     _sig(lib, "ddpx_bn_apply", I, P, P, P, I, I, I, I, I, I, P, P)
+    _sig(lib, "ddpx_bn_local_stats", I, P, I, I, I, I, P, P)
+    _sig(lib, "ddpx_bn_bwd_sums", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P)
+    _sig(lib, "ddpx_bn_bwd_apply", I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P)
     _sig(lib, "ddpx_bn_bwd_blocks", I, I, I, I, I)
     _sig(lib, "ddpx_bn_bwd", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_bias_act_bwd", I, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P)

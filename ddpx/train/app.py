@@ -179,8 +179,9 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
     every argument defaults from :func:`current_config` (device: the first GPU, else the CPU).
 
     ``--sync_bn`` (reference: the commented-out ``convert_sync_batchnorm`` at
-    ``/root/reference/multigpu.py:127``) swaps every BatchNorm2d for :class:`SyncBatchNorm2d` on ``comm``
-    before the flat parameter store is built; the VGG then runs on the torch-op path.
+    ``/root/reference/multigpu.py:127``): the native VGG merges BatchNorm statistics across ranks inside its
+    own kernels' sequence (``model.sync_bn_comm``); the torch-op path swaps every BatchNorm2d for
+    :class:`SyncBatchNorm2d` on ``comm`` before the flat parameter store is built.
     """
     if args is None:
         args = current_config()
@@ -197,9 +198,11 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels, fp8=getattr(args, "fp8", False))
     if getattr(args, "sync_bn", False) and distributed:
-        if hasattr(model, "use_native"):
-            model.use_native = False
-        model = convert_sync_batchnorm(model, comm)
+        if getattr(model, "use_native", False) and device.type == "cuda":
+            # native path: the BN kernels merge statistics across ranks themselves (ops/vgg_native.py)
+            model.sync_bn_comm = comm
+        else:
+            model = convert_sync_batchnorm(model, comm)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"),

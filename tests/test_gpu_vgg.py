@@ -160,3 +160,48 @@ def test_vgg_fused_optimizer_bitwise(gpu):
             o.step()
     for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
         assert torch.equal(p, q), n
+
+
+class _MirrorComm:
+    """A 2-rank communicator whose other rank holds exactly this rank's data: SyncBatchNorm over it must
+    reproduce plain BatchNorm on the local batch (global statistics == local ones)."""
+    world_size = 2
+    rank = 0
+
+    def allgather(self, out, inp, stream=None):
+        out.view(2, -1).copy_(inp.view(1, -1).expand(2, -1))
+
+    def allreduce_(self, t, op="sum", stream=None, async_op=False):
+        assert op == "sum"
+        t.mul_(2.0)
+
+
+def test_native_sync_batchnorm_kernels_match_local_bn(gpu):
+    """Native SyncBN forward (local stats -> all-gather -> rank-ordered merge) and backward (sums ->
+    all-reduce -> apply) against the plain native BN on the same batch, through a mirror communicator."""
+    import ddpx
+    from ddpx.models import VGG
+    torch.manual_seed(3)
+    a, b = VGG(), VGG()
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        m.use_native = True
+        ddpx.prepare_model(m, gpu)
+    b.sync_bn_comm = _MirrorComm()
+    x = torch.rand(24, 32, 32, 8, device=gpu)
+    x[..., 3:] = 0
+    x = x.to(torch.bfloat16)
+    t = torch.randint(0, 10, (24,), device=gpu)
+    la, _ = a.forward_loss(x, t)
+    lb, _ = b.forward_loss(x, t)
+    assert abs(la.item() - lb.item()) < 1e-4 * max(1.0, abs(la.item()))
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        if ba.is_floating_point():
+            assert torch.allclose(ba, bb, rtol=1e-4, atol=1e-6), n
+    la.backward()
+    lb.backward()
+    # the sync path divides (2 x local sums) by 2M instead of local sums by M: the same values up to
+    # fp32 rounding, which can flip bf16 roundings of dy; 8 layers deep that stays under 2 %
+    bad = [(n, _rel(q.main_grad, p.main_grad)) for (n, p), q in zip(a.named_parameters(), b.parameters())
+           if _rel(q.main_grad, p.main_grad) > 2e-2]
+    assert not bad, bad
