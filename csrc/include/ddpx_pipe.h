@@ -107,6 +107,13 @@ struct Params {
   float* slab;
   unsigned slab_bytes;
   int* tcnt;               // per-tile tickets, zero between launches (the last arriver resets its own)
+  // Column sums finished in-launch (the dgrad epilogue's bias gradient of the layer below): with cs_tcnt
+  // set, every row tile writes its partial column sums write-through and takes its column tile's ticket;
+  // the last row tile sums all partials in row-tile order and stores cs_out (fp32 / bf16, cs_flags bit 0;
+  // accumulate, bit 1) or, with sgd.p set, applies them as an SGD update of that parameter.
+  void* cs_out;
+  int cs_flags;
+  int* cs_tcnt;
 };
 
 constexpr unsigned kOOB = 0x80000000u;
@@ -628,7 +635,46 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   // ---- per-tile column sums (bias gradient) ----
   __syncthreads();
   quad_colsum<BN, NT>(red, cs, tid, colres);
-  if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
+  if (NW != 4 || !p.cs_tcnt) {  // (the in-launch finish is built for the 4-wave tiles only: it adds
+                                // spills to the register-bound 8-wave ones, which no dgrad picks)
+    if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
+    return;
+  }
+  // in-launch finish (MI355X_MICROARCH.md "Valid forms", row 1): sc1 partials, drained, then the column
+  // tile's ticket; the last row tile reads every partial with sc1 loads, in row-tile order
+  if (tid < BN && n0 + tid < p.N)
+    __hip_atomic_store(p.colsum + (size_t)tm * p.N + n0 + tid, colres[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* csflag = reinterpret_cast<int*>(colres + BN);
+  if (tid == 0)
+    *csflag = __hip_atomic_fetch_add(p.cs_tcnt + tn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tiles_m - 1;
+  __syncthreads();
+  if (!*csflag) return;
+  if (tid == 0) __hip_atomic_store(p.cs_tcnt + tn, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid >= BN || n0 + tid >= p.N) return;
+  const __amdgpu_buffer_rsrc_t rcs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.colsum, 0, (unsigned)((size_t)tiles_m * p.N * 4), 0x00020000);
+  float tot = 0.f;
+  for (int t0 = 0; t0 < tiles_m; t0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)  // all in flight together; rows past tiles_m read zeros (bounds check)
+      v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rcs, (unsigned)(((size_t)(t0 + q) * p.N + n0 + tid) * 4), 0, 16 /* sc1 */));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tot += v[q];
+  }
+  const int n = n0 + tid;
+  if (p.sgd.p) {
+    sgd_apply(p.sgd, n, tot, *p.sgd.lr);
+  } else if (p.cs_flags & 1) {
+    unsigned short* o = reinterpret_cast<unsigned short*>(p.cs_out) + n;
+    *o = f2bf((p.cs_flags & 2) ? tot + bf2f(*o) : tot);
+  } else {
+    float* o = reinterpret_cast<float*>(p.cs_out) + n;
+    *o = (p.cs_flags & 2) ? tot + *o : tot;
+  }
 }
 
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,

@@ -31,25 +31,6 @@
 namespace ddpx {
 namespace pipe {
 
-// out[n] (=|+=) sum_t partial[t][n]   (fixed order: deterministic)
-__global__ void __launch_bounds__(256) reduce_partials_kernel(const float* __restrict__ part, int T, int N,
-                                                              float* __restrict__ out, int out_bf16, int accumulate,
-                                                              SgdArgs sgd) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int t = 0; t < T; ++t) s += part[(size_t)t * N + n];
-  if (sgd.p) {
-    sgd_apply(sgd, n, s, *sgd.lr);
-  } else if (out_bf16) {
-    unsigned short* o = reinterpret_cast<unsigned short*>(out);
-    if (accumulate) s += bf2f(o[n]);
-    o[n] = f2bf(s);
-  } else {
-    out[n] = accumulate ? out[n] + s : s;
-  }
-}
-
 // Default tile per operand-layout class, from the MI355X sweep of the MLP shapes
 // (benchmarks/mlp_gemm_bench.py, benchmarks/sgd_bw.py; profiles/r1_gemm2): the M=512-row products
 // want 64x64 tiles with 128-wide K stages (fwd 27.1 vs 29.1 us, dgrad 36.5 vs 45.1 us at H=4096),
@@ -130,7 +111,8 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
                             int M, int N, int K, int lda, int ldb, int ldc, int ldaux, int a_kcontig, int b_kcontig,
                             int epi, int accumulate, float alpha, int tile_cfg, float* sgd_p, float* sgd_buf,
                             void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd, int splits,
-                            float* slab, long long slab_floats, int* tcnt, hipStream_t stream) {
+                            float* slab, long long slab_floats, int* tcnt, void* cs_out, int cs_flags,
+                            int* cs_tcnt, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (a_kcontig ? (K % 8 || lda % 8) : (M % 8 || lda % 8)) return -1;
   if (b_kcontig ? (K % 8 || ldb % 8) : (N % 8 || ldb % 8)) return -2;
@@ -141,7 +123,10 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   pipe::Params p{(const unsigned short*)A, (const unsigned short*)B, C, bias, (const unsigned short*)aux, colsum,
                  M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes,
                  SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
-                 pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr};
+                 pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr, cs_out, cs_flags, cs_tcnt};
+  if (cs_tcnt && (!colsum || epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || (!cs_out && !sgd_p) ||
+                  (sgd_p && !sgd_lr)))
+    return -10;
   if (epi == pipe::EPI_SGD && (!sgd_p || !sgd_lr || (sgd_mom != 0.f && !sgd_buf))) return -5;
   static const int sgd_plain = [] {
     const char* e = getenv("DDPX_SGD_PLAIN");
@@ -149,6 +134,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   p.sgd_plain = sgd_plain;
   int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
+  if (cs_tcnt && (cfg == 8 || cfg >= 13)) return -11;  // in-launch column sums: 4-wave tiles only
   if (splits > 1) {  // in-launch split-K (ddpx_gemm_pipe_plan): the caller's cfg, slab and zeroed tickets
     if (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || !slab || !tcnt || tile_cfg < 0 || !a_kcontig)
       return -7;
@@ -195,13 +181,4 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   else if (b_kcontig) e = pipe::dispatch<false, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
   else e = pipe::dispatch<false, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
   return (int)e;
-}
-
-DDPX_API int ddpx_reduce_partials(const float* part, int T, int N, void* out, int out_bf16, int accumulate,
-                                  float* sgd_p, float* sgd_buf, void* sgd_shadow, const float* sgd_lr, float sgd_mom,
-                                  float sgd_wd, hipStream_t s) {
-  if (N <= 0) return 0;
-  hipLaunchKernelGGL(pipe::reduce_partials_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, T, N, (float*)out,
-                     out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
-  return (int)hipGetLastError();
 }

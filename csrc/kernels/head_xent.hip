@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(256)
 head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __restrict__ W,
                 const float* __restrict__ b, const int64_t* __restrict__ tgt, int M, int K, int C, int ldh, int KS,
                 int kslice, float inv_m, float* __restrict__ logits, float* __restrict__ dlogits,
-                int* __restrict__ correct, float* part, float* loss_rows, int* tickets, float* __restrict__ loss_mean) {
+                int* __restrict__ correct, float* part, float* loss_rows, int* tickets, float* __restrict__ loss_mean,
+                const float* __restrict__ lr_table, int lr_n, int* __restrict__ lr_counter, float* __restrict__ lr_out) {
   // one LDS object (cdna_hip_programming §5 item 4a): [4 waves][16][17] partials + [16][17] sums + flags
   __shared__ float lds[4 * 16 * 17 + 16 * 17 + 4];
   float* zs = lds + 4 * 16 * 17;
@@ -171,6 +172,14 @@ head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __re
   if (lane == 0) {
     *loss_mean = s / (float)M;
     __hip_atomic_store(tickets + nrb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lr_counter) {
+      // the training step's device LR schedule (SGD.device_lr_step): lr = table[step], step += 1.  Every
+      // reader of the step counter (the batch gather) ran in an earlier kernel and every reader of lr (the
+      // optimizer) runs in a later one, so this single thread saves the step its own 1-thread launch.
+      const int k = *lr_counter;
+      *lr_out = lr_table[k < lr_n ? k : lr_n - 1];
+      *lr_counter = k + 1;
+    }
   }
 }
 
@@ -384,14 +393,17 @@ DDPX_API int64_t ddpx_head_fwd_scratch(int M, int K) {
 }
 DDPX_API int64_t ddpx_head_fwd_tickets(int M) { return (M + 15) / 16 + 1; }
 
+// lr_table / lr_counter / lr_out (optional, with loss_mean): advance the device LR schedule in the launch.
 DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const int64_t* tgt, int M, int K, int C,
                            int ldh, float inv_m, float* logits, float* dlogits, int* correct, float* scratch,
-                           int* tickets, float* loss_mean, hipStream_t s) {
+                           int* tickets, float* loss_mean, const float* lr_table, int lr_n, int* lr_counter,
+                           float* lr_out, hipStream_t s) {
   if (M <= 0) return 0;
   if (C < 1 || C > kHeadC) return -1;
   if (K % 8 || ldh % 8) return -2;
   if (!scratch || !tickets) return -3;
   if (loss_mean && !tgt) return -4;
+  if (lr_counter && (!loss_mean || !lr_table || !lr_out || lr_n < 1)) return -5;
   const int rbs = (M + 15) / 16;
   const int ks = head_ksplit(M, K);
   int kslice = (K + ks - 1) / ks;
@@ -400,7 +412,7 @@ DDPX_API int ddpx_head_fwd(const void* H, const void* W, const float* b, const i
   float* loss_rows = scratch + (size_t)rbs * ks * 256;
   hipLaunchKernelGGL(head_fwd_kernel, dim3(rbs * ks), dim3(256), 0, s, (const unsigned short*)H,
                      (const unsigned short*)W, b, tgt, M, K, C, ldh, ks, kslice, inv_m, logits, dlogits, correct, part,
-                     loss_rows, tickets, loss_mean);
+                     loss_rows, tickets, loss_mean, lr_table, lr_n, lr_counter, lr_out);
   return (int)hipGetLastError();
 }
 

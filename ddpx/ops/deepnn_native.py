@@ -30,6 +30,7 @@ from torch import nn
 
 from . import conv as K
 from . import gemm as G
+from ..optim.sgd import take_lr_advance
 from .head import head_backward, head_forward
 from .vgg_native import _prep_input
 from ..runtime import native
@@ -127,7 +128,8 @@ def _forward(model, x, targets, want_logits, want_grad, training):
     drop = training and p > 0.0
     d0 = dropout_(a0, p, plan) if drop else a0
     loss, logits, dl = head_forward(d0, flat.shadow_of(plan.lin1.weight), plan.lin1.bias, targets,
-                                    want_logits=want_logits, want_grad=want_grad)
+                                    want_logits=want_logits, want_grad=want_grad,
+                                    lr_advance=take_lr_advance(flat) if want_grad else None)
     scale = 1.0 / (1.0 - p) if drop else 1.0
     return saved, (x.shape, feat, d0, scale), loss, logits, dl
 

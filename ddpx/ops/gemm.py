@@ -70,16 +70,18 @@ def plan(M, N, K, a_kcontig, b_kcontig, epi):
 
 
 _TICKETS: dict = {}
+_CS_TICKETS: dict = {}
 
 
-def _tickets(dev, n):
-    """Per-device tile tickets of the in-launch split-K (zero between launches: each tile's last split
-    resets its own).  GEMMs on one device run in stream order, so one buffer serves every launch."""
-    t = _TICKETS.get(dev)
+def _tickets(dev, n, pool=None):
+    """Per-device tile tickets of the in-launch combines (zero between launches: each last arriver resets
+    its own).  GEMMs on one device run in stream order, so one buffer per kind serves every launch."""
+    pool = _TICKETS if pool is None else pool
+    t = pool.get(dev)
     if t is None or t.numel() < n:
         if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("split-K GEMM: first launch of this size must happen outside graph capture")
-        t = _TICKETS[dev] = torch.zeros((max(n, 4096),), dtype=torch.int32, device=dev)
+            raise RuntimeError("GEMM tickets: first launch of this size must happen outside graph capture")
+        t = pool[dev] = torch.zeros((max(n, 4096),), dtype=torch.int32, device=dev)
     return t
 
 
@@ -90,8 +92,13 @@ def tile_dims(cfg):
 
 
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
-             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None, splits=None):
-    """``splits`` (with an explicit ``tile``): force the in-launch split-K on that tile config."""
+             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None, splits=None,
+             cs_out=None, cs_accumulate=False, cs_sgd=None):
+    """``splits`` (with an explicit ``tile``): force the in-launch split-K on that tile config.
+
+    ``colsum`` ([tiles_m, N] fp32 scratch) with ``cs_out`` (fp32 / bf16 [N]) or ``cs_sgd``: the column
+    sums of the stored output are finished inside the launch (the last row tile of each column tile adds
+    the partials in order) and stored / accumulated into ``cs_out`` or applied as an SGD update."""
     lib = native.kernels()
     impl = impl or GEMM_IMPL
     s = native.stream_handle(stream)
@@ -118,10 +125,16 @@ def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias
         if splits > 1:
             slab = torch.empty(sf, dtype=torch.float32, device=a.device)
             tk = _tickets(a.device, nt)
+        cs_t, cs_flags = None, 0
+        if cs_out is not None or cs_sgd is not None:
+            _req(colsum is not None and sgd is None, "in-launch column sums need the colsum scratch, no EPI_SGD")
+            cs_t = _tickets(a.device, N, pool=_CS_TICKETS)
+            cs_flags = int(cs_out is not None and cs_out.dtype == torch.bfloat16) | (2 if cs_accumulate else 0)
+            sgd = cs_sgd  # the bias SGD rides on the (otherwise unused) optimizer arguments
         rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
                                 native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
                                 int(accumulate), float(alpha), tile, *native.sgd_args(sgd), splits, native.ptr(slab), sf,
-                                native.ptr(tk), s)
+                                native.ptr(tk), native.ptr(cs_out), cs_flags, native.ptr(cs_t), s)
     native.check(rc, f"ddpx_gemm_{impl}(M={M},N={N},K={K},epi={epi})")
     return c
 
@@ -129,14 +142,6 @@ def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias
 def tiles_m(M, N, K, a_kcontig, b_kcontig, tile=-1):
     """Rows of per-tile column-sum partials the kernel chosen for this shape writes."""
     return native.kernels().ddpx_gemm_pipe_tiles_m(M, N, K, int(a_kcontig), int(b_kcontig), tile)
-
-
-def reduce_partials(part, T, N, out, accumulate=False, sgd=None):
-    lib = native.kernels()
-    native.check(lib.ddpx_reduce_partials(part.data_ptr(), T, N, native.ptr(out),
-                                          int(out is not None and out.dtype == torch.bfloat16), int(accumulate),
-                                          *native.sgd_args(sgd), native.stream_handle()), "ddpx_reduce_partials")
-    return out
 
 
 def linear_fwd(x, w, bias=None, relu=False, out=None, out_dtype=torch.bfloat16, tile=-1, splits=None):
@@ -168,7 +173,8 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
     """dX = dY W (bf16), optionally times (relu_mask_of > 0) — the ReLU backward of the layer below.
 
     ``bias_grad`` ([K] fp32 or bf16): also produce Σ_m dX[m, :] — the bias gradient of the layer that
-    produced ``relu_mask_of`` — from per-tile column sums in the GEMM epilogue plus a fixed-order reduce.
+    produced ``relu_mask_of`` — from per-tile column sums in the GEMM epilogue, summed in row-tile order
+    by the last row tile of each column tile in the same launch (``bias_sgd``: applied as an SGD update).
     """
     _check_bf16_2d(dy, "dy")
     _check_bf16_2d(w, "w")
@@ -193,9 +199,8 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
     gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
              b_kcontig=False, epi=epi, aux=relu_mask_of,
              ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
-             impl=None if part is None else "pipe", splits=splits)
-    if part is not None:
-        reduce_partials(part, part.shape[0], K, bias_grad, accumulate=bias_grad_accumulate, sgd=bias_sgd)
+             impl=None if part is None else "pipe", splits=splits, cs_out=bias_grad,
+             cs_accumulate=bias_grad_accumulate, cs_sgd=bias_sgd)
     return out
 
 

@@ -26,8 +26,11 @@ def _check(h, w, b, targets):
         raise ValueError("head: targets must be int64 [M]")
 
 
-def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correct=None):
-    """Returns (loss 0-d fp32 | None, logits [M,C] fp32 | None, dlogits [M,C] fp32 | None)."""
+def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correct=None, lr_advance=None):
+    """Returns (loss 0-d fp32 | None, logits [M,C] fp32 | None, dlogits [M,C] fp32 | None).
+
+    ``lr_advance`` ((table, counter, lr) device tensors, from ``ddpx.optim.sgd.take_lr_advance``): the
+    same launch also advances the training step's device LR schedule (lr = table[step]; step += 1)."""
     M, K = h.shape
     C = w.shape[0]
     if not h.is_cuda:
@@ -48,10 +51,12 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
     lib = native.kernels()
     # slice partials of the logits + row losses of the batch mean (combined in-launch by last arrivers)
     scratch = torch.empty((int(lib.ddpx_head_fwd_scratch(M, K)),), dtype=torch.float32, device=dev)
+    tab, cnt, lrd = lr_advance if (lr_advance is not None and have_t) else (None, None, None)
     rc = lib.ddpx_head_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, C, h.stride(0),
                            1.0 / M, native.ptr(logits), native.ptr(dl), native.ptr(correct), scratch.data_ptr(),
                            _tickets(dev, int(lib.ddpx_head_fwd_tickets(M))).data_ptr(), native.ptr(loss),
-                           native.stream_handle())
+                           native.ptr(tab), int(tab.numel()) if tab is not None else 0, native.ptr(cnt),
+                           native.ptr(lrd), native.stream_handle())
     native.check(rc, "ddpx_head_fwd")
     return loss, logits, dl
 

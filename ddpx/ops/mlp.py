@@ -23,6 +23,7 @@ from __future__ import annotations
 import torch
 
 from . import gemm as G
+from ..optim.sgd import take_lr_advance
 from .head import head_backward, head_forward
 
 
@@ -81,7 +82,7 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
     wl, bl = ps[-1]
     flat.before_read(wl)
     loss, logits, dl = head_forward(hs[-1], flat.shadow_of(wl), bl, targets, want_logits=want_logits,
-                                    want_grad=want_grad)
+                                    want_grad=want_grad, lr_advance=take_lr_advance(flat) if want_grad else None)
     return hs, loss, logits, dl, saved8
 
 

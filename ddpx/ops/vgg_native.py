@@ -26,6 +26,7 @@ import torch
 from torch import nn
 
 from . import conv as K
+from ..optim.sgd import take_lr_advance
 from .head import head_backward, head_forward
 
 
@@ -96,7 +97,7 @@ def _forward(model, x, targets, want_logits, want_grad, training):
     feat = K.avgpool(x)  # [N, 512] bf16
     cls = model.classifier
     loss, logits, dl = head_forward(feat, flat.shadow_of(cls.weight), cls.bias, targets, want_logits=want_logits,
-                                    want_grad=want_grad)
+                                    want_grad=want_grad, lr_advance=take_lr_advance(flat) if want_grad else None)
     return saved, (x.shape, feat), loss, logits, dl
 
 

@@ -16,11 +16,32 @@ from a device scalar, which makes ``step()`` safe inside a HIP graph.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.optim import Optimizer
 
 from ..ops.elementwise import sgd_flat_
 from ..runtime.flat_params import FlatParams, flat_of
+
+
+# Device LR-schedule advance waiting for a kernel to carry it (SGD.device_lr_step): the classifier head's
+# forward launch takes it (take_lr_advance), which saves the training step a separate 1-thread kernel;
+# anything that reads lr before a head forward took it launches it on its own first (SGD._flush_lr).
+# DDPX_LR_IN_HEAD=0 always launches the separate kernel.
+_PENDING_LR = None
+_LR_IN_HEAD = os.environ.get("DDPX_LR_IN_HEAD", "1") != "0"
+
+
+def take_lr_advance(flat):
+    """(table, counter, lr) if the optimizer of ``flat`` has an LR advance pending (it is then the caller's
+    launch that performs it), else None."""
+    global _PENDING_LR
+    p = _PENDING_LR
+    if p is None or p[0].flat is not flat:
+        return None
+    _PENDING_LR = None
+    return p[1:]
 
 
 class SGD(Optimizer):
@@ -51,7 +72,7 @@ class SGD(Optimizer):
         # that produces its gradient (no gradient round trip through HBM, no separate SGD pass).
         self.fused_backward = bool(fused_backward and flat.master.is_cuda and not nesterov)
         need_dev_lr = capturable or self.fused_backward
-        self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if need_dev_lr else None
+        self._lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device) if need_dev_lr else None
         if self.fused_backward:
             flat.fused_opt = self
         self._lr_table = None  # device-side LR schedule (attach_device_schedule)
@@ -61,6 +82,12 @@ class SGD(Optimizer):
         if getattr(flat.sink, "sharded", False):
             flat.sink.attach_optimizer(self)
         self.step_count = 0
+
+    @property
+    def lr_dev(self):
+        """Device learning-rate scalar (None without one); current once any pending advance has run."""
+        self._flush_lr()
+        return self._lr_dev
 
     @property
     def momentum_buffer(self):
@@ -82,8 +109,8 @@ class SGD(Optimizer):
         """Copy the host learning rate into the device scalar (outside graph capture).
 
         No-op while a device-side schedule is attached (the step kernel sequence advances it)."""
-        if self.lr_dev is not None and self._lr_table is None:
-            self.lr_dev.fill_(float(self.param_groups[0]["lr"]))
+        if self._lr_dev is not None and self._lr_table is None:
+            self._lr_dev.fill_(float(self.param_groups[0]["lr"]))
 
     def attach_device_schedule(self, scheduler, horizon: int | None = None):
         """Tabulate a LambdaLR-style schedule on the device (lr[k] = base_lr * lambda(k)).
@@ -93,7 +120,7 @@ class SGD(Optimizer):
         replays need no host-to-device write.  The host scheduler keeps stepping for bookkeeping
         (state_dict, logging).  ``horizon``: table length (default: the one-cycle's end + 1).
         """
-        if self.lr_dev is None or not self.lr_dev.is_cuda:
+        if self._lr_dev is None or not self._lr_dev.is_cuda:
             return False
         lam = scheduler.lr_lambdas[0]
         base = scheduler.base_lrs[0]
@@ -101,8 +128,8 @@ class SGD(Optimizer):
             spe, ne = getattr(lam, "steps_per_epoch", None), getattr(lam, "num_epochs", None)
             horizon = spe * ne + 1 if spe and ne else 100_000
         table = torch.tensor([base * lam(k) for k in range(horizon)], dtype=torch.float32)
-        self._lr_table = table.to(self.lr_dev.device)
-        self._lr_counter = torch.tensor([scheduler.last_epoch], dtype=torch.int32, device=self.lr_dev.device)
+        self._lr_table = table.to(self._lr_dev.device)
+        self._lr_counter = torch.tensor([scheduler.last_epoch], dtype=torch.int32, device=self._lr_dev.device)
         return True
 
     def step_counter(self):
@@ -113,13 +140,29 @@ class SGD(Optimizer):
     def device_lr_step(self):
         if self._lr_table is None:
             return
+        global _PENDING_LR
+        self._flush_lr()
+        if _LR_IN_HEAD:
+            _PENDING_LR = (self, self._lr_table, self._lr_counter, self._lr_dev)
+            return
+        self._launch_lr_advance()
+
+    def _flush_lr(self):
+        """Launch this optimizer's pending LR advance if no kernel took it (before anything reads lr)."""
+        global _PENDING_LR
+        if _PENDING_LR is not None and _PENDING_LR[0] is self:
+            _PENDING_LR = None
+            self._launch_lr_advance()
+
+    def _launch_lr_advance(self):
         from ..runtime import native
         native.check(native.kernels().ddpx_lr_advance(self._lr_table.data_ptr(), self._lr_table.numel(),
-                                                      self._lr_counter.data_ptr(), self.lr_dev.data_ptr(),
+                                                      self._lr_counter.data_ptr(), self._lr_dev.data_ptr(),
                                                       native.stream_handle()), "ddpx_lr_advance")
 
     def _lr_arg(self):
-        return self.lr_dev if self.lr_dev is not None else float(self.param_groups[0]["lr"])
+        self._flush_lr()
+        return self._lr_dev if self._lr_dev is not None else float(self.param_groups[0]["lr"])
 
     def _update(self, start, end, g):
         f = self.flat

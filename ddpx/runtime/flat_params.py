@@ -217,6 +217,7 @@ class FlatParams:
         g = o.param_groups[0]
         buf = o.momentum_buffer[sl] if o.momentum_buffer is not None else None
         sh = self.shadow[sl] if self.shadow is not None else None
+        o._flush_lr()  # an LR advance no head forward took must land before this epilogue reads lr
         return (self.master[sl], buf, sh, o.lr_dev, g["momentum"], g["weight_decay"])
 
     def mark_updated(self, p):

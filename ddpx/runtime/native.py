@@ -52,7 +52,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_scale_f32", I, P, I64, F, P)
     _sig(lib, "ddpx_lr_advance", I, P, I, P, P, P)
     _sig(lib, "ddpx_gemm_pipe", I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, P, F, F, I, P,
-         I64, P, P)
+         I64, P, P, I, P, P)
     _sig(lib, "ddpx_gemm_pipe_tiles_m", I, I, I, I, I, I, I)
     _sig(lib, "ddpx_gemm_tile_dims", None, I, ctypes.POINTER(c_int), ctypes.POINTER(c_int))
     _sig(lib, "ddpx_gemm_pipe_plan", I, I, I, I, I, I, I, ctypes.POINTER(c_int), ctypes.POINTER(c_int64),
@@ -60,10 +60,9 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_mx8_quant", I, P, I, I, I, P, I, P, P, I, P, I, P)
     _sig(lib, "ddpx_mx8_probe", I, P, P, P, P, P, I, I, P)
     _sig(lib, "ddpx_gemm_mx8", I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, P, P, P, P, F, F, P)
-    _sig(lib, "ddpx_reduce_partials", I, P, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_head_fwd_scratch", I64, I, I)
     _sig(lib, "ddpx_head_fwd_tickets", I64, I)
-    _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P, P)
+    _sig(lib, "ddpx_head_fwd", I, P, P, P, P, I, I, I, I, F, P, P, P, P, P, P, P, I, P, P, P)
     _sig(lib, "ddpx_head_bwd", I, P, P, P, P, I, I, I, I, P, I, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P,
          F, F, P)
     _sig(lib, "ddpx_accuracy", I, P, P, I, I, P, P)

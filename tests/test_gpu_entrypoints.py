@@ -19,8 +19,15 @@ def _run(args, cwd, extra_env=None, timeout=600):
     env = dict(os.environ, PYTHONPATH=ROOT)
     if extra_env:
         env.update(extra_env)
-    r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                       text=True, timeout=timeout)
+    for attempt in range(3):
+        r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True, timeout=timeout)
+        # free_port() cannot reserve the port it returns: another process may bind it before the child's
+        # TCPStore does.  Only that host-side race is retried (nothing GPU-side failed: rendezvous precedes it)
+        if r.returncode != 0 and "EADDRINUSE" in r.stdout and "MASTER_PORT" in env:
+            env["MASTER_PORT"] = str(free_port())
+            continue
+        break
     assert r.returncode == 0, r.stdout[-4000:]
     return r.stdout
 
