@@ -85,13 +85,21 @@ def main():
     d1 = torch.empty_like(h1)
 
     cases = {}
-    for tile in (-1, 12, 5):
+    for tile in (-1, 12, 5, 1, 4):
         cases[f"fwd0_t{tile}"] = lambda tile=tile: G.linear_fwd(x, w0, b0, relu=True, out=h1, tile=tile)
         cases[f"fwd1_t{tile}"] = lambda tile=tile: G.linear_fwd(h1, w1, b1, relu=True, out=h2, tile=tile)
         cases[f"dgrad1_t{tile}"] = lambda tile=tile: G.linear_dgrad(d2, w1, relu_mask_of=h1, out=d1, tile=tile)
-    for tile in (-1, 13, 5):
+    for tile in (-1, 13, 5, 1, 0):
         cases[f"wgrad1_t{tile}"] = lambda tile=tile: G.linear_wgrad(d2, h1, dW1, tile=tile)
         cases[f"wgrad0_t{tile}"] = lambda tile=tile: G.linear_wgrad(d1, x, dW0, tile=tile)
+    mb1 = torch.zeros(H * H, device=dev)
+    mb0 = torch.zeros(H * D0, device=dev)
+    pw1 = torch.randn(H * H, device=dev) * 0.01
+    pw0 = torch.randn(H * D0, device=dev) * 0.01
+    sw1 = torch.empty(H * H, dtype=bf, device=dev)
+    sw0 = torch.empty(H * D0, dtype=bf, device=dev)
+    cases["wgrad1_sgd"] = lambda: G.linear_wgrad(d2, h1, None, sgd=(pw1, mb1, sw1, lr, 0.9, 5e-4))
+    cases["wgrad0_sgd"] = lambda: G.linear_wgrad(d1, x, None, sgd=(pw0, mb0, sw0, lr, 0.9, 5e-4))
     cases["head_fwd"] = lambda: head_forward(h2, w2, b2, t, want_logits=False)
     cases["head_bwd"] = lambda: head_backward(dl, go, h2, w2, dW2, db2, dH=d2, dbprev=dbp)
     cases["sgd_flat"] = lambda: sgd_flat_(p, mb, gg, sh, lr, 0.9, 5e-4)

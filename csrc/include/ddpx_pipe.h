@@ -196,10 +196,27 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kbase, in
     const int k1 = k0 + 4;
     const int off0 = k0 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k0)) << 5) + p * 8;
     const int off1 = k1 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k1)) << 5) + p * 8;
-    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(lds + off0));
-    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(lds + off1));
+    // Inline asm, not __builtin_amdgcn_ds_read_tr16_b64: hipcc (ROCm 7.2) treats the builtin as a possible
+    // reader of every pending LDS-DMA write and puts an `s_waitcnt vmcnt(0)` in front of it, draining the
+    // stage that was just issued for t + STAGES - 1 and collapsing every >= 3-stage ring into a 1-stage one.
+    // The ring's own counted vmcnt + barrier order these reads; the caller waits lgkmcnt before use
+    // (tr_wait()).
+    short4v lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"((LDS_AS const char*)(lds + off0)) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"((LDS_AS const char*)(lds + off1)) : "memory");
     short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// After a batch of frag() reads, before their values are used: the transposing reads are inline asm
+// (invisible to the compiler's waitcnt pass), so wait for LDS here and keep the MFMAs behind the wait
+// (cdna_hip_programming §5.4 rule 18).
+template <bool ANY_TR>
+__device__ __forceinline__ void tr_wait() {
+  if constexpr (ANY_TR) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -499,6 +516,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
       for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / WGM) + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) b[j] = frag<BN, BKc>(sb, wn * (BN / 2) + j * 16, kk, lane);
+      tr_wait<!AK || !BKc>();
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

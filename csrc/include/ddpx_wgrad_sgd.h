@@ -1,0 +1,193 @@
+// ddpx — weight gradient + SGD in one warp-specialised persistent kernel (gfx950).
+//
+//   W -= lr * sgd_direction( dY^T X )          dY [K=batch][M=out] bf16, X [K][N=in] bf16, W fp32 [M][N]
+//
+// The single-process optimizer fused into backward (SGD(fused_backward=True)) streams 18 B per weight
+// (master + momentum in, master + momentum + bf16 shadow out) right where the weight gradient is born,
+// so the gradient never round-trips through HBM.  In the tile-per-workgroup GEMM that stream ran AFTER
+// each tile's MFMA main loop: both halves serialised and the fused kernels (toy MLP fc1 / fc0: 97 / 78 us,
+// profiles/r2_head) were no faster than a stored fp32 gradient plus one flat SGD pass.
+//
+// Here every workgroup (one per CU, 8 waves) owns a list of 64x128 tiles and splits its waves by role:
+//   * waves 0-3 (math): the LDS-DMA ring + v_mfma_f32_16x16x32_bf16 main loop of tile i (the pipe core of
+//     ddpx_pipe.h), then its fp32 accumulators into one of two LDS tile buffers;
+//   * waves 4-7 (stream): the optimizer update of tile i-1 from the other buffer — master / momentum loads
+//     for tile i issued one iteration ahead, non-temporal, and the update spread over the K-steps —
+//     so a CU's HBM stream runs while its matrix cores work on the next tile.
+// Both roles execute exactly nk + 1 s_barriers per iteration (nk K-steps of 64, then the buffer hand-off)
+// for nt + 1 iterations (one drain iteration), so the barrier sequence matches by construction.
+// The update arithmetic is sgd_apply's fma sequence: bitwise equal to the stored-gradient + flat-SGD path.
+#pragma once
+
+#include "ddpx_pipe.h"
+
+namespace ddpx {
+namespace wsgd {
+
+constexpr int BM = 64, BN = 128, STAGES = 3;
+constexpr int ALD = BN + 4;  // LDS tile-buffer row stride (floats)
+constexpr int A_SUB = BM * 64 * 2, B_SUB = BN * 64 * 2, SLOT = A_SUB + B_SUB;
+constexpr int ACC_BYTES = BM * ALD * 4;
+constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES;  // 138 KiB: one workgroup per CU
+constexpr int VPT = BM * BN / 4 / 256;                    // f32x4 vectors per stream thread per tile (8)
+
+__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
+  constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
+  constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  float* const accb = reinterpret_cast<float*>(smem + STAGES * SLOT);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = p.M / BM;
+  const int ntiles = tiles_m * (p.N / BN);
+  const int nt = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= ntiles)
+  const int nk = p.K / 64;
+  auto tile_origin = [&](int i, int& m0, int& n0) {
+    const int g = (int)blockIdx.x + i * (int)gridDim.x;
+    m0 = (g % tiles_m) * BM;
+    n0 = (g / tiles_m) * BN;
+  };
+
+  if (wave < 4) {
+    // ------------------------------------------------------------------ math waves
+    const int wm = wave >> 1, wn = wave & 1;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, p.b_bytes, 0x00020000);
+    for (int i = 0; i <= nt; ++i) {
+      if (i == nt) {  // drain iteration: the stream waves finish the last tile
+        for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
+      } else {
+        int m0, n0;
+        tile_origin(i, m0, n0);
+        auto issue = [&](int t) {
+          char* slot = smem + (t % STAGES) * SLOT;
+          pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, p.lda, m0, p.M, t * 64, p.K, wave, lane);
+          pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, p.ldb, n0, p.N, t * 64, p.K,
+                                                           wave, lane);
+        };
+        f32x4 acc[FM][FN];
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < STAGES - 1; ++s)
+          if (s < nk) issue(s);
+        for (int t = 0; t < nk; ++t) {
+          const int ahead = min(STAGES - 2, nk - 1 - t);
+          if (ahead >= 1) pipe::wait_vmcnt<LPW>();
+          else pipe::wait_vmcnt<0>();
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+          const char* sa = smem + (t % STAGES) * SLOT;
+          const char* sb = sa + A_SUB;
+#pragma unroll
+          for (int kk = 0; kk < 64; kk += 32) {
+            bf16x8 af[FM], bfr[FN];
+#pragma unroll
+            for (int a = 0; a < FM; ++a) af[a] = pipe::frag<BM, false>(sa, wm * 32 + a * 16, kk, lane);
+#pragma unroll
+            for (int b = 0; b < FN; ++b) bfr[b] = pipe::frag<BN, false>(sb, wn * 64 + b * 16, kk, lane);
+            pipe::tr_wait<true>();
+#pragma unroll
+            for (int a = 0; a < FM; ++a)
+#pragma unroll
+              for (int b = 0; b < FN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+          }
+        }
+        // accumulators -> tile buffer i&1 (C/D map: row 4*(lane>>4)+r, col lane&15 of each 16x16 block)
+        float* T = accb + (i & 1) * (ACC_BYTES / 4);
+        const int mr = wm * 32 + 4 * (lane >> 4), nc = wn * 64 + (lane & 15);
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) T[(mr + a * 16 + r) * ALD + nc + b * 16] = acc[a][b][r] * p.alpha;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // hand-off: tile i's buffer complete, tile i-1's buffer released
+    }
+  } else {
+    // ---------------------------------------------------------------- stream waves
+    const int st = tid - 256;
+    const int row0 = st >> 5, col = 4 * (st & 31);  // vector v: row row0 + 8 v, columns col..col+3
+    const float lr = *p.sgd.lr;
+    const float mom = p.sgd.mom, wd = p.sgd.wd;
+    const bool has_mom = mom != 0.f;
+    f32x4 pc[VPT], mc[VPT], pn[VPT], mn[VPT];
+    auto load_tile = [&](int i, f32x4 (&pv)[VPT], f32x4 (&mv)[VPT]) {
+      int m0, n0;
+      tile_origin(i, m0, n0);
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        const size_t off = (size_t)(m0 + row0 + 8 * v) * p.ldc + n0 + col;
+        pv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.p + off));
+        mv[v] = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.buf + off))
+                        : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    int pm0 = 0, pn0 = 0;  // origin of the tile being updated (i - 1)
+    for (int i = 0; i <= nt; ++i) {
+      if (i < nt) load_tile(i, pn, mn);  // one iteration ahead of its update
+      const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
+      for (int t = 0; t < nk; ++t) {
+        __builtin_amdgcn_s_barrier();
+        if (i == 0) continue;
+        // this K-step's share of tile i-1's update
+        const int v0 = t * VPT / nk, v1 = (t + 1) * VPT / nk;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+          if (v < v0 || v >= v1) continue;
+          const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + 8 * v) * ALD + col);
+          f32x4 po, bo;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
+            float d = fmaf(wd, pc[v][q], g[q]);
+            if (has_mom) {
+              d = fmaf(mom, mc[v][q], d);
+              bo[q] = d;
+            }
+            po[q] = fmaf(-lr, d, pc[v][q]);
+          }
+          const size_t off = (size_t)(pm0 + row0 + 8 * v) * p.ldc + pn0 + col;
+          __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(p.sgd.p + off));
+          if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(p.sgd.buf + off));
+          if (p.sgd.shadow)
+            *reinterpret_cast<u32x2*>(p.sgd.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (i < nt) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+          pc[v] = pn[v];
+          mc[v] = mn[v];
+        }
+        tile_origin(i, pm0, pn0);
+      }
+    }
+  }
+}
+
+// Eligible shapes: the plain weight-gradient layout (A M-contig, B N-contig), M % 64 == 0, N % 128 == 0,
+// K % 64 == 0 (whole K-steps: the two roles' barrier counts are nk), ldc % 4 == 0.
+static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
+  return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K % 64 == 0 && p.K >= 64 && (p.ldc & 3) == 0 &&
+         p.sgd.p && p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf);
+}
+
+static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
+  const int ntiles = (p.M / BM) * (p.N / BN);
+  const int grid = ntiles < num_cus ? ntiles : num_cus;
+  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace wsgd
+}  // namespace ddpx

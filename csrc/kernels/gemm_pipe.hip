@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "ddpx_pipe.h"
+#include "ddpx_wgrad_sgd.h"
 
 namespace ddpx {
 namespace pipe {
@@ -158,6 +159,22 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   if (tile_cfg < 0 && !a_kcontig && !b_kcontig && epi != pipe::EPI_SGD && !colsum &&
       ((M + 255) / 256) * ((N + 255) / 256) >= 128)
     cfg = 13;
+  // Weight gradient with the SGD update: the warp-specialised persistent kernel (MFMA waves + optimizer
+  // stream waves per CU, ddpx_wgrad_sgd.h) when the shape allows; DDPX_WGRAD_WS=0 keeps the tile kernel.
+  static const int wgrad_ws = [] {
+    const char* e = getenv("DDPX_WGRAD_WS");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (epi == pipe::EPI_SGD && wgrad_ws && tile_cfg < 0 && splits <= 1 && wsgd::eligible(p, a_kcontig, b_kcontig)) {
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    return (int)wsgd::launch(p, cus, stream);
+  }
   // Master/momentum LDS prefetch for the fused-SGD tiles: opt-in (DDPX_SGD_PREFETCH=1).  Measured
   // slower on MI355X (toy fc1 64x128: 112 vs 77 us; profiles/r1_epi): the 64 KiB side buffer halves
   // occupancy and the prefetch lands on the critical path of short (K = 512) main loops.

@@ -196,12 +196,23 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
         _req(bias_sgd is None or bias_sgd[0].numel() == K, "bias_sgd target must have K elements")
         T = tiles_m(M, K, N, True, False, tile)
         part = torch.empty((T, K), dtype=torch.float32, device=dy.device)
+    # the in-launch column-sum finish is built for the 4-wave tiles; an explicitly chosen 8-wave tile
+    # (tests / probes) leaves the partials to a torch reduction
+    in_launch = tile not in _EIGHT_WAVE_TILES
+    _req(in_launch or bias_sgd is None, "fused bias SGD needs a 4-wave dgrad tile")
     gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
              b_kcontig=False, epi=epi, aux=relu_mask_of,
              ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
-             impl=None if part is None else "pipe", splits=splits, cs_out=bias_grad,
-             cs_accumulate=bias_grad_accumulate, cs_sgd=bias_sgd)
+             impl=None if part is None else "pipe", splits=splits,
+             cs_out=bias_grad if in_launch else None, cs_accumulate=bias_grad_accumulate,
+             cs_sgd=bias_sgd if in_launch else None)
+    if part is not None and not in_launch and bias_grad is not None:
+        s = part.sum(0).to(bias_grad.dtype)
+        bias_grad.add_(s) if bias_grad_accumulate else bias_grad.copy_(s)
     return out
+
+
+_EIGHT_WAVE_TILES = (8, 13, 14, 15)
 
 
 def linear_wgrad(dy, x, out, accumulate=False, tile=-1, sgd=None):

@@ -35,7 +35,8 @@ def _resolved(argv, world):
 def test_single_gpu_toy_mlp_defaults():
     a = _resolved([], 1)
     assert a.model == "mlp" and a.hidden == 4096 and a.batch_size == 512
-    assert a.grad_dtype == "fp32" and a.fused_optimizer == 0
+    # single process: SGD fused into the backward kernels (fp32 master / momentum, same arithmetic)
+    assert a.grad_dtype == "fp32" and a.fused_optimizer == 1
     assert not a.shard_optimizer and not a.overlap_optimizer and not a.comm_side_optimizer
 
 
@@ -53,8 +54,8 @@ def test_zero1_opt_in():
     assert a.shard_optimizer == 1 and a.comm_side_optimizer == 1 and a.defer_gather == 1
 
 
-def test_other_models_keep_fused_optimizer():
-    for m in ("mlp_wide", "vgg", "deepnn"):
+def test_every_model_fuses_the_single_gpu_optimizer():
+    for m in ("mlp", "mlp_wide", "vgg", "deepnn"):
         a = _resolved(["--model", m], 1)
         assert a.fused_optimizer == 1, m
     assert _resolved(["--model", "mlp_wide"], 1).hidden == 16384

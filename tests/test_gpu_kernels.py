@@ -382,3 +382,30 @@ def test_device_lr_schedule_matches_lambdalr(gpu):
         opt.device_lr_step()
         assert abs(opt.lr_dev.item() - host) < 1e-7
         sched.step()
+
+
+@pytest.mark.parametrize("M,N,K,mom", [(4096, 3072, 512, 0.9), (512, 384, 192, 0.9), (256, 128, 64, 0.0)])
+def test_wgrad_sgd_warp_specialised_matches_unfused(gpu, M, N, K, mom):
+    """dW = dY^T X applied as an SGD update by the warp-specialised kernel (MFMA waves + optimizer stream
+    waves) == fp32 dW from the GEMM + the flat SGD pass, bit for bit (master, momentum, shadow)."""
+    from ddpx.ops import gemm as G
+    from ddpx.ops.elementwise import sgd_flat_
+    torch.manual_seed(9)
+    dy = _rand_bf16(K, M, dev=gpu)
+    x = _rand_bf16(K, N, dev=gpu)
+    p0 = torch.randn(M * N, device=gpu) * 0.02
+    b0 = torch.randn(M * N, device=gpu) * 0.01
+    lr = torch.full((), 0.05, device=gpu)
+    pa, ba = p0.clone(), b0.clone()
+    sa = torch.empty(M * N, dtype=torch.bfloat16, device=gpu)
+    G.linear_wgrad(dy, x, None, sgd=(pa, ba if mom else None, sa, lr, mom, 5e-4))
+    g = torch.empty(M, N, device=gpu)
+    G.linear_wgrad(dy, x, g)
+    pb, bb = p0.clone(), b0.clone()
+    sb = torch.empty_like(sa)
+    sgd_flat_(pb, bb if mom else pb, g.view(-1), sb, lr, mom, 5e-4)
+    torch.cuda.synchronize()
+    assert torch.equal(pa, pb)
+    assert torch.equal(sa, sb)
+    if mom:
+        assert torch.equal(ba, bb)
