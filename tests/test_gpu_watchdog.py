@@ -15,22 +15,12 @@ import time
 
 import pytest
 import torch
-import torch.distributed as dist
 
 from tests._dist_util import free_port
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-
-@pytest.fixture(scope="module")
-def pg(gpu):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(free_port())
-    dist.init_process_group("gloo", rank=0, world_size=1)
-    yield
-    dist.destroy_process_group()
 
 
 class HostFlag:
@@ -67,9 +57,10 @@ def _stalled_step(comm, flag, status, x):
     return body
 
 
-def test_watchdog_reports_timeout_of_graph_replayed_collective(gpu, pg):
+def _timeout_case():
     from ddpx.parallel.comm import CommError, RcclComm
     from ddpx.runtime.graphs import CapturedStep
+    gpu = torch.device("cuda", 0)
     comm = RcclComm(gpu, timeout_s=2.0)
     comm.set_timeout(2.0, "raise")
     flag = HostFlag()
@@ -101,9 +92,10 @@ def test_watchdog_reports_timeout_of_graph_replayed_collective(gpu, pg):
     comm.close()
 
 
-def test_healthy_replays_do_not_time_out(gpu, pg):
+def _healthy_case():
     from ddpx.parallel.comm import RcclComm
     from ddpx.runtime.graphs import CapturedStep
+    gpu = torch.device("cuda", 0)
     comm = RcclComm(gpu, timeout_s=2.0)
     comm.set_timeout(2.0, "raise")
     flag = HostFlag()
@@ -119,6 +111,37 @@ def test_healthy_replays_do_not_time_out(gpu, pg):
     comm.check()
     flag.close()
     comm.close()
+
+
+_CASE_SCRIPT = textwrap.dedent("""
+    import os, sys
+    sys.path.insert(0, {root!r})
+    import torch, torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    import tests.test_gpu_watchdog as t
+    getattr(t, {case!r})()
+    dist.destroy_process_group()
+    print("CASE OK", flush=True)
+""")
+
+
+def _run_case(case):
+    """Each case in a process of its own: they drive RCCL communicators into timeouts / aborts, which must
+    not share a process with the rest of the suite (an aborted communicator's leftovers broke a later
+    one only when ~660 tests had run before it in the same process)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", _CASE_SCRIPT.format(root=ROOT, case=case)], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, errors="replace", timeout=90)
+    assert r.returncode == 0 and "CASE OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_watchdog_reports_timeout_of_graph_replayed_collective(gpu):
+    _run_case("_timeout_case")
+
+
+def test_healthy_replays_do_not_time_out(gpu):
+    _run_case("_healthy_case")
 
 
 _EXIT_SCRIPT = textwrap.dedent("""
