@@ -55,6 +55,9 @@ def parse(argv=None):
     p.add_argument("--fp8", type=int, default=None,
                    help="1: MX-FP8 hidden-layer forward / weight-gradient GEMMs (MLP models; default 0)")
     p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
+    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
+                   help="compute precision of the ddpx engine on the GPU: bf16 (default) or fp32, the reference's "
+                        "recipe on the exact-f32 MFMA kernels (the stock reference then runs without autocast)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--graph_steps", type=int, default=1,
                    help="training steps per captured HIP graph (the launch gap between replays is paid once "
@@ -179,6 +182,8 @@ def make_data(args, device, rank, world, layout=None):
         layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
         if args.impl == "ddpx" and args.model in ("vgg", "deepnn"):
             layout = "nhwc8_bf16"
+        if args.impl == "ddpx" and getattr(args, "dtype", "auto") == "fp32":
+            layout = {"vgg": "nhwc4_f32", "deepnn": "nchw_f32"}.get(args.model, "flat_f32")
         if device.type == "cpu":
             layout = "nchw_f32"
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
@@ -224,13 +229,14 @@ def build_ddpx(args, device, world):
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
     cpu = device.type == "cpu"
-    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="fp32" if cpu else "bf16",
+    fp32 = cpu or args.dtype == "fp32"
+    model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="fp32" if fp32 else "bf16",
                         device=device, fp8=bool(args.fp8))
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update may be fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4,
               capturable=not (args.no_graph or cpu),
-              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not cpu))
+              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not fp32))
     net = model
     if world > 1 or args.ddp_single:
         if cpu:
@@ -280,7 +286,8 @@ def torch_runner(args, device, world, loader, idx_all, full):
     """Eager step loop of the stock recipe (and of the ddpx engine on the CPU)."""
     import torch
     bs = args.batch_size
-    amp = device.type == "cuda" and (args.model not in ("vgg", "deepnn") or args.torch_amp)
+    amp = (device.type == "cuda" and (args.model not in ("vgg", "deepnn") or args.torch_amp)
+           and getattr(args, "dtype", "auto") != "fp32")
     model, net, opt, sched = build_torch(args, device, world)
 
     def one_step(k):
@@ -305,10 +312,12 @@ def torch_runner(args, device, world, loader, idx_all, full):
 
 
 def measure_stock_same_run(args, device, loader, idx_all, full):
-    """Stock PyTorch-ROCm recipe (nn.Linear + bf16 autocast + foreach SGD), same data, same process."""
+    """Stock PyTorch-ROCm recipe (nn.Linear + bf16 autocast + foreach SGD; fp32 without autocast when
+    --dtype fp32), same data, same process."""
     import torch
     a = argparse.Namespace(**vars(args))
-    a.impl, a.torch_amp = "torch", True
+    a.impl, a.torch_amp = "torch", args.dtype != "fp32"
+    loader = make_data(a, device, 0, 1)  # the stock model's own (NCHW / flat fp32) input layout
     _, _, _, _, run = torch_runner(a, device, 1, loader, idx_all, full)
     run(0, 5)
     torch.cuda.synchronize()
@@ -317,7 +326,8 @@ def measure_stock_same_run(args, device, loader, idx_all, full):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.stock_steps
     return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(args.batch_size / dt, 2),
-            "recipe": "torch.nn + bf16 autocast + foreach SGD", "steps": args.stock_steps}
+            "recipe": "torch.nn + " + ("fp32" if args.dtype == "fp32" else "bf16 autocast") + " + foreach SGD",
+            "steps": args.stock_steps}
 
 
 def main(argv=None):
@@ -472,7 +482,7 @@ def main(argv=None):
                   "mlp_wide": f"wide-mlp-3072x{args.hidden}x{args.layers}",
                   "vgg": "vgg11-cifar", "deepnn": "deepnn-cifar"}[args.model]
     base = baseline_value(f"{args.model}_x{world}") if args.impl == "ddpx" else None
-    if cpu:
+    if cpu or (args.impl == "ddpx" and args.dtype == "fp32"):
         dtype = "fp32"
     elif args.model.startswith("mlp"):
         dtype = "mxfp8/bf16" if (args.fp8 and args.impl == "ddpx") else "bf16"

@@ -13,7 +13,8 @@
 
 namespace ddpx {
 
-enum OutLayout : int { OUT_NCHW_F32 = 0, OUT_NCHW_BF16 = 1, OUT_NHWC_BF16 = 2, OUT_NHWC_F32 = 3, OUT_NHWC8_BF16 = 4 };
+enum OutLayout : int { OUT_NCHW_F32 = 0, OUT_NCHW_BF16 = 1, OUT_NHWC_BF16 = 2, OUT_NHWC_F32 = 3, OUT_NHWC8_BF16 = 4,
+                       OUT_NHWC4_F32 = 5 };
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -30,7 +31,8 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
                                              const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad,
                                              uint64_t seed, int train, int layout, void* __restrict__ out,
                                              int64_t* __restrict__ tgt_out) {
-  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
+                     layout == OUT_NHWC4_F32);
   const int G = W / 8;  // 8-pixel groups per row (W % 8 == 0 checked on the host)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int total = nhwc ? B * H * W : B * C * H * G;
@@ -92,6 +94,14 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
       *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned short*>(out) + (((size_t)b * H + y) * W + xo) * 8) = pk;
       return;
     }
+    if (layout == OUT_NHWC4_F32) {
+      // NHWC fp32 with the channels zero-padded to 4 (16-B pixels: the fp32 conv0 implicit-GEMM input)
+      f32x4 v;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) v[cc] = (ok && cc < C) ? (float)img[(size_t)cc * H * W + sy * W + sx] * inv : 0.f;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + (((size_t)b * H + y) * W + xo) * 4) = v;
+      return;
+    }
     const size_t o = (((size_t)b * H + y) * W + xo) * C;
     for (int cc = 0; cc < C; ++cc) {
       const float v = ok ? (float)img[(size_t)cc * H * W + sy * W + sx] * inv : 0.f;
@@ -128,8 +138,9 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
                           hipStream_t s) {
   if (B <= 0) return 0;
   if (W % 8) return -1;
-  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
-  if (layout == OUT_NHWC8_BF16 && C > 8) return -2;
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
+                     layout == OUT_NHWC4_F32);
+  if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx, B, C, H, W, pad, seed, train, layout, out, tgt_out, (const int*)nullptr, 1);
@@ -143,8 +154,9 @@ DDPX_API int ddpx_augment_cursor(const void* images, const int64_t* labels, cons
                                  int64_t* tgt_out, const int* cursor, hipStream_t s) {
   if (B <= 0 || nbatch <= 0 || !cursor) return -3;
   if (W % 8) return -1;
-  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16);
-  if (layout == OUT_NHWC8_BF16 && C > 8) return -2;
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
+                     layout == OUT_NHWC4_F32);
+  if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx_all, B, C, H, W, pad, seed, train, layout, out, tgt_out, cursor, nbatch);

@@ -1,0 +1,750 @@
+// ddpx — the reference's fp32 recipe on MI355X (``--dtype fp32``; /root/reference/singlegpu.py:134 trains
+// VGG in fp32 and reports "fp32 model has accuracy", :248-249).
+//
+// Every operation of the VGG / MLP training step in exact fp32, on CDNA4 directly:
+//
+//   * one GEMM core for Linear fwd / dgrad / wgrad and the 3x3 convolutions as implicit GEMMs (NHWC, the
+//     im2col never materialised): v_mfma_f32_16x16x4_f32 — f32 in, f32 accumulate, bitwise an fmaf chain,
+//     64 FLOP/clk/SIMD = the f32 vector peak (157 TF; gfx950 has no xf32).  256-thread workgroups of
+//     2x2 waves, 128x128 / 128x64 / 64x64 tiles, BK = 16, register-staged global loads of tile t+1 issued
+//     before the MFMAs of tile t, double-buffered LDS (one barrier per K step), rows padded by 20 floats
+//     (conflict-free fragment reads and transposing stores on the 64-bank LDS), XCD-aware tile order;
+//   * weight gradients of the convolutions split over K (= N*H*W) into fixed-order partial slabs reduced
+//     (and permuted to torch's [Co][Ci][3][3]) by one pass — deterministic, no float atomics;
+//   * BatchNorm2d training statistics as per-chunk (mean, M2) merged by Chan's formula in the finalize
+//     (running stats: momentum, unbiased variance; num_batches_tracked on device), apply + ReLU +
+//     MaxPool2d(2) fused in one pass, backward with the pool routing (first maximum of each window, as
+//     torch) and the ReLU mask recomputed from the saved pre-BN activation;
+//   * global average pool, and the 10-class head: logits + softmax cross-entropy + dlogits, with
+//     dW / db / dfeature (+ ReLU mask for the MLP) in the backward.
+#include "ddpx_common.h"
+
+namespace ddpx {
+namespace f32k {
+
+enum Mode { DENSE_KC = 0, DENSE_OC = 1, IM2COL_KC = 2, IM2COL_OC = 3 };
+
+// A logical operand X(o, k): o = row of A / column of B ("outer"), k = reduction index.
+//   DENSE_KC : p[o * ld + k]           (contiguous along k; K % 4 == 0)
+//   DENSE_OC : p[k * ld + o]           (contiguous along o; O % 4 == 0)
+//   IM2COL_KC: o = pixel m, k = (r*3+s)*C + c -> x[n][h+sgn(r-1)][w+sgn(s-1)][c]   (forward / data gradient A)
+//   IM2COL_OC: o = (r*3+s)*C + c, k = pixel m  (same element)                         (weight gradient B)
+// Out-of-range rows / k / padding taps read as 0.  C, H, W are powers of two (log2 given).
+struct Operand {
+  const float* p;
+  int ld, O;
+  int lc, lh, lw, sgn;
+};
+
+__device__ __forceinline__ f32x4 im2col4(const Operand& X, int m, int k) {
+  const int n = m >> (X.lh + X.lw);
+  const int h = (m >> X.lw) & ((1 << X.lh) - 1);
+  const int w = m & ((1 << X.lw) - 1);
+  const int rs = k >> X.lc;
+  const int c = k & ((1 << X.lc) - 1);
+  const int r = (rs * 11) >> 5;  // rs / 3 for rs < 9
+  const int s = rs - 3 * r;
+  const int ih = h + X.sgn * (r - 1), iw = w + X.sgn * (s - 1);
+  if (rs >= 9 || ih < 0 || iw < 0 || ih >= (1 << X.lh) || iw >= (1 << X.lw)) return (f32x4){0.f, 0.f, 0.f, 0.f};
+  const size_t off = ((((size_t)n << X.lh | ih) << X.lw | iw) << X.lc) | c;
+  return *reinterpret_cast<const f32x4*>(X.p + off);
+}
+
+template <int MODE>
+__device__ __forceinline__ f32x4 load4(const Operand& X, int o, int k, int kend) {
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  if (o >= X.O || k >= kend) return zero;
+  if constexpr (MODE == DENSE_KC) return *reinterpret_cast<const f32x4*>(X.p + (size_t)o * X.ld + k);
+  if constexpr (MODE == DENSE_OC) return *reinterpret_cast<const f32x4*>(X.p + (size_t)k * X.ld + o);
+  if constexpr (MODE == IM2COL_KC) return im2col4(X, o, k);
+  return im2col4(X, k, o);
+}
+
+constexpr int BK = 16, PAD = 20, NT = 256;
+
+template <int MODE, int BO>
+struct Stage {
+  static constexpr int NV = BO * BK / 4 / NT;  // float4 per thread per tile
+  static constexpr bool KC = (MODE == DENSE_KC || MODE == IM2COL_KC);
+  f32x4 r[NV];
+  __device__ __forceinline__ void load(const Operand& X, int o0, int kt, int kend, int tid) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = tid + NT * v;
+      if constexpr (KC) r[v] = load4<MODE>(X, o0 + (idx >> 2), kt + (idx & 3) * 4, kend);
+      else r[v] = load4<MODE>(X, o0 + (idx % (BO / 4)) * 4, kt + idx / (BO / 4), kend);
+    }
+  }
+  __device__ __forceinline__ void store(float (*S)[BO + PAD], int tid) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = tid + NT * v;
+      if constexpr (KC) {
+        const int o = idx >> 2, kq = (idx & 3) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S[kq + e][o] = r[v][e];
+      } else {
+        *reinterpret_cast<f32x4*>(&S[idx / (BO / 4)][(idx % (BO / 4)) * 4]) = r[v];
+      }
+    }
+  }
+};
+
+enum Flags { F_RELU = 1, F_ACCUM = 2, F_SPLIT = 4 };
+
+// C[m][n] (+)= sum_k A(m,k) B(k,n)  [+ bias[n]] [relu] [* (mask[m][n] > 0)]; F_SPLIT: the K range of
+// blockIdx's split z goes to the raw slab C + z * split_stride.
+template <int BM, int BN, int AM, int BMD>
+__global__ void __launch_bounds__(NT)
+gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C, int ldc,
+                long split_stride, const float* __restrict__ bias, const float* __restrict__ mask, int flags,
+                int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = tiles_m * tiles_n;
+  const int z = bid / per, t2 = bid - z * per;
+  // consecutive ids (one XCD's range) walk down M inside one column panel of B: the B panel stays in L2
+  const int tm = t2 % tiles_m, tn = t2 / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k0 = z * kchunk, k1 = min(K, k0 + kchunk);
+  const int nk = (k1 - k0 + BK - 1) / BK;
+
+  constexpr int FM = BM / 32, FN = BN / 32;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  Stage<AM, BM> sa;
+  Stage<BMD, BN> sb;
+  if (nk > 0) {
+    sa.load(A, m0, k0, k1, tid);
+    sb.load(B, n0, k0, k1, tid);
+    sa.store(As[0], tid);
+    sb.store(Bs[0], tid);
+  }
+  __syncthreads();
+  const int lr = lane >> 4, lc = lane & 15;
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < nk;
+    if (more) {
+      sa.load(A, m0, k0 + (it + 1) * BK, k1, tid);
+      sb.load(B, n0, k0 + (it + 1) * BK, k1, tid);
+    }
+    // blocked summation: each K step's 16 products go into a fresh accumulator that is then added to the
+    // running sum — the rounding chain is K/16 long instead of K (4x smaller error at K = 4608, where a
+    // plain MFMA chain left the conv7 output 4e-6 from fp64, enough to flip max-pool routings)
+    f32x4 part[FM][FN];
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = As[cur][kk + lr][wm * (BM / 2) + i * 16 + lc];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = Bs[cur][kk + lr][wn * (BN / 2) + j * 16 + lc];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], kk ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f},
+                                                            0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
+    if (more) {
+      sa.store(As[cur ^ 1], tid);
+      sb.store(Bs[cur ^ 1], tid);
+    }
+    __syncthreads();
+  }
+
+  float* out = (flags & F_SPLIT) ? C + (size_t)z * split_stride : C;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * (BM / 2) + i * 16 + lr * 4 + e;
+        const int col = n0 + wn * (BN / 2) + j * 16 + lc;
+        if (row >= M || col >= N) continue;
+        float v = acc[i][j][e];
+        const size_t o = (size_t)row * ldc + col;
+        if (!(flags & F_SPLIT)) {
+          if (bias) v += bias[col];
+          if (flags & F_ACCUM) v += out[o];
+          if (flags & F_RELU) v = fmaxf(v, 0.f);
+          if (mask && !(mask[o] > 0.f)) v = 0.f;
+        }
+        out[o] = v;
+      }
+}
+
+template <int BM, int BN, int AM, int BMD>
+static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
+                   long split_stride, const float* bias, const float* mask, int flags, hipStream_t s) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  const int nwg = tm * tn * splits;
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AM, BMD>), dim3(nwg), dim3(NT), 0, s, A, B, M, N, K, kchunk, C, ldc,
+                     split_stride, bias, mask, flags, tm, tn);
+}
+
+template <int AM, int BMD>
+static void dispatch_tile(int tile, const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C,
+                          int ldc, long ss, const float* bias, const float* mask, int flags, hipStream_t s) {
+  switch (tile) {
+    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
+    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
+    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
+  }
+}
+
+// ------------------------------------------------------------------ conv helpers
+// Forward / data-gradient GEMM weights from torch's [Co][Ci][3][3] fp32 master:
+//   wf[(r*3+s)*Cp + ci][co]  (Cp >= Ci zero-padded input channels)     — B of the forward
+//   wd[(r*3+s)*Co + co][ci]  (only when wd != null)                     — B of the data gradient
+__global__ void __launch_bounds__(256) wprep_kernel(const float* __restrict__ w, int Co, int Ci, int Cp,
+                                                     float* __restrict__ wf, float* __restrict__ wd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over 9 * Cp * Co
+  if (i >= 9 * Cp * Co) return;
+  const int co = i % Co, k = i / Co, ci = k % Cp, rs = k / Cp;
+  const float v = ci < Ci ? w[((size_t)co * Ci + ci) * 9 + rs] : 0.f;
+  wf[i] = v;
+  if (wd && ci < Ci) wd[((size_t)rs * Co + co) * Ci + ci] = v;
+}
+
+// grad[co][ci][r][s] (+)= sum_z part[z][co][(r*3+s)*Cp + ci]   (fixed order over z)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
+                                                            int Cp, float* __restrict__ grad, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over Co * Ci * 9, torch order
+  if (i >= Co * Ci * 9) return;
+  const int rs = i % 9, ci = (i / 9) % Ci, co = i / (9 * Ci);
+  const size_t stride = (size_t)Co * 9 * Cp;
+  const float* p = part + (size_t)co * 9 * Cp + rs * Cp + ci;
+  float acc = 0.f;
+  for (int z = 0; z < S; ++z) acc += p[z * stride];
+  grad[i] = accumulate ? grad[i] + acc : acc;
+}
+
+// out[i] (+)= sum_z part[z][i]
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ part, int S, long n,
+                                                             float* __restrict__ out, int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int z = 0; z < S; ++z) acc += part[z * n + i];
+  out[i] = accumulate ? out[i] + acc : acc;
+}
+
+// ------------------------------------------------------------------ BatchNorm (NHWC [P][C], fp32)
+// Threads: channel c = tid % C, row group g = tid / C (G = blockDim / C groups).  blockDim = max(256, C).
+__device__ __forceinline__ float block_group_sum(float v, float* red, int C, int G, int tid) {
+  red[tid] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (tid < C)
+    for (int g = 0; g < G; ++g) s += red[g * C + tid];
+  __syncthreads();
+  return s;  // valid on tid < C
+}
+
+// part[t][0][c] = mean of chunk t, part[t][1][c] = M2 of chunk t (two passes over the L2-resident chunk)
+__global__ void __launch_bounds__(512) bn_stats_kernel(const float* __restrict__ y, int P, int C, int R,
+                                                        float* __restrict__ part) {
+  __shared__ float red[512];
+  __shared__ float bc[512];
+  const int tid = threadIdx.x, c = tid % C, G = blockDim.x / C, g = tid / C;
+  const int r0 = blockIdx.x * R, r1 = min(P, r0 + R);
+  float s = 0.f;
+  for (int r = r0 + g; r < r1; r += G) s += y[(size_t)r * C + c];
+  s = block_group_sum(s, red, C, G, tid);
+  if (tid < C) bc[tid] = s / (float)(r1 - r0);
+  __syncthreads();
+  const float mu = bc[c];
+  float q = 0.f;
+  for (int r = r0 + g; r < r1; r += G) {
+    const float d = y[(size_t)r * C + c] - mu;
+    q = fmaf(d, d, q);
+  }
+  q = block_group_sum(q, red, C, G, tid);
+  if (tid < C) {
+    part[(size_t)blockIdx.x * 2 * C + c] = mu;
+    part[(size_t)blockIdx.x * 2 * C + C + c] = q;
+  }
+}
+
+// Chan merge of the chunk statistics + running-stat update + affine coefficients a = gamma*rstd, b = beta.
+// The normalisation is applied as a*(y - mean) + beta, not a*y + (beta - a*mean): the folded form cancels
+// two terms of size |mean|/std and loses that many bits per layer.  Eval: running statistics.
+// 1024 threads = 64 channels x 16 chunk groups per workgroup; fp64 merge, fixed order (deterministic).
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ part, int T, int R, int P, int C,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            float* __restrict__ rmean, float* __restrict__ rvar,
+                                                            int64_t* __restrict__ nbt, float momentum, float eps,
+                                                            int training, float* __restrict__ a,
+                                                            float* __restrict__ b, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && training && nbt) *nbt += 1;
+  float mu = 0.f, var = 0.f;
+  if (training) {
+    double sm = 0.0;
+    if (ok)
+      for (int t = g; t < T; t += 16) sm += (double)min(R, P - t * R) * part[(size_t)t * 2 * C + c];
+    red[g][cl] = sm;
+    __syncthreads();
+    double m = 0.0;
+    for (int k = 0; k < 16; ++k) m += red[k][cl];
+    m /= P;
+    __syncthreads();
+    double m2 = 0.0;
+    if (ok)
+      for (int t = g; t < T; t += 16) {
+        const double d = part[(size_t)t * 2 * C + c] - m;
+        m2 += part[(size_t)t * 2 * C + C + c] + (double)min(R, P - t * R) * d * d;
+      }
+    red[g][cl] = m2;
+    __syncthreads();
+    m2 = 0.0;
+    for (int k = 0; k < 16; ++k) m2 += red[k][cl];
+    if (g != 0 || !ok) return;
+    mu = (float)m;
+    var = (float)(m2 / P);
+    const float unb = P > 1 ? (float)(m2 / (P - 1)) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  } else {
+    if (g != 0 || !ok) return;
+    mu = rmean[c];
+    var = rvar[c];
+  }
+  const float rs = 1.f / sqrtf(var + eps);
+  a[c] = gamma[c] * rs;
+  b[c] = beta[c];
+  mean_out[c] = mu;
+  rstd_out[c] = rs;
+}
+
+// out = [maxpool2](relu(a*(y - mean) + b)), 4 channels per thread
+__global__ void __launch_bounds__(256) bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ a,
+                                                        const float* __restrict__ b, const float* __restrict__ mean,
+                                                        int N, int H, int W, int C, int relu, int pool,
+                                                        float* __restrict__ out) {
+  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W, C4 = C / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * Ho * Wo * C4) return;
+  const int c = (int)(i % C4) * 4;
+  const long pix = i / C4;
+  const int wo = (int)(pix % Wo), ho = (int)((pix / Wo) % Ho), n = (int)(pix / ((long)Wo * Ho));
+  const f32x4 av = *reinterpret_cast<const f32x4*>(a + c), bv = *reinterpret_cast<const f32x4*>(b + c);
+  const f32x4 mv = *reinterpret_cast<const f32x4*>(mean + c);
+  f32x4 r;
+  if (!pool) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(y + (size_t)pix * C + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float z = fmaf(av[e], v[e] - mv[e], bv[e]);
+      r[e] = relu ? fmaxf(z, 0.f) : z;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = -INFINITY;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const size_t p = ((size_t)n * H + 2 * ho + dy) * W + 2 * wo + dx;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float z = fmaf(av[e], v[e] - mv[e], bv[e]);
+          if (relu) z = fmaxf(z, 0.f);
+          r[e] = fmaxf(r[e], z);
+        }
+      }
+  }
+  *reinterpret_cast<f32x4*>(out + (size_t)i * 4) = r;
+}
+
+// Gradient at pre-BN pixel (n,h,w,c) of the block output's gradient g: ReLU mask and the 2x2 max-pool routing
+// (the FIRST maximum of the window in row-major order gets the gradient, as torch's max_pool2d backward).
+__device__ __forceinline__ float routed_grad(const float* __restrict__ g, const float* __restrict__ y, float av,
+                                             float bv, float mu, int n, int h, int w, int H, int W, int C, int c,
+                                             int pool, float z) {
+  if (!(z > 0.f)) return 0.f;  // ReLU(z) == 0: no gradient (torch threshold_backward)
+  if (!pool) return g[(((size_t)n * H + h) * W + w) * C + c];
+  const int h0 = h & ~1, w0 = w & ~1;
+  int first = -1;
+  float best = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const size_t p = ((size_t)n * H + h0 + (q >> 1)) * W + w0 + (q & 1);
+    const float zz = fmaxf(fmaf(av, y[p * C + c] - mu, bv), 0.f);
+    if (zz > best) { best = zz; first = q; }
+  }
+  if (first != ((h - h0) << 1 | (w - w0))) return 0.f;
+  return g[(((size_t)n * (H / 2) + (h >> 1)) * (W / 2) + (w >> 1)) * C + c];
+}
+
+// part[t][0][c] = sum gz, part[t][1][c] = sum gz * xhat over pixel chunk t
+__global__ void __launch_bounds__(512) bn_bwd_sums_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                           const float* __restrict__ a, const float* __restrict__ b,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, int N, int H, int W, int C,
+                                                           int pool, int R, float* __restrict__ part) {
+  __shared__ float red[512];
+  const int tid = threadIdx.x, c = tid % C, G = blockDim.x / C, gi = tid / C;
+  const int P = N * H * W;
+  const int r0 = blockIdx.x * R, r1 = min(P, r0 + R);
+  const float av = a[c], bv = b[c], mu = mean[c], rs = rstd[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = r0 + gi; r < r1; r += G) {
+    const int w = r % W, h = (r / W) % H, n = r / (W * H);
+    const float yv = y[(size_t)r * C + c];
+    const float gz = routed_grad(g, y, av, bv, mu, n, h, w, H, W, C, c, pool, fmaf(av, yv - mu, bv));
+    s1 += gz;
+    s2 = fmaf(gz, (yv - mu) * rs, s2);
+  }
+  s1 = block_group_sum(s1, red, C, G, tid);
+  s2 = block_group_sum(s2, red, C, G, tid);
+  if (tid < C) {
+    part[(size_t)blockIdx.x * 2 * C + c] = s1;
+    part[(size_t)blockIdx.x * 2 * C + C + c] = s2;
+  }
+}
+
+// c1 = sum gz / P, c2 = sum gz*xhat / P;  dgamma (+)= sum gz*xhat, dbeta (+)= sum gz
+// (64 channels x 16 chunk groups per workgroup, fp64, fixed order)
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ part, int T, int P, int C,
+                                                                float* __restrict__ c1, float* __restrict__ c2,
+                                                                float* __restrict__ dgamma,
+                                                                float* __restrict__ dbeta, int accumulate) {
+  __shared__ double red[2][16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int t = g; t < T; t += 16) {
+      s1 += part[(size_t)t * 2 * C + c];
+      s2 += part[(size_t)t * 2 * C + C + c];
+    }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  s1 = s2 = 0.0;
+  for (int k = 0; k < 16; ++k) {
+    s1 += red[0][k][cl];
+    s2 += red[1][k][cl];
+  }
+  c1[c] = (float)(s1 / P);
+  c2[c] = (float)(s2 / P);
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s2 : (float)s2;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s1 : (float)s1;
+}
+
+// dy = a * (gz - c1 - xhat * c2)
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                            const float* __restrict__ a, const float* __restrict__ b,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ c1, const float* __restrict__ c2,
+                                                            int N, int H, int W, int C, int pool,
+                                                            float* __restrict__ dy) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * H * W * C) return;
+  const int c = (int)(i % C);
+  const long r = i / C;
+  const int w = (int)(r % W), h = (int)((r / W) % H), n = (int)(r / ((long)W * H));
+  const float av = a[c], bv = b[c], mu = mean[c], yv = y[i];
+  const float gz = routed_grad(g, y, av, bv, mu, n, h, w, H, W, C, c, pool, fmaf(av, yv - mu, bv));
+  const float xh = (yv - mu) * rstd[c];
+  dy[i] = av * (gz - c1[c] - xh * c2[c]);
+}
+
+// ------------------------------------------------------------------ pooling / head
+__global__ void __launch_bounds__(256) avgpool_kernel(const float* __restrict__ x, int N, int S, int C,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += x[((size_t)n * S + k) * C + c];
+  out[i] = s / (float)S;
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restrict__ g, int N, int S, int C,
+                                                           float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * S * C) return;
+  const int c = (int)(i % C);
+  const long n = i / ((long)S * C);
+  dx[i] = g[n * C + c] / (float)S;
+}
+
+// logits[m][j] = h[m] . w[j] + bias[j]   (one thread per logit; the 10-class head is far below MFMA size)
+__global__ void __launch_bounds__(256) head_logits_kernel(const float* __restrict__ h, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, int M, int K, int NC,
+                                                           float* __restrict__ logits) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * NC) return;
+  const int m = i / NC, j = i % NC;
+  const f32x4* hp = reinterpret_cast<const f32x4*>(h + (size_t)m * K);
+  const f32x4* wp = reinterpret_cast<const f32x4*>(w + (size_t)j * K);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int k = 0; k < K / 4; ++k) {
+    const f32x4 x = hp[k], y = wp[k];
+    s0 = fmaf(x[0], y[0], s0);
+    s1 = fmaf(x[1], y[1], s1);
+    s2 = fmaf(x[2], y[2], s2);
+    s3 = fmaf(x[3], y[3], s3);
+  }
+  logits[i] = (s0 + s1) + (s2 + s3) + bias[j];
+}
+
+// One workgroup: per-row log-softmax, loss = mean_m (lse - logit[target]), dl = (softmax - onehot) / M.
+__global__ void __launch_bounds__(1024) xent_kernel(const float* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                     int M, int NC, float* __restrict__ loss,
+                                                     float* __restrict__ dl) {
+  __shared__ float red[1024];
+  const int tid = threadIdx.x;
+  float acc = 0.f;
+  for (int m = tid; m < M; m += 1024) {
+    const float* l = logits + (size_t)m * NC;
+    float mx = -INFINITY;
+    for (int j = 0; j < NC; ++j) mx = fmaxf(mx, l[j]);
+    float se = 0.f;
+    for (int j = 0; j < NC; ++j) se += expf(l[j] - mx);
+    const float lse = mx + logf(se);
+    const int t = (int)tgt[m];
+    acc += lse - l[t];
+    if (dl)
+      for (int j = 0; j < NC; ++j) dl[(size_t)m * NC + j] = (expf(l[j] - lse) - (j == t ? 1.f : 0.f)) / (float)M;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0 && loss) *loss = red[0] / (float)M;
+}
+
+// dW[j][k] (+)= go * sum_m dl[m][j] h[m][k];  db[j] (+)= go * sum_m dl[m][j]
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
+                                                          const float* __restrict__ h, int M, int K, int NC,
+                                                          float* __restrict__ dW, float* __restrict__ db,
+                                                          int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const float s = go ? *go : 1.f;
+  if (i < NC * K) {
+    const int j = i / K, k = i % K;
+    float acc = 0.f;
+    for (int m = 0; m < M; ++m) acc = fmaf(dl[(size_t)m * NC + j], h[(size_t)m * K + k], acc);
+    acc *= s;
+    dW[i] = accumulate ? dW[i] + acc : acc;
+  } else if (i < NC * K + NC) {
+    const int j = i - NC * K;
+    float acc = 0.f;
+    for (int m = 0; m < M; ++m) acc += dl[(size_t)m * NC + j];
+    acc *= s;
+    db[j] = accumulate ? db[j] + acc : acc;
+  }
+}
+
+// dh[m][k] = go * sum_j dl[m][j] w[j][k]   [* (h[m][k] > 0)]
+__global__ void __launch_bounds__(256) head_dgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
+                                                          const float* __restrict__ w, const float* __restrict__ h,
+                                                          int M, int K, int NC, int relu_mask,
+                                                          float* __restrict__ dh) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)M * K) return;
+  const int m = (int)(i / K), k = (int)(i % K);
+  float acc = 0.f;
+  for (int j = 0; j < NC; ++j) acc = fmaf(dl[(size_t)m * NC + j], w[(size_t)j * K + k], acc);
+  acc *= go ? *go : 1.f;
+  if (relu_mask && !(h[i] > 0.f)) acc = 0.f;
+  dh[i] = acc;
+}
+
+// out[n] (+)= sum_m x[m][n]
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x, int M, int N,
+                                                      float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int m = 0; m < M; ++m) acc += x[(size_t)m * N + n];
+  out[n] = accumulate ? out[n] + acc : acc;
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+}  // namespace f32k
+}  // namespace ddpx
+
+using namespace ddpx;
+using namespace ddpx::f32k;
+
+static inline unsigned nblk(long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+// C (+)= A B on the f32 MFMA core.  amode/bmode: Mode; conv geometry (C, H, W of the NHWC tensor an
+// IM2COL operand reads, and the tap sign) applies to whichever operand is IM2COL.  splits > 1: raw partial
+// slabs C + z*split_stride (no epilogue).  tile: 0 = 128x128, 1 = 128x64, 2 = 64x64, -1 = auto.
+DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const float* b, int ldb, int M, int N, int K,
+                           int gc, int gh, int gw, int sgn, int splits, float* c, int ldc, int64_t split_stride,
+                           const float* bias, const float* mask, int flags, int tile, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  const bool kc = amode == DENSE_KC || amode == IM2COL_KC || bmode == DENSE_KC;
+  if ((kc && K % 4) || splits < 1) return -1;  // k-contiguous operands load 4 consecutive k
+  const bool im = amode >= IM2COL_KC || bmode >= IM2COL_KC;
+  int lc = 0, lh = 0, lw = 0;
+  if (im) {
+    lc = ilog2(gc), lh = ilog2(gh), lw = ilog2(gw);
+    if (lc < 2 || lh < 0 || lw < 0) return -2;  // channels: power of two >= 4 (16-B taps)
+    if ((amode == IM2COL_KC && K != 9 * gc) || (bmode == IM2COL_OC && N != 9 * gc)) return -2;
+  }
+  if ((amode == DENSE_OC && M % 4) || (bmode == DENSE_OC && N % 4) || (bmode == IM2COL_OC && N % 4)) return -3;
+  if ((amode == DENSE_KC && lda % 4) || (bmode == DENSE_KC && ldb % 4) || (amode == DENSE_OC && lda % 4) ||
+      (bmode == DENSE_OC && ldb % 4))
+    return -4;
+  if (splits > 1) flags |= F_SPLIT;
+  Operand A{a, lda, M, lc, lh, lw, sgn}, B{b, ldb, N, lc, lh, lw, sgn};
+  if (tile < 0) {
+    const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
+    tile = N <= 64 ? 1 : (t128 >= 512 ? 0 : 2);
+  }
+  const int key = amode * 4 + bmode;
+  switch (key) {
+    case DENSE_KC * 4 + DENSE_KC:
+      dispatch_tile<DENSE_KC, DENSE_KC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      break;
+    case DENSE_KC * 4 + DENSE_OC:
+      dispatch_tile<DENSE_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      break;
+    case DENSE_OC * 4 + DENSE_OC:
+      dispatch_tile<DENSE_OC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      break;
+    case IM2COL_KC * 4 + DENSE_OC:
+      dispatch_tile<IM2COL_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      break;
+    case DENSE_OC * 4 + IM2COL_OC:
+      dispatch_tile<DENSE_OC, IM2COL_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      break;
+    default:
+      return -5;
+  }
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_splitk_reduce(const float* part, int S, int64_t n, float* out, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk(n)), dim3(256), 0, s, part, S, (long)n, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_conv_wprep(const float* w, int Co, int Ci, int Cp, float* wf, float* wd, hipStream_t s) {
+  if (Cp < Ci || (wd && Cp != Ci)) return -1;
+  hipLaunchKernelGGL(wprep_kernel, dim3(nblk((long)9 * Cp * Co)), dim3(256), 0, s, w, Co, Ci, Cp, wf, wd);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_conv_wgrad_reduce(const float* part, int S, int Co, int Ci, int Cp, float* grad, int accumulate,
+                                        hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblk((long)Co * Ci * 9)), dim3(256), 0, s, part, S, Co, Ci, Cp, grad,
+                     accumulate);
+  return (int)hipGetLastError();
+}
+
+static int bn_threads(int C) { return C >= 256 ? C : 256; }
+
+DDPX_API int ddpx_f32_bn_stats(const float* y, int P, int C, int R, float* part, hipStream_t s) {
+  if (C > 512 || (256 % C && C % 256)) return -1;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk(P, R)), dim3(bn_threads(C)), 0, s, y, P, C, R, part);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_bn_finalize(const float* part, int T, int R, int P, int C, const float* gamma, const float* beta,
+                                  float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
+                                  float* a, float* b, float* mean, float* rstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, R, P, C, gamma, beta, rmean, rvar,
+                     nbt, momentum, eps, training, a, b, mean, rstd);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_bn_apply(const float* y, const float* a, const float* b, const float* mean, int N, int H, int W,
+                               int C, int relu, int pool, float* out, hipStream_t s) {
+  if (C % 4 || (pool && (H % 2 || W % 2))) return -1;
+  const long n = (long)N * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(nblk(n)), dim3(256), 0, s, y, a, b, mean, N, H, W, C, relu, pool, out);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_bn_bwd_sums(const float* g, const float* y, const float* a, const float* b, const float* mean,
+                                  const float* rstd, int N, int H, int W, int C, int pool, int R, float* part,
+                                  hipStream_t s) {
+  if (C > 512 || (256 % C && C % 256)) return -1;
+  hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nblk((long)N * H * W, R)), dim3(bn_threads(C)), 0, s, g, y, a, b, mean,
+                     rstd, N, H, W, C, pool, R, part);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_bn_bwd_finalize(const float* part, int T, int P, int C, float* c1, float* c2, float* dgamma,
+                                      float* dbeta, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, P, C, c1, c2, dgamma, dbeta,
+                     accumulate);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_bn_bwd_apply(const float* g, const float* y, const float* a, const float* b, const float* mean,
+                                   const float* rstd, const float* c1, const float* c2, int N, int H, int W, int C,
+                                   int pool, float* dy, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk((long)N * H * W * C)), dim3(256), 0, s, g, y, a, b, mean, rstd,
+                     c1, c2, N, H, W, C, pool, dy);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_avgpool(const float* x, int N, int S, int C, float* out, int backward, hipStream_t s) {
+  if (backward)
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(nblk((long)N * S * C)), dim3(256), 0, s, x, N, S, C, out);
+  else
+    hipLaunchKernelGGL(avgpool_kernel, dim3(nblk((long)N * C)), dim3(256), 0, s, x, N, S, C, out);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_head_fwd(const float* h, const float* w, const float* bias, const int64_t* tgt, int M, int K,
+                               int NC, float* logits, float* loss, float* dl, hipStream_t s) {
+  if (K % 4) return -1;
+  hipLaunchKernelGGL(head_logits_kernel, dim3(nblk((long)M * NC)), dim3(256), 0, s, h, w, bias, M, K, NC, logits);
+  if (tgt) hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(1024), 0, s, logits, tgt, M, NC, loss, dl);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_head_bwd(const float* dl, const float* go, const float* h, const float* w, int M, int K, int NC,
+                               float* dW, float* db, int accumulate, float* dh, int relu_mask, hipStream_t s) {
+  if (dW) hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk((long)NC * K + NC)), dim3(256), 0, s, dl, go, h, M, K, NC,
+                             dW, db, accumulate);
+  if (dh) hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
+                             relu_mask, dh);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_colsum(const float* x, int M, int N, float* out, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_kernel, dim3(nblk(N)), dim3(256), 0, s, x, M, N, out, accumulate);
+  return (int)hipGetLastError();
+}

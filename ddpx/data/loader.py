@@ -25,7 +25,7 @@ from .datasets import ImageDataset
 from .sampler import DistributedIndexSampler
 
 LAYOUTS = {"nchw_f32": 0, "nchw_bf16": 1, "nhwc_bf16": 2, "nhwc_f32": 3, "flat_bf16": 1, "flat_f32": 0,
-           "nhwc8_bf16": 4}
+           "nhwc8_bf16": 4, "nhwc4_f32": 5}
 
 _M64 = (1 << 64) - 1
 
@@ -66,10 +66,12 @@ def augment_cpu(images_u8, labels, idx, seed, train=True, pad=4, layout="nchw_f3
     else:
         out = x.float()
     out = out * (1.0 / 255.0)  # same fp32 constant multiply as the HIP kernel (bit-identical)
-    if layout in ("nhwc_bf16", "nhwc_f32", "nhwc8_bf16"):
+    if layout in ("nhwc_bf16", "nhwc_f32", "nhwc8_bf16", "nhwc4_f32"):
         out = out.permute(0, 2, 3, 1).contiguous()
     if layout == "nhwc8_bf16":
         out = torch.nn.functional.pad(out, (0, 8 - C))
+    if layout == "nhwc4_f32":
+        out = torch.nn.functional.pad(out, (0, 4 - C))
     if layout in ("flat_bf16", "flat_f32"):
         out = out.reshape(B, -1)
     if "bf16" in layout:
@@ -84,7 +86,7 @@ def augment_gpu(images_u8, labels, idx, seed, train=True, pad=4, layout="nchw_f3
     dt = torch.bfloat16 if "bf16" in layout else torch.float32
     shape = {"nchw_f32": (B, C, H, W), "nchw_bf16": (B, C, H, W), "nhwc_bf16": (B, H, W, C),
              "nhwc_f32": (B, H, W, C), "flat_bf16": (B, C * H * W), "flat_f32": (B, C * H * W),
-             "nhwc8_bf16": (B, H, W, 8)}[layout]
+             "nhwc8_bf16": (B, H, W, 8), "nhwc4_f32": (B, H, W, 4)}[layout]
     if out is None:
         out = torch.empty(shape, dtype=dt, device=images_u8.device)
     if tgt is None:

@@ -18,8 +18,9 @@ def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", de
     cdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     if name == "vgg":
         m = VGG()
-        # native NHWC bf16 kernels on the GPU unless fp32 (torch/MIOpen) was asked for
-        m.use_native = kernels == "native" and dev.type == "cuda" and dtype != "fp32"
+        # native NHWC kernels on the GPU: bf16 MFMA, or the exact-f32 MFMA path for the reference's fp32
+        m.use_native = kernels == "native" and dev.type == "cuda"
+        m.native_dtype = "fp32" if dtype == "fp32" else "bf16"
     elif name == "deepnn":
         m = DeepNN()
         m.use_native = kernels == "native" and dev.type == "cuda" and dtype != "fp32"

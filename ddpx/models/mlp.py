@@ -43,6 +43,11 @@ class MLP(nn.Module):
     def linears(self):
         return [getattr(self, f"fc{i}") for i in range(self.num_layers)]
 
+    def _native_f32_ok(self, x):
+        """The reference's fp32 precision on the exact-f32 MFMA kernels (``ddpx.ops.f32``)."""
+        return (self.use_native and x.is_cuda and self.compute_dtype == torch.float32 and not x.requires_grad
+                and getattr(self.fc0.weight, "_ddpx_flat", None) is not None)
+
     def _native_ok(self, x):
         if not (self.use_native and x.is_cuda and self.compute_dtype == torch.bfloat16):
             return False
@@ -60,12 +65,15 @@ class MLP(nn.Module):
                 for lin in lins[:-1]:
                     x = F.relu(lin(x))
                 return lins[-1](x).float()
-        x = x.float()
+        x = x.to(self.fc0.weight.dtype) if self.fc0.weight.dtype == torch.float64 else x.float()
         for lin in lins[:-1]:
             x = F.relu(lin(x))
         return lins[-1](x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._native_f32_ok(x) and not torch.is_grad_enabled():
+            from ..ops import f32
+            return f32.mlp_logits(self, x)
         if self._native_ok(x):
             from ..ops import mlp as mlp_ops
             return mlp_ops.mlp_logits(self, self._flatten(x))
@@ -73,6 +81,9 @@ class MLP(nn.Module):
 
     def forward_loss(self, x: torch.Tensor, targets: torch.Tensor):
         """Fused forward + mean cross-entropy.  Returns (loss, logits-or-None)."""
+        if self._native_f32_ok(x):
+            from ..ops import f32
+            return f32.mlp_loss(self, x, targets), None
         if self._native_ok(x):
             from ..ops import mlp as mlp_ops
             return mlp_ops.mlp_loss(self, self._flatten(x), targets), None
@@ -86,6 +97,10 @@ class MLP(nn.Module):
 
     def ddpx_spec(self, device):
         """Flat-store layout request: bf16 compute shadow + all params written by native kernels."""
+        if torch.device(device).type == "cuda" and self.use_native and self.compute_dtype == torch.float32:
+            from ..runtime import native
+            native.kernels()
+            return {"native_params": list(self.parameters())}  # fp32: kernels read the masters
         if self.native_active(device):
             from ..runtime import native
             native.kernels()  # fail loudly if the extension is missing on a GPU
@@ -95,7 +110,9 @@ class MLP(nn.Module):
         return {}
 
     def input_layout(self, device) -> str:
-        return "flat_bf16" if self.native_active(device) else "nchw_f32"
+        if self.native_active(device):
+            return "flat_bf16"
+        return "flat_f32" if torch.device(device).type == "cuda" and self.use_native else "nchw_f32"
 
     @property
     def ddpx_lazy_gather(self) -> bool:

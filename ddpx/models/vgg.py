@@ -45,6 +45,9 @@ class VGG(nn.Module):
         self.backbone = nn.Sequential(OrderedDict(layers))
         self.classifier = nn.Linear(512, num_classes)
         self.use_native = False
+        # native precision: "bf16" (NHWC bf16 MFMA kernels, fp32 masters) or "fp32" (the reference's
+        # recipe, /root/reference/singlegpu.py:134, on the exact-f32 MFMA kernels of ddpx.ops.f32)
+        self.native_dtype = "bf16"
 
     # ---- ddpx engine protocol -------------------------------------------------
     def native_active(self, device) -> bool:
@@ -54,26 +57,42 @@ class VGG(nn.Module):
         if self.native_active(device):
             from ..runtime import native
             native.kernels()  # fail loudly if the extension is missing on a GPU
+            if self.native_dtype == "fp32":
+                return {"native_params": list(self.parameters())}
             return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters())}
         return {}
 
     def input_layout(self, device) -> str:
-        return "nhwc8_bf16" if self.native_active(device) else "nchw_f32"
+        if not self.native_active(device):
+            return "nchw_f32"
+        return "nhwc4_f32" if self.native_dtype == "fp32" else "nhwc8_bf16"
 
     def _native_ok(self, x):
-        return (self.use_native and x.is_cuda and not x.requires_grad
-                and getattr(self.classifier.weight, "_ddpx_shadow", None) is not None)
+        if not (self.use_native and x.is_cuda and not x.requires_grad):
+            return False
+        if self.native_dtype == "fp32":
+            return getattr(self.classifier.weight, "_ddpx_flat", None) is not None
+        return getattr(self.classifier.weight, "_ddpx_shadow", None) is not None
 
     def forward_loss(self, x: torch.Tensor, targets: torch.Tensor):
         """Fused forward + mean cross-entropy on the native path (torch ops otherwise)."""
         if self._native_ok(x):
+            if self.native_dtype == "fp32":
+                from ..ops import f32
+                return f32.vgg_loss(self, x, targets), None
             from ..ops import vgg_native
             return vgg_native.vgg_loss(self, x, targets), None
         logits = self.forward(x)
         return torch.nn.functional.cross_entropy(logits, targets), logits
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self._native_ok(x):
+        if self._native_ok(x) and self.native_dtype == "fp32":
+            if not torch.is_grad_enabled():  # logits with autograd go through torch ops below
+                from ..ops import f32
+                return f32.vgg_logits(self, x)
+            from ..ops.f32 import prep_vgg_input
+            x = prep_vgg_input(x)[..., :3].permute(0, 3, 1, 2)
+        elif self._native_ok(x):
             from ..ops import vgg_native
             return vgg_native.vgg_forward(self, x)
         # backbone: [N, 3, 32, 32] => [N, 512, 2, 2]

@@ -1,0 +1,407 @@
+"""The reference's fp32 recipe on native MI355X kernels (``--dtype fp32``).
+
+``/root/reference/singlegpu.py:134`` builds the VGG in fp32 and ``:248-249`` reports "fp32 model has
+accuracy"; this module runs that precision end to end on ``csrc/kernels/f32_train.hip`` instead of
+torch/MIOpen: exact-f32 MFMA (``v_mfma_f32_16x16x4_f32``) GEMMs for Linear and the 3x3 convolutions
+(implicit GEMM over NHWC, weight gradients split over N*H*W and reduced in fixed order), BatchNorm2d
+statistics / apply+ReLU+MaxPool / backward, global average pool and the 10-class head + cross-entropy.
+
+The fp32 masters in the flat parameter store are read directly (no compute shadow); gradients land in
+``main_grad`` (DDP bucket storage) through the ``FlatParams`` grad protocol, so DDP, the flat SGD and
+the checkpoint format are the same as on the bf16 path.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..runtime import native
+
+DENSE_KC, DENSE_OC, IM2COL_KC, IM2COL_OC = 0, 1, 2, 3
+F_RELU, F_ACCUM = 1, 2
+
+_P, _I, _I64, _F = native.c_void_p, native.c_int, native.c_int64, native.c_float
+for _sig in (
+        ("ddpx_f32_gemm", _I, _I, _P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I64, _P, _P, _I, _I,
+         _P),
+        ("ddpx_f32_splitk_reduce", _I, _P, _I, _I64, _P, _I, _P),
+        ("ddpx_f32_conv_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
+        ("ddpx_f32_conv_wgrad_reduce", _I, _P, _I, _I, _I, _I, _P, _I, _P),
+        ("ddpx_f32_bn_stats", _I, _P, _I, _I, _I, _P, _P),
+        ("ddpx_f32_bn_finalize", _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _I, _P, _P, _P, _P, _P),
+        ("ddpx_f32_bn_apply", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
+        ("ddpx_f32_bn_bwd_sums", _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
+        ("ddpx_f32_bn_bwd_finalize", _I, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P),
+        ("ddpx_f32_bn_bwd_apply", _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
+        ("ddpx_f32_avgpool", _I, _P, _I, _I, _I, _P, _I, _P),
+        ("ddpx_f32_head_fwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P),
+        ("ddpx_f32_head_bwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _I, _P),
+        ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
+):
+    native.register_kernel_sig(*_sig)
+
+
+
+def bn_chunk_rows(P: int, C: int) -> int:
+    """Pixel rows per BatchNorm statistics chunk: ~16K elements, so a layer splits into enough workgroups
+    to fill the chip (2048 at 64 channels x 32x32 x 512 images) with short per-thread row loops."""
+    return max(8, min(P, 16384 // C))
+
+
+def _req(c, msg):
+    if not c:
+        raise ValueError(msg)
+
+
+def _f32(t, name):
+    _req(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous(), f"{name} must be contiguous fp32 on GPU")
+    _req(t.data_ptr() % 16 == 0, f"{name} must be 16-B aligned")
+
+
+def _call(name, *args):
+    native.check(getattr(native.kernels(), name)(*args, native.stream_handle()), name)
+
+
+def gemm(amode, a, lda, bmode, b, ldb, M, N, K, out, ldc=None, bias=None, mask=None, relu=False, accumulate=False,
+         geom=(0, 0, 0, 1), splits=1, split_stride=0, tile=-1):
+    """out (+)= A B on the f32 MFMA core (operand modes: see f32_train.hip)."""
+    flags = (F_RELU if relu else 0) | (F_ACCUM if accumulate else 0)
+    _call("ddpx_f32_gemm", amode, a.data_ptr(), lda, bmode, b.data_ptr(), ldb, M, N, K, *geom, splits,
+          out.data_ptr(), N if ldc is None else ldc, split_stride, native.ptr(bias), native.ptr(mask), flags, tile)
+
+
+# ---------------------------------------------------------------------------------------------- Linear
+def linear_fwd(x, w, bias=None, relu=False):
+    """y = x W^T + b [relu] — x [M,K], W [N,K] (torch layout)."""
+    M, K = x.shape
+    N = w.shape[0]
+    _f32(x, "x")
+    _f32(w, "w")
+    _req(w.shape[1] == K, "linear_fwd: shape mismatch")
+    y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    gemm(DENSE_KC, x, K, DENSE_KC, w, K, M, N, K, y, bias=bias, relu=relu)
+    return y
+
+
+def linear_dgrad(dy, w, mask=None):
+    """dx = dy W [* (mask > 0)] — dy [M,N], W [N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    _f32(dy, "dy")
+    dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
+    gemm(DENSE_KC, dy, N, DENSE_OC, w, K, M, K, N, dx, mask=mask)
+    return dx
+
+
+def linear_wgrad(dy, x, out, accumulate=False):
+    """dW (+)= dy^T x — dy [M,N], x [M,K], dW [N,K]."""
+    M, N = dy.shape
+    K = x.shape[1]
+    _req(out.shape == (N, K) and out.is_contiguous(), "linear_wgrad: bad output")
+    gemm(DENSE_OC, dy, N, DENSE_OC, x, K, N, K, M, out, accumulate=accumulate)
+
+
+def colsum(x, out, accumulate=False):
+    M, N = x.shape
+    _call("ddpx_f32_colsum", x.data_ptr(), M, N, out.data_ptr(), int(accumulate))
+
+
+def head_forward(h, w, b, targets=None):
+    """(loss [scalar] or None, logits [M,NC], dlogits [M,NC] or None) of the fp32 classifier head."""
+    M, K = h.shape
+    NC = w.shape[0]
+    _f32(h, "h")
+    logits = torch.empty((M, NC), dtype=torch.float32, device=h.device)
+    loss = dl = None
+    if targets is not None:
+        _req(targets.dtype == torch.int64 and targets.numel() == M, "targets must be int64 [M]")
+        loss = torch.empty((), dtype=torch.float32, device=h.device)
+        dl = torch.empty_like(logits)
+    _call("ddpx_f32_head_fwd", h.data_ptr(), w.data_ptr(), b.data_ptr(), native.ptr(targets), M, K, NC,
+          logits.data_ptr(), native.ptr(loss), native.ptr(dl))
+    return loss, logits, dl
+
+
+def head_backward(dl, grad_out, h, w, dW, db, accumulate=False, relu_mask=False, want_dh=True):
+    M, K = h.shape
+    NC = w.shape[0]
+    go = grad_out.float().contiguous() if grad_out is not None else None
+    dh = torch.empty_like(h) if want_dh else None
+    _call("ddpx_f32_head_bwd", dl.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, NC, native.ptr(dW),
+          native.ptr(db), int(accumulate), native.ptr(dh), int(relu_mask))
+    return dh
+
+
+# ---------------------------------------------------------------------------------------------- conv / BN
+def conv_channels(ci: int) -> int:
+    """Input channels as stored (NHWC, 16-B pixels: the 3-channel image is zero-padded to 4)."""
+    return max(4, (ci + 3) // 4 * 4)
+
+
+def conv_wprep(w, wf, wd):
+    Co, Ci = w.shape[:2]
+    Cp = conv_channels(Ci)
+    _req(wf.numel() == 9 * Cp * Co and (wd is None or wd.numel() == 9 * Co * Ci), "conv_wprep: bad buffers")
+    _call("ddpx_f32_conv_wprep", w.data_ptr(), Co, Ci, Cp, wf.data_ptr(), native.ptr(wd))
+
+
+def conv_fwd(x, wf, Co):
+    """y [N*H*W, Co] = conv3x3(x [N,H,W,Cp], pad 1)."""
+    N, H, W, C = x.shape
+    _f32(x, "x")
+    P = N * H * W
+    y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
+    gemm(IM2COL_KC, x, 0, DENSE_OC, wf, Co, P, Co, 9 * C, y, geom=(C, H, W, 1))
+    return y
+
+
+def conv_dgrad(dy, wd, N, H, W, C, Co):
+    """dx [N,H,W,C] = transposed conv of dy [N*H*W, Co] with wd [(r,s,co), ci]."""
+    _f32(dy, "dy")
+    dx = torch.empty((N, H, W, C), dtype=torch.float32, device=dy.device)
+    gemm(IM2COL_KC, dy, 0, DENSE_OC, wd, C, N * H * W, C, 9 * Co, dx, geom=(Co, H, W, -1))
+    return dx
+
+
+def wgrad_splits(Co, Ncols, P):
+    tiles = ((Co + 127) // 128) * ((Ncols + 127) // 128)
+    s = max(1, min(P // 1024, (2048 + tiles - 1) // tiles))
+    return s
+
+
+def conv_wgrad(dy, x, Co, Ci, out, accumulate=False):
+    """out [Co,Ci,3,3] (+)= weight gradient from dy [P, Co] and x [N,H,W,Cp]."""
+    N, H, W, Cp = x.shape
+    P = N * H * W
+    ncol = 9 * Cp
+    S = wgrad_splits(Co, ncol, P)
+    part = torch.empty((S, Co, ncol), dtype=torch.float32, device=dy.device)
+    gemm(DENSE_OC, dy, Co, IM2COL_OC, x, 0, Co, ncol, P, part, geom=(Cp, H, W, 1), splits=S,
+         split_stride=Co * ncol)
+    _call("ddpx_f32_conv_wgrad_reduce", part.data_ptr(), S, Co, Ci, Cp, out.data_ptr(), int(accumulate))
+
+
+def bn_forward(y, N, H, W, C, bn, training, pool):
+    """(x_next, a, b, mean, rstd): statistics + running-stat update + [pool](relu(a*(y-mean)+b)), a = gamma*rstd,
+    b = beta."""
+    dev = y.device
+    P = N * H * W
+    a = torch.empty(C, dtype=torch.float32, device=dev)
+    b, mean, rstd = torch.empty_like(a), torch.empty_like(a), torch.empty_like(a)
+    R = bn_chunk_rows(P, C)
+    T = (P + R - 1) // R
+    part = torch.empty((T, 2, C), dtype=torch.float32, device=dev) if training else a
+    if training:
+        _call("ddpx_f32_bn_stats", y.data_ptr(), P, C, R, part.data_ptr())
+    nbt = bn.num_batches_tracked if (training and bn.num_batches_tracked is not None) else None
+    _call("ddpx_f32_bn_finalize", part.data_ptr(), T, R, P, C, bn.weight.data_ptr(), bn.bias.data_ptr(),
+          bn.running_mean.data_ptr(), bn.running_var.data_ptr(), native.ptr(nbt), float(bn.momentum),
+          float(bn.eps), int(training), a.data_ptr(), b.data_ptr(), mean.data_ptr(), rstd.data_ptr())
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    out = torch.empty((N, Ho, Wo, C), dtype=torch.float32, device=dev)
+    _call("ddpx_f32_bn_apply", y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(), N, H, W, C, 1, int(pool),
+          out.data_ptr())
+    return out, a, b, mean, rstd
+
+
+def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumulate=False):
+    """dy [P, C] of BatchNorm+ReLU(+MaxPool) given the block output gradient g; dgamma/dbeta (+)= ..."""
+    _f32(g, "g")
+    P = N * H * W
+    R = bn_chunk_rows(P, C)
+    T = (P + R - 1) // R
+    part = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
+    _call("ddpx_f32_bn_bwd_sums", g.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+          rstd.data_ptr(), N, H, W, C, int(pool), R, part.data_ptr())
+    c1, c2 = torch.empty_like(a), torch.empty_like(a)
+    _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), native.ptr(dgamma),
+          native.ptr(dbeta), int(accumulate))
+    dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
+    _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+          rstd.data_ptr(), c1.data_ptr(), c2.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
+    return dy
+
+
+def avgpool(x):
+    N, H, W, C = x.shape
+    out = torch.empty((N, C), dtype=torch.float32, device=x.device)
+    _call("ddpx_f32_avgpool", x.data_ptr(), N, H * W, C, out.data_ptr(), 0)
+    return out
+
+
+def avgpool_backward(g, N, H, W, C):
+    dx = torch.empty((N, H, W, C), dtype=torch.float32, device=g.device)
+    _call("ddpx_f32_avgpool", g.data_ptr(), N, H * W, C, dx.data_ptr(), 1)
+    return dx
+
+
+# ---------------------------------------------------------------------------------------------- grads
+def _grad_write(flat, p, fn):
+    """Run fn(out, accumulate) into p's gradient slot (DDP bucket storage) and announce it."""
+    g, acc = flat.grad_target(p)
+    fn(g, acc)
+    flat.grad_done(p)
+
+
+# ---------------------------------------------------------------------------------------------- VGG
+class _VGGPlan:
+    def __init__(self, model):
+        self.blocks = _blocks_of(model)
+        dev = model.classifier.weight.device
+        self.wf, self.wd = [], []
+        for conv, _, _ in self.blocks:
+            Co, Ci = conv.weight.shape[:2]
+            self.wf.append(torch.empty(9 * conv_channels(Ci) * Co, dtype=torch.float32, device=dev))
+            self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev) if Ci % 4 == 0 else None)
+
+
+def _blocks_of(model):
+    from torch import nn
+    mods = list(model.backbone.children())
+    blocks, i = [], 0
+    while i < len(mods):
+        conv, bn = mods[i], mods[i + 1]
+        assert isinstance(conv, nn.Conv2d) and isinstance(bn, nn.BatchNorm2d)
+        i += 3
+        pool = i < len(mods) and isinstance(mods[i], nn.MaxPool2d)
+        if pool:
+            i += 1
+        blocks.append((conv, bn, pool))
+    return blocks
+
+
+def _vgg_plan(model):
+    p = getattr(model, "_ddpx_plan_f32", None)
+    if p is None:
+        p = _VGGPlan(model)
+        model._ddpx_plan_f32 = p
+    return p
+
+
+def prep_vgg_input(x):
+    """NHWC fp32 with 4 channels (the loader's ``nhwc4_f32`` layout), or NCHW fp32 from a reference loader."""
+    if x.dim() == 4 and x.shape[-1] == 4 and x.dtype == torch.float32:
+        return x.contiguous()
+    if x.dim() == 4 and x.shape[1] == 3:
+        x = x.float().permute(0, 2, 3, 1)
+        return torch.nn.functional.pad(x, (0, 1)).contiguous()
+    raise ValueError(f"unsupported VGG input {tuple(x.shape)} {x.dtype}")
+
+
+def _vgg_forward(model, x, targets, training):
+    plan = _vgg_plan(model)
+    saved = []
+    N, H, W, C = x.shape
+    for bi, (conv, bn, pool) in enumerate(plan.blocks):
+        Co = conv.weight.shape[0]
+        conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
+        y = conv_fwd(x, plan.wf[bi], Co)
+        xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool)
+        saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
+        x = xn
+        H, W, C = xn.shape[1], xn.shape[2], Co
+    feat = avgpool(x)
+    cls = model.classifier
+    loss, logits, dl = head_forward(feat, cls.weight, cls.bias, targets)
+    return saved, (x.shape, feat), loss, logits, dl
+
+
+def _vgg_backward(model, saved, last, dl, grad_out):
+    plan = _vgg_plan(model)
+    flat = model.classifier.weight._ddpx_flat
+    cls = model.classifier
+    xshape, feat = last
+    dW, acc = flat.grad_target(cls.weight)
+    db, _ = flat.grad_target(cls.bias)
+    dfeat = head_backward(dl, grad_out, feat, cls.weight, dW, db, accumulate=acc)
+    flat.grad_done(cls.weight)
+    flat.grad_done(cls.bias)
+    g = avgpool_backward(dfeat, *xshape)
+    for bi in range(len(plan.blocks) - 1, -1, -1):
+        conv, bn, pool = plan.blocks[bi]
+        x, y, a, b, mean, rstd, (N, H, W, C, Co), _ = saved[bi]
+        dgam, accg = flat.grad_target(bn.weight)
+        dbet, _ = flat.grad_target(bn.bias)
+        dy = bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgam, dbet, accumulate=accg)
+        flat.grad_done(bn.weight)
+        flat.grad_done(bn.bias)
+        _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
+        if bi > 0:
+            g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+
+
+class _VGGLossF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, targets, model, *params):
+        saved, last, loss, _, dl = _vgg_forward(model, x, targets, model.training)
+        ctx.model, ctx.saved, ctx.last, ctx.dl, ctx.n = model, saved, last, dl, len(params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        _vgg_backward(ctx.model, ctx.saved, ctx.last, ctx.dl, grad_loss)
+        ctx.saved = ctx.last = ctx.dl = None
+        return (None, None, None) + (None,) * ctx.n
+
+
+def vgg_loss(model, x, targets):
+    return _VGGLossF32.apply(prep_vgg_input(x), targets, model, *model.parameters())
+
+
+def vgg_logits(model, x):
+    """Inference logits (no autograd through the native fp32 path)."""
+    with torch.no_grad():
+        _, _, _, logits, _ = _vgg_forward(model, prep_vgg_input(x), None, model.training)
+    return logits
+
+
+# ---------------------------------------------------------------------------------------------- MLP
+def _mlp_forward(model, x, targets):
+    lins = model.linears()
+    hs = [x]
+    for lin in lins[:-1]:
+        hs.append(linear_fwd(hs[-1], lin.weight, lin.bias, relu=True))
+    last = lins[-1]
+    loss, logits, dl = head_forward(hs[-1], last.weight, last.bias, targets)
+    return hs, loss, logits, dl
+
+
+def _mlp_backward(model, hs, dl, grad_out):
+    lins = model.linears()
+    flat = lins[0].weight._ddpx_flat
+    last = lins[-1]
+    dW, acc = flat.grad_target(last.weight)
+    db, _ = flat.grad_target(last.bias)
+    dz = head_backward(dl, grad_out, hs[-1], last.weight, dW, db, accumulate=acc, relu_mask=True)
+    flat.grad_done(last.weight)
+    flat.grad_done(last.bias)
+    for i in range(len(lins) - 2, -1, -1):
+        lin = lins[i]
+        _grad_write(flat, lin.weight, lambda o, ac: linear_wgrad(dz, hs[i], o, ac))
+        _grad_write(flat, lin.bias, lambda o, ac: colsum(dz, o, ac))
+        if i > 0:
+            dz = linear_dgrad(dz, lin.weight, mask=hs[i])
+
+
+class _MLPLossF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, targets, model, *params):
+        hs, loss, _, dl = _mlp_forward(model, x, targets)
+        ctx.model, ctx.hs, ctx.dl, ctx.n = model, hs, dl, len(params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        _mlp_backward(ctx.model, ctx.hs, ctx.dl, grad_loss)
+        ctx.hs = ctx.dl = None
+        return (None, None, None) + (None,) * ctx.n
+
+
+def mlp_loss(model, x, targets):
+    x = x.reshape(x.shape[0], -1).float().contiguous()
+    return _MLPLossF32.apply(x, targets, model, *model.parameters())
+
+
+def mlp_logits(model, x):
+    with torch.no_grad():
+        _, _, logits, _ = _mlp_forward(model, x.reshape(x.shape[0], -1).float().contiguous(), None)
+    return logits

@@ -198,10 +198,13 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels, fp8=getattr(args, "fp8", False))
     if getattr(args, "sync_bn", False) and distributed:
-        if getattr(model, "use_native", False) and device.type == "cuda":
+        if (getattr(model, "use_native", False) and device.type == "cuda"
+                and getattr(model, "native_dtype", "bf16") != "fp32"):
             # native path: the BN kernels merge statistics across ranks themselves (ops/vgg_native.py)
             model.sync_bn_comm = comm
         else:
+            if getattr(model, "native_dtype", "bf16") == "fp32":
+                model.use_native = False  # fp32 SyncBatchNorm: torch-op BatchNorm on the merged statistics
             model = convert_sync_batchnorm(model, comm)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,

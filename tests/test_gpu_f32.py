@@ -1,0 +1,242 @@
+"""The fp32 native path (``ddpx.ops.f32`` on ``csrc/kernels/f32_train.hip``) vs fp64 / fp32 torch references.
+
+The reference trains VGG in fp32 (``/root/reference/singlegpu.py:134``); these kernels are exact-f32 MFMA
+(f32 products, f32 accumulation), so they are held to fp32 round-off (relative 1e-5 .. 1e-4 against an
+fp64 reference), not to bf16 tolerances.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 4096, 3072), (100, 72, 36), (257, 132, 516)])
+def test_linear_fwd_dgrad_wgrad(gpu, M, N, K):
+    from ddpx.ops import f32
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=gpu)
+    w = torch.randn(N, K, device=gpu) / K ** 0.5
+    b = torch.randn(N, device=gpu)
+    y = f32.linear_fwd(x, w, b, relu=True)
+    ref = torch.relu(x.double() @ w.double().t() + b.double())
+    assert _rel(y, ref) < 1e-5
+    dy = torch.randn(M, N, device=gpu)
+    mask = torch.randn(M, K, device=gpu)
+    dx = f32.linear_dgrad(dy, w, mask=mask)
+    refx = (dy.double() @ w.double()) * (mask > 0)
+    assert _rel(dx, refx) < 1e-5
+    dW = torch.empty(N, K, device=gpu)
+    f32.linear_wgrad(dy, x, dW)
+    refw = dy.double().t() @ x.double()
+    assert _rel(dW, refw) < 1e-5
+    f32.linear_wgrad(dy, x, dW, accumulate=True)
+    assert _rel(dW, 2 * refw) < 1e-5
+    db = torch.empty(N, device=gpu)
+    f32.colsum(dy, db)
+    assert _rel(db, dy.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,Ci,Co", [(4, 32, 3, 64), (8, 16, 64, 128), (16, 8, 128, 256), (32, 4, 256, 512),
+                                       (64, 2, 512, 512), (2, 32, 64, 64)])
+def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
+    from ddpx.ops import f32
+    torch.manual_seed(0)
+    Cp = f32.conv_channels(Ci)
+    x = torch.randn(N, Ci, H, H, device=gpu)
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+    xn = F.pad(x.permute(0, 2, 3, 1), (0, Cp - Ci)).contiguous()
+    wf = torch.empty(9 * Cp * Co, device=gpu)
+    wd = torch.empty(9 * Co * Ci, device=gpu) if Ci % 4 == 0 else None
+    f32.conv_wprep(w, wf, wd)
+    y = f32.conv_fwd(xn, wf, Co)
+    xd, wdd = x.double().cpu(), w.double().cpu()
+    ref = F.conv2d(xd, wdd, padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _rel(y.cpu(), ref) < 1e-5
+    dy = torch.randn(N * H * H, Co, device=gpu)
+    xr = xd.clone().requires_grad_(True)
+    wr = wdd.clone().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy.double().cpu().view(N, H, H, Co).permute(0, 3, 1, 2))
+    dw = torch.empty(Co, Ci, 3, 3, device=gpu)
+    f32.conv_wgrad(dy, xn, Co, Ci, dw)
+    assert _rel(dw.cpu(), wr.grad) < 1e-5
+    if wd is not None:
+        dx = f32.conv_dgrad(dy, wd, N, H, H, Ci, Co)
+        assert _rel(dx.cpu().permute(0, 3, 1, 2), xr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_bn_relu_pool_fwd_bwd(gpu, pool):
+    from ddpx.ops import f32
+    torch.manual_seed(1)
+    N, H, C = 16, 8, 128
+    y = torch.randn(N * H * H, C, device=gpu) * 2 + 0.5
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    ref_bn = torch.nn.BatchNorm2d(C).double()
+    ref_bn.load_state_dict({k: v.double().cpu() if v.is_floating_point() else v.cpu()
+                            for k, v in bn.state_dict().items()})
+    out, a, b, mean, rstd = f32.bn_forward(y, N, H, H, C, bn, True, pool)
+    yr = y.double().cpu().view(N, H, H, C).permute(0, 3, 1, 2).clone().requires_grad_(True)
+    z = torch.relu(ref_bn(yr))
+    if pool:
+        z = F.max_pool2d(z, 2)
+    assert _rel(out.cpu().permute(0, 3, 1, 2), z) < 1e-5
+    assert _rel(bn.running_mean.cpu(), ref_bn.running_mean) < 1e-5
+    assert _rel(bn.running_var.cpu(), ref_bn.running_var) < 1e-5
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn_like(out)
+    z.backward(g.double().cpu().permute(0, 3, 1, 2))
+    dgam, dbet = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+    dy = f32.bn_backward(g, y, a, b, mean, rstd, N, H, H, C, pool, dgam, dbet)
+    assert _rel(dy.cpu().view(N, H, H, C).permute(0, 3, 1, 2), yr.grad) < 1e-4
+    assert _rel(dgam.cpu(), ref_bn.weight.grad) < 1e-4
+    assert _rel(dbet.cpu(), ref_bn.bias.grad) < 1e-4
+
+
+def test_head_xent(gpu):
+    from ddpx.ops import f32
+    torch.manual_seed(2)
+    M, K, NC = 300, 512, 10
+    h = torch.randn(M, K, device=gpu).relu()
+    w = torch.randn(NC, K, device=gpu) / K ** 0.5
+    b = torch.randn(NC, device=gpu)
+    t = torch.randint(0, NC, (M,), device=gpu)
+    loss, logits, dl = f32.head_forward(h, w, b, t)
+    hr, wr, br = (v.double().cpu().requires_grad_(True) for v in (h, w, b))
+    lr = hr @ wr.t() + br
+    ref = F.cross_entropy(lr, t.cpu())
+    assert _rel(logits.cpu(), lr.detach()) < 1e-6
+    assert abs(loss.item() - ref.item()) < 1e-5
+    ref.backward(torch.tensor(0.5, dtype=torch.float64))
+    dW, db = torch.empty(NC, K, device=gpu), torch.empty(NC, device=gpu)
+    dh = f32.head_backward(dl, torch.tensor(0.5, device=gpu), h, w, dW, db, relu_mask=True)
+    assert _rel(dW.cpu(), wr.grad) < 1e-5
+    assert _rel(db.cpu(), br.grad) < 1e-5
+    assert _rel(dh.cpu(), hr.grad * (hr.detach() > 0)) < 1e-5
+
+
+def test_augment_nhwc4_f32_matches_cpu(gpu):
+    from ddpx.data.loader import augment_cpu, augment_gpu
+    torch.manual_seed(3)
+    imgs = torch.randint(0, 256, (64, 3, 32, 32), dtype=torch.uint8)
+    labels = torch.randint(0, 10, (64,))
+    idx = torch.randperm(64)[:32]
+    xc, yc = augment_cpu(imgs, labels, idx, 1234, True, 4, "nhwc4_f32")
+    xg, yg = augment_gpu(imgs.to(gpu), labels.to(gpu), idx.to(gpu), 1234, True, 4, "nhwc4_f32")
+    assert xg.shape == (32, 32, 32, 4)
+    assert torch.equal(xg.cpu(), xc)
+    assert torch.equal(yg.cpu(), yc)
+
+
+def _train_pair(gpu, name, steps, lr=0.05):
+    """(native fp32 losses, torch fp32 losses, native model, torch model) from one init."""
+    import copy
+
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.optim.sgd import SGD
+    torch.manual_seed(4)
+    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None)
+    ref = copy.deepcopy(native).to(gpu)
+    ref.use_native = False
+    ddpx.prepare_model(native, gpu)
+    opt = SGD(native.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    ropt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    gen = torch.Generator().manual_seed(5)
+    ln, lt = [], []
+    for _ in range(steps):
+        x = torch.rand(64, 3, 32, 32, generator=gen).to(gpu)
+        y = torch.randint(0, 10, (64,), generator=gen).to(gpu)
+        opt.zero_grad()
+        loss, logits = native.forward_loss(x, y)
+        assert logits is None  # the native fp32 path ran
+        loss.backward()
+        opt.step()
+        ln.append(loss.item())
+        ropt.zero_grad()
+        rl = F.cross_entropy(ref(x), y)
+        rl.backward()
+        ropt.step()
+        lt.append(rl.item())
+    return ln, lt, native, ref
+
+
+@pytest.mark.parametrize("name", ["vgg", "mlp"])
+def test_native_fp32_gradients_match_torch_fp32(gpu, name):
+    """One backward from the same init and batch: every parameter gradient to fp32 round-off."""
+    import copy
+
+    import ddpx
+    from ddpx.models import build_model
+    torch.manual_seed(7)
+    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None)
+    ref = copy.deepcopy(native).to(gpu)
+    ref.use_native = False
+    flat = ddpx.prepare_model(native, gpu)
+    x = torch.rand(64, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (64,), device=gpu)
+    flat.zero_grad()
+    loss, logits = native.forward_loss(x, y)
+    assert logits is None
+    loss.backward()
+    rl = F.cross_entropy(ref(x), y)
+    rl.backward()
+    assert abs(loss.item() - rl.item()) < 1e-5
+    # fp64 on the CPU is the arbiter: gradients that cancel over 65K pixels (conv0 after BatchNorm) differ
+    # between any two fp32 summation orders by more than the usual 1e-5
+    r64 = copy.deepcopy(ref).cpu().double()
+    r64.compute_dtype = torch.float64
+    r64.zero_grad()
+    F.cross_entropy(r64(x.cpu().double()), y.cpu()).backward()
+    rp, p64 = dict(ref.named_parameters()), dict(r64.named_parameters())
+    # Below a 2x2 max-pool, a gradient moves by ~2e-3 when a handful of the 131K windows route to another
+    # element because two candidates lie within fp32 round-off of each other (measured: 3 flips -> 8e-3
+    # before the blocked-summation GEMM, tools/dbg_f32_vgg.py); torch's own fp32 path lands at 1e-3..2.3e-3
+    # on this batch.  Above the last pooling decision (bn7, classifier) the gradients are exact to 1e-5.
+    bad = []
+    for n, p in native.named_parameters():
+        e_native, e_torch = _rel(p.main_grad.cpu(), p64[n].grad), _rel(rp[n].grad.cpu(), p64[n].grad)
+        print(f"{n}: native {e_native:.2e} torch-fp32 {e_torch:.2e}")
+        top = name == "mlp" or n.startswith(("classifier", "backbone.bn7"))
+        if not e_native < (1e-5 if top else 5e-3):
+            bad.append((n, e_native, e_torch))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["vgg", "mlp"])
+def test_native_fp32_training_tracks_torch_fp32(gpu, name):
+    ln, lt, native, ref = _train_pair(gpu, name, steps=5, lr=0.01)
+    # exact-f32 kernels: the first loss agrees to round-off, later ones to fp32 trajectory drift
+    assert abs(ln[0] - lt[0]) < 1e-4 * max(1.0, abs(lt[0])), (ln, lt)
+    for a, b in zip(ln, lt):
+        assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (ln, lt)
+    sd, rsd = native.state_dict(), ref.state_dict()
+    assert sd.keys() == rsd.keys()
+    for k in sd:
+        if sd[k].is_floating_point():
+            # matrices relative; BatchNorm / bias vectors start at 0 or 1 and move by ~lr*grad, so absolute
+            err = (sd[k].double() - rsd[k].double()).norm().item()
+            assert err < 5e-3 * max(1.0, rsd[k].double().norm().item()), (k, err)
+
+
+def test_vgg_fp32_eval_logits(gpu):
+    from ddpx.models import build_model
+    import ddpx
+    torch.manual_seed(6)
+    m = build_model("vgg", dtype="fp32", device=gpu)
+    ddpx.prepare_model(m, gpu)
+    m.eval()
+    x = torch.rand(32, 3, 32, 32, device=gpu)
+    with torch.no_grad():
+        got = m(x)
+        m.use_native = False
+        want = m(x)
+    assert _rel(got, want) < 1e-4
