@@ -64,9 +64,11 @@ struct Comm {
   std::thread watchdog;
   std::atomic<bool> stop{false};
   std::atomic<int> error{0};  // 0 ok, 1 async nccl error, 2 timeout, 3 aborted
-  double timeout_s = 0.0;
-  bool track = false;
-  int action = ACT_EXIT;
+  // set by the owning thread (ddpx_comm_set_timeout), read by the watchdog: atomics (a host ThreadSanitizer
+  // run of csrc/tests/rt_sanitize.cpp flagged the plain fields as a data race)
+  std::atomic<double> timeout_s{0.0};
+  std::atomic<bool> track{false};
+  std::atomic<int> action{ACT_EXIT};
   double exit_grace_s = 10.0;
   std::atomic<long long> tracked{0};  // operations / graph replays registered with the watchdog
 };
@@ -133,7 +135,8 @@ void watchdog_loop(Comm* c) {
           continue;
         }
         const double age = std::chrono::duration<double>(Clock::now() - p.t0).count();
-        if (c->timeout_s > 0 && age > c->timeout_s) {
+        const double to = c->timeout_s.load();
+        if (to > 0 && age > to) {
           memcpy(late, p.what, sizeof(late));
           late_age = age;
         }
@@ -142,7 +145,7 @@ void watchdog_loop(Comm* c) {
     }
     if (late[0]) {
       fprintf(stderr, "[ddpx rank %d] collective '%s' timed out: not complete after %.1fs (timeout %.1fs)\n",
-              c->rank, late, late_age, c->timeout_s);
+              c->rank, late, late_age, c->timeout_s.load());
       fflush(stderr);
       on_failure(c, 2, "collective timed out");
     }
@@ -300,15 +303,19 @@ DDPX_API int ddpx_comm_destroy(void* h, int abort) {
   c->stop.store(true);
   if (c->watchdog.joinable()) c->watchdog.join();
   int e = 0;
-  std::lock_guard<std::mutex> g(c->issue_mu);
-  if (c->nccl && !c->aborted.load()) {
-    if (abort || c->error.load()) e = check(ncclCommAbort(c->nccl));
-    else {
-      hipStreamSynchronize(c->stream);
-      e = check(ncclCommDestroy(c->nccl));
+  {
+    // scoped: the guard must release issue_mu before `delete c` destroys it (the host ThreadSanitizer
+    // harness csrc/tests/rt_sanitize.cpp caught the unlock-after-free of the unscoped guard)
+    std::lock_guard<std::mutex> g(c->issue_mu);
+    if (c->nccl && !c->aborted.load()) {
+      if (abort || c->error.load()) e = check(ncclCommAbort(c->nccl));
+      else {
+        hipStreamSynchronize(c->stream);
+        e = check(ncclCommDestroy(c->nccl));
+      }
     }
+    c->nccl = nullptr;
   }
-  c->nccl = nullptr;
   for (auto& p : c->pending) hipEventDestroy(p.ev);
   for (auto ev : c->free_events) hipEventDestroy(ev);
   hipStreamDestroy(c->stream);
