@@ -31,7 +31,10 @@ constexpr int ACC_BYTES = BM * ALD * 4;
 constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES;  // 138 KiB: one workgroup per CU
 constexpr int VPT = BM * BN / 4 / 256;                    // f32x4 vectors per stream thread per tile (8)
 
-__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
+// Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
+// independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
+// boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
+__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -40,31 +43,43 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_m = p.M / BM;
-  const int ntiles = tiles_m * (p.N / BN);
+  const int tiles_m0 = p0.M / BM, tiles_m1 = p1.M / BM;
+  const int nt0 = tiles_m0 * (p0.N / BN);
+  const int ntiles = nt0 + nt1;
   const int nt = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= ntiles)
-  const int nk = p.K / 64;
-  auto tile_origin = [&](int i, int& m0, int& n0) {
-    const int g = (int)blockIdx.x + i * (int)gridDim.x;
-    m0 = (g % tiles_m) * BM;
-    n0 = (g / tiles_m) * BN;
+  const int nk = p0.K / 64;
+  // tile i of this workgroup: origin and which GEMM it belongs to (uniform per workgroup)
+  auto tile_origin = [&](int i, int& m0, int& n0) -> int {
+    int g = (int)blockIdx.x + i * (int)gridDim.x;
+    const int sel = g >= nt0;
+    if (sel) g -= nt0;
+    const int tm = sel ? tiles_m1 : tiles_m0;
+    m0 = (g % tm) * BM;
+    n0 = (g / tm) * BN;
+    return sel;
   };
+  const pipe::Params& p = p0;  // K, alpha, lr, momentum, wd: shared by both GEMMs
 
   if (wave < 4) {
     // ------------------------------------------------------------------ math waves
     const int wm = wave >> 1, wn = wave & 1;
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, p.a_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, p.b_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p0.A, 0, p0.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb0 = __builtin_amdgcn_make_buffer_rsrc((void*)p0.B, 0, p0.b_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)p1.A, 0, p1.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb1 = __builtin_amdgcn_make_buffer_rsrc((void*)p1.B, 0, p1.b_bytes, 0x00020000);
     for (int i = 0; i <= nt; ++i) {
       if (i == nt) {  // drain iteration: the stream waves finish the last tile
         for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
       } else {
         int m0, n0;
-        tile_origin(i, m0, n0);
+        const int sel = tile_origin(i, m0, n0);
+        const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0, rb = sel ? rb1 : rb0;
+        const int lda = sel ? p1.lda : p0.lda, ldb = sel ? p1.ldb : p0.ldb;
+        const int Mg = sel ? p1.M : p0.M, Ng = sel ? p1.N : p0.N;
         auto issue = [&](int t) {
           char* slot = smem + (t % STAGES) * SLOT;
-          pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, p.lda, m0, p.M, t * 64, p.K, wave, lane);
-          pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, p.ldb, n0, p.N, t * 64, p.K,
+          pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, t * 64, p.K, wave, lane);
+          pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, t * 64, p.K,
                                                            wave, lane);
         };
         f32x4 acc[FM][FN];
@@ -122,16 +137,18 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
     f32x4 pc[VPT], mc[VPT], pn[VPT], mn[VPT];
     auto load_tile = [&](int i, f32x4 (&pv)[VPT], f32x4 (&mv)[VPT]) {
       int m0, n0;
-      tile_origin(i, m0, n0);
+      const int sel = tile_origin(i, m0, n0);
+      const SgdArgs& sg = sel ? p1.sgd : p0.sgd;
+      const int ldc = sel ? p1.ldc : p0.ldc;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const size_t off = (size_t)(m0 + row0 + 8 * v) * p.ldc + n0 + col;
-        pv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.p + off));
-        mv[v] = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p.sgd.buf + off))
+        const size_t off = (size_t)(m0 + row0 + 8 * v) * ldc + n0 + col;
+        pv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.p + off));
+        mv[v] = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.buf + off))
                         : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     };
-    int pm0 = 0, pn0 = 0;  // origin of the tile being updated (i - 1)
+    int pm0 = 0, pn0 = 0, psel = 0;  // origin / GEMM of the tile being updated (i - 1)
     for (int i = 0; i <= nt; ++i) {
       if (i < nt) load_tile(i, pn, mn);  // one iteration ahead of its update
       const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
@@ -154,11 +171,12 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
             }
             po[q] = fmaf(-lr, d, pc[v][q]);
           }
-          const size_t off = (size_t)(pm0 + row0 + 8 * v) * p.ldc + pn0 + col;
-          __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(p.sgd.p + off));
-          if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(p.sgd.buf + off));
-          if (p.sgd.shadow)
-            *reinterpret_cast<u32x2*>(p.sgd.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+          const SgdArgs& sg = psel ? p1.sgd : p0.sgd;
+          const size_t off = (size_t)(pm0 + row0 + 8 * v) * (psel ? p1.ldc : p0.ldc) + pn0 + col;
+          __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(sg.p + off));
+          if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sg.buf + off));
+          if (sg.shadow)
+            *reinterpret_cast<u32x2*>(sg.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -169,7 +187,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p) {
           pc[v] = pn[v];
           mc[v] = mn[v];
         }
-        tile_origin(i, pm0, pn0);
+        psel = tile_origin(i, pm0, pn0);
       }
     }
   }
@@ -185,7 +203,21 @@ static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
 static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p);
+  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p, p, 0);
+  return hipGetLastError();
+}
+
+// Both weight gradients (+ their SGD updates) in one launch; the caller checked eligible() for both and equal
+// K / alpha / lr / momentum / wd (pair_compatible).
+static inline bool pair_compatible(const pipe::Params& a, const pipe::Params& b) {
+  return a.K == b.K && a.alpha == b.alpha && a.sgd.lr == b.sgd.lr && a.sgd.mom == b.sgd.mom && a.sgd.wd == b.sgd.wd;
+}
+
+static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params& p1, int num_cus, hipStream_t s) {
+  const int nt1 = (p1.M / BM) * (p1.N / BN);
+  const int ntiles = (p0.M / BM) * (p0.N / BN) + nt1;
+  const int grid = ntiles < num_cus ? ntiles : num_cus;
+  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
   return hipGetLastError();
 }
 

@@ -253,3 +253,34 @@ def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-
     out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     return gemm_raw(a, b, out, M=M, N=N, K=K, lda=a.stride(0), ldb=b.stride(0), ldc=N, a_kcontig=a_kcontig,
                     b_kcontig=b_kcontig, epi=epi, tile=tile, impl=impl)
+
+
+native.register_kernel_sig("ddpx_wgrad_sgd_pair", native.c_int, *([native.c_void_p, native.c_void_p] + [native.c_int] * 5
+                                                                  + [native.c_void_p] * 3) * 2,
+                           native.c_int, native.c_void_p, native.c_float, native.c_float, native.c_void_p)
+
+
+def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1) -> bool:
+    """Both fused weight-gradient + SGD updates (dW_i = dy_iᵀ x_i applied to sgd_i's parameter) in ONE
+    warp-specialised launch.  False (nothing launched) when the pair is not eligible; the caller then
+    issues them one by one with :func:`linear_wgrad`."""
+    for t, n in ((dy0, "dy0"), (x0, "x0"), (dy1, "dy1"), (x1, "x1")):
+        _check_bf16_2d(t, n)
+    if dy0.shape[0] != dy1.shape[0] or x0.shape[0] != dy0.shape[0] or x1.shape[0] != dy1.shape[0]:
+        return False
+    if sgd0[3] is not sgd1[3] or sgd0[4] != sgd1[4] or sgd0[5] != sgd1[5]:
+        return False  # lr tensor, momentum, weight decay must be shared
+    K = dy0.shape[0]
+    args = []
+    for dy, x, sg in ((dy0, x0, sgd0), (dy1, x1, sgd1)):
+        M, N = dy.shape[1], x.shape[1]
+        _req(sg[0].numel() == M * N, "sgd target size mismatch")
+        args += [dy.data_ptr(), x.data_ptr(), M, N, dy.stride(0), x.stride(0), N, sg[0].data_ptr(),
+                 native.ptr(sg[1]), native.ptr(sg[2])]
+    lr = sg[3]
+    rc = native.kernels().ddpx_wgrad_sgd_pair(*args, K, lr.data_ptr(), float(sgd0[4]), float(sgd0[5]),
+                                              native.stream_handle())
+    if rc == -20:
+        return False
+    native.check(rc, "ddpx_wgrad_sgd_pair")
+    return True

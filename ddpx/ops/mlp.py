@@ -20,11 +20,16 @@ The data-gradient GEMM stays bf16.  Master weights, gradients and SGD are unchan
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import gemm as G
 from ..optim.sgd import take_lr_advance
 from .head import head_backward, head_forward
+
+# DDPX_WGRAD_PAIR=0: launch the last two layers' fused weight-gradient + SGD kernels one by one
+_PAIR_WGRAD = os.environ.get("DDPX_WGRAD_PAIR", "1") != "0"
 
 
 def _to_bf16_2d(x):
@@ -117,6 +122,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                       sgd_w=flat.fused_spec(wl), sgd_b=flat.fused_spec(bl), sgd_prev=flat.fused_spec(bprev))
         for p in (wl, bl, bprev):
             flat.mark_updated(p)
+        deferred = None  # layer 1's update, launched together with layer 0's (one warp-specialised launch)
         for l in range(L - 1, -1, -1):
             w, _ = ps[l]
             dnext = None
@@ -124,7 +130,17 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                 bp = ps[l - 1][1]
                 dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
                 flat.mark_updated(bp)
-            _wgrad(saved8, l, dpre, hs[l], None, sgd=flat.fused_spec(w))
+            if l == 1 and not saved8 and _PAIR_WGRAD:
+                deferred = (dpre, hs[1], flat.fused_spec(w), w)
+            elif l == 0 and deferred is not None:
+                d1, h1, s1, w1 = deferred
+                s0 = flat.fused_spec(w)
+                if not G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0):
+                    G.linear_wgrad(d1, h1, None, sgd=s1)
+                    _wgrad(saved8, 0, dpre, hs[0], None, sgd=s0)
+                flat.mark_updated(w1)
+            else:
+                _wgrad(saved8, l, dpre, hs[l], None, sgd=flat.fused_spec(w))
             flat.mark_updated(w)
             dpre = dnext
         return

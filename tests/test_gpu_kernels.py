@@ -409,3 +409,32 @@ def test_wgrad_sgd_warp_specialised_matches_unfused(gpu, M, N, K, mom):
     assert torch.equal(sa, sb)
     if mom:
         assert torch.equal(ba, bb)
+
+
+@pytest.mark.parametrize("mom", [0.9, 0.0])
+def test_wgrad_sgd_pair_matches_single_launches(gpu, mom):
+    """Two fused weight-gradient + SGD updates in ONE warp-specialised launch (the toy MLP's fc1 + fc0)
+    == the same two updates launched one by one, bit for bit (master, momentum, shadow)."""
+    from ddpx.ops import gemm as G
+    torch.manual_seed(10)
+    K = 512
+    shapes = [(256, 512), (128, 384)]  # (M_out, N_in) of the two layers
+    dys = [_rand_bf16(K, m, dev=gpu) for m, _ in shapes]
+    xs = [_rand_bf16(K, n, dev=gpu) for _, n in shapes]
+    lr = torch.full((), 0.05, device=gpu)
+    init = [(torch.randn(m * n, device=gpu) * 0.02, torch.randn(m * n, device=gpu) * 0.01) for m, n in shapes]
+
+    def state():
+        return [(p.clone(), b.clone(), torch.empty(p.numel(), dtype=torch.bfloat16, device=gpu)) for p, b in init]
+
+    sa, sb = state(), state()
+    specs = [(p, b if mom else None, s, lr, mom, 5e-4) for p, b, s in sa]
+    assert G.wgrad_sgd_pair(dys[0], xs[0], specs[0], dys[1], xs[1], specs[1])
+    for dy, x, (p, b, s) in zip(dys, xs, sb):
+        G.linear_wgrad(dy, x, None, sgd=(p, b if mom else None, s, lr, mom, 5e-4))
+    torch.cuda.synchronize()
+    for (pa, ba, sha), (pb, bb, shb) in zip(sa, sb):
+        assert torch.equal(pa, pb)
+        assert torch.equal(sha, shb)
+        if mom:
+            assert torch.equal(ba, bb)
