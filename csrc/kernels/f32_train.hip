@@ -60,7 +60,7 @@ __device__ __forceinline__ f32x4 load4(const Operand& X, int o, int k, int kend)
   return im2col4(X, k, o);
 }
 
-constexpr int BK = 16, PAD = 20, NT = 256;
+constexpr int BK = 16, PAD = 20, NT = 256;  // Stage<KC> maps 4 float4 per row: BK is 16
 
 template <int MODE, int BO>
 struct Stage {
@@ -495,24 +495,34 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restric
   dx[i] = g[n * C + c] / (float)S;
 }
 
-// logits[m][j] = h[m] . w[j] + bias[j]   (one thread per logit; the 10-class head is far below MFMA size)
+// logits[m][j] = h[m] . w[j] + bias[j]: one wave per row, lanes stride K with 16-B loads and keep all NC (<= 16)
+// class sums, then one wave reduction per class (the head is far below MFMA size; h is read once).
+constexpr int kMaxNC = 16;
 __global__ void __launch_bounds__(256) head_logits_kernel(const float* __restrict__ h, const float* __restrict__ w,
                                                            const float* __restrict__ bias, int M, int K, int NC,
                                                            float* __restrict__ logits) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= M * NC) return;
-  const int m = i / NC, j = i % NC;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float acc[kMaxNC];
+#pragma unroll
+  for (int j = 0; j < kMaxNC; ++j) acc[j] = 0.f;
   const f32x4* hp = reinterpret_cast<const f32x4*>(h + (size_t)m * K);
-  const f32x4* wp = reinterpret_cast<const f32x4*>(w + (size_t)j * K);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  for (int k = 0; k < K / 4; ++k) {
-    const f32x4 x = hp[k], y = wp[k];
-    s0 = fmaf(x[0], y[0], s0);
-    s1 = fmaf(x[1], y[1], s1);
-    s2 = fmaf(x[2], y[2], s2);
-    s3 = fmaf(x[3], y[3], s3);
+  for (int k4 = lane; k4 < K / 4; k4 += 64) {
+    const f32x4 x = hp[k4];
+#pragma unroll
+    for (int j = 0; j < kMaxNC; ++j) {
+      if (j >= NC) break;
+      const f32x4 y = reinterpret_cast<const f32x4*>(w + (size_t)j * K)[k4];
+      acc[j] = fmaf(x[0], y[0], fmaf(x[1], y[1], fmaf(x[2], y[2], fmaf(x[3], y[3], acc[j]))));
+    }
   }
-  logits[i] = (s0 + s1) + (s2 + s3) + bias[j];
+#pragma unroll
+  for (int j = 0; j < kMaxNC; ++j) {
+    if (j >= NC) break;
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) logits[(size_t)m * NC + j] = v + bias[j];
+  }
 }
 
 // One workgroup: per-row log-softmax, loss = mean_m (lse - logit[target]), dl = (softmax - onehot) / M.
@@ -544,24 +554,46 @@ __global__ void __launch_bounds__(1024) xent_kernel(const float* __restrict__ lo
 }
 
 // dW[j][k] (+)= go * sum_m dl[m][j] h[m][k];  db[j] (+)= go * sum_m dl[m][j]
-__global__ void __launch_bounds__(256) head_wgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
-                                                          const float* __restrict__ h, int M, int K, int NC,
-                                                          float* __restrict__ dW, float* __restrict__ db,
-                                                          int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+// Workgroups of 64 columns k x 16 row groups (h read once, coalesced; all NC classes per thread), fixed-order
+// LDS reduction over the row groups; the last workgroup also sums db (one wave per class).
+__global__ void __launch_bounds__(1024) head_wgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
+                                                           const float* __restrict__ h, int M, int K, int NC,
+                                                           float* __restrict__ dW, float* __restrict__ db,
+                                                           int accumulate) {
+  __shared__ float red[16][kMaxNC][64];
   const float s = go ? *go : 1.f;
-  if (i < NC * K) {
-    const int j = i / K, k = i % K;
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) acc = fmaf(dl[(size_t)m * NC + j], h[(size_t)m * K + k], acc);
-    acc *= s;
-    dW[i] = accumulate ? dW[i] + acc : acc;
-  } else if (i < NC * K + NC) {
-    const int j = i - NC * K;
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) acc += dl[(size_t)m * NC + j];
-    acc *= s;
-    db[j] = accumulate ? db[j] + acc : acc;
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  if (blockIdx.x == gridDim.x - 1) {  // bias gradient
+    if (g < NC && db) {
+      float acc = 0.f;
+      for (int m = cl; m < M; m += 64) acc += dl[(size_t)m * NC + g];
+      acc = wave_sum(acc) * s;
+      if (cl == 0) db[g] = accumulate ? db[g] + acc : acc;
+    }
+    return;
+  }
+  const int k = blockIdx.x * 64 + cl;
+  float acc[kMaxNC];
+#pragma unroll
+  for (int j = 0; j < kMaxNC; ++j) acc[j] = 0.f;
+  if (k < K)
+    for (int m = g; m < M; m += 16) {
+      const float hv = h[(size_t)m * K + k];
+#pragma unroll
+      for (int j = 0; j < kMaxNC; ++j) {
+        if (j >= NC) break;
+        acc[j] = fmaf(dl[(size_t)m * NC + j], hv, acc[j]);
+      }
+    }
+#pragma unroll
+  for (int j = 0; j < kMaxNC; ++j) red[g][j][cl] = acc[j];
+  __syncthreads();
+  if (g < NC && k < K) {
+    float t = 0.f;
+    for (int q = 0; q < 16; ++q) t += red[q][g][cl];
+    t *= s;
+    const size_t o = (size_t)g * K + k;
+    dW[o] = accumulate ? dW[o] + t : t;
   }
 }
 
@@ -580,14 +612,22 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const float* __restrict
   dh[i] = acc;
 }
 
-// out[n] (+)= sum_m x[m][n]
-__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ x, int M, int N,
-                                                      float* __restrict__ out, int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+// out[n] (+)= sum_m x[m][n]: workgroups of 64 columns x 16 row groups, fixed-order LDS reduction
+__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ x, int M, int N,
+                                                       float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + cl;
   float acc = 0.f;
-  for (int m = 0; m < M; ++m) acc += x[(size_t)m * N + n];
-  out[n] = accumulate ? out[n] + acc : acc;
+  if (n < N)
+    for (int m = g; m < M; m += 16) acc += x[(size_t)m * N + n];
+  red[g][cl] = acc;
+  __syncthreads();
+  if (g == 0 && n < N) {
+    float t = 0.f;
+    for (int q = 0; q < 16; ++q) t += red[q][cl];
+    out[n] = accumulate ? out[n] + t : t;
+  }
 }
 
 static int ilog2(int v) {
@@ -730,21 +770,23 @@ DDPX_API int ddpx_f32_avgpool(const float* x, int N, int S, int C, float* out, i
 DDPX_API int ddpx_f32_head_fwd(const float* h, const float* w, const float* bias, const int64_t* tgt, int M, int K,
                                int NC, float* logits, float* loss, float* dl, hipStream_t s) {
   if (K % 4) return -1;
-  hipLaunchKernelGGL(head_logits_kernel, dim3(nblk((long)M * NC)), dim3(256), 0, s, h, w, bias, M, K, NC, logits);
+  if (NC > kMaxNC) return -2;
+  hipLaunchKernelGGL(head_logits_kernel, dim3(nblk(M, 4)), dim3(256), 0, s, h, w, bias, M, K, NC, logits);
   if (tgt) hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(1024), 0, s, logits, tgt, M, NC, loss, dl);
   return (int)hipGetLastError();
 }
 
 DDPX_API int ddpx_f32_head_bwd(const float* dl, const float* go, const float* h, const float* w, int M, int K, int NC,
                                float* dW, float* db, int accumulate, float* dh, int relu_mask, hipStream_t s) {
-  if (dW) hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk((long)NC * K + NC)), dim3(256), 0, s, dl, go, h, M, K, NC,
-                             dW, db, accumulate);
+  if (NC > kMaxNC) return -2;
+  if (dW) hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk(K, 64) + 1), dim3(1024), 0, s, dl, go, h, M, K, NC, dW, db,
+                             accumulate);
   if (dh) hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
                              relu_mask, dh);
   return (int)hipGetLastError();
 }
 
 DDPX_API int ddpx_f32_colsum(const float* x, int M, int N, float* out, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3(nblk(N)), dim3(256), 0, s, x, M, N, out, accumulate);
+  hipLaunchKernelGGL(colsum_kernel, dim3(nblk(N, 64)), dim3(1024), 0, s, x, M, N, out, accumulate);
   return (int)hipGetLastError();
 }
