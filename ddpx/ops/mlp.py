@@ -12,8 +12,8 @@ its DDP bucket slice, then announced to the reducer):
 The weight gradient of a layer is issued BEFORE its data gradient so the
 bucket holding it starts its all-reduce while the next GEMMs run.
 
-``model.fp8`` (the wide-MLP config, BASELINE.json configs[4]): the hidden layers' forward and
-weight-gradient GEMMs run on MX-FP8 (``ddpx.ops.fp8``: e4m3 activations, weights and output
+``model.fp8`` (the wide-MLP config, BASELINE.json configs[4]): the hidden layers' forward (and, with
+``DDPX_FP8_WGRAD=1``, weight-gradient) GEMMs run on MX-FP8 (``ddpx.ops.fp8``: e4m3 activations, weights and output
 gradients, E8M0 block-32 scales applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4``); the
 forward quantises each input both row-wise (its GEMM) and transposed (the later wgrad's B operand).
 The data-gradient GEMM stays bf16.  Master weights, gradients and SGD are unchanged (fp32).
@@ -30,6 +30,8 @@ from .head import head_backward, head_forward
 
 # DDPX_WGRAD_PAIR=0: launch the last two layers' fused weight-gradient + SGD kernels one by one
 _PAIR_WGRAD = os.environ.get("DDPX_WGRAD_PAIR", "1") != "0"
+# DDPX_FP8_WGRAD=1: MX-FP8 weight-gradient GEMMs too (default: MX-FP8 forward GEMMs, bf16 backward)
+_FP8_WGRAD = os.environ.get("DDPX_FP8_WGRAD", "0") == "1"
 
 
 def _to_bf16_2d(x):
@@ -59,7 +61,10 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
     fp8 = _fp8_ok(model, x)
     if for_backward is None:
         for_backward = want_grad
-    saved8 = [] if (fp8 and for_backward) else None
+    # the backward's weight-gradient GEMMs stay bf16 unless DDPX_FP8_WGRAD=1: single-process, the fused
+    # bf16 weight-gradient + SGD pair hides those GEMMs under the optimizer's HBM stream, which the fp8
+    # GEMM's per-tile SGD epilogue cannot (profiles/r2_fp8)
+    saved8 = [] if (fp8 and for_backward and _FP8_WGRAD) else None
     for (w, b) in ps[:-1]:
         rc = None if fp8 else flat.chunks_of(w)
         if rc is not None:
@@ -75,7 +80,7 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
         flat.before_read(w)
         if fp8:
             from . import fp8 as F8
-            if for_backward:
+            if saved8 is not None:
                 hq, hqt = F8.quant(hs[-1], F8.E4M3, rows=True, cols=True)
                 saved8.append(hqt)
             else:

@@ -95,10 +95,14 @@ def test_mx_gemm_sgd_epilogue(gpu):
     assert torch.equal(sh, p.to(torch.bfloat16))
 
 
-def test_mlp_fp8_step_tracks_bf16(gpu):
-    """A whole MX-FP8 MLP training step (fwd + wgrad in fp8) stays close to the bf16 step."""
+@pytest.mark.parametrize("wgrad8", [False, True])
+def test_mlp_fp8_step_tracks_bf16(gpu, wgrad8, monkeypatch):
+    """A whole MX-FP8 MLP training step (fp8 forward; fp8 weight gradients too with DDPX_FP8_WGRAD) stays
+    close to the bf16 step."""
     import ddpx
     from ddpx.models import MLP
+    from ddpx.ops import mlp as mlp_ops
+    monkeypatch.setattr(mlp_ops, "_FP8_WGRAD", wgrad8)
     torch.manual_seed(4)
     a, b = MLP(hidden=1024), MLP(hidden=1024)
     b.load_state_dict(a.state_dict())
