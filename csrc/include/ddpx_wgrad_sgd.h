@@ -19,22 +19,35 @@
 // The update arithmetic is sgd_apply's fma sequence: bitwise equal to the stored-gradient + flat-SGD path.
 #pragma once
 
+#include <cstdlib>
+
 #include "ddpx_pipe.h"
 
 namespace ddpx {
 namespace wsgd {
 
-constexpr int BM = 64, BN = 128, STAGES = 3;
-constexpr int ALD = BN + 4;  // LDS tile-buffer row stride (floats)
+constexpr int BM = 64, BN = 128;
 constexpr int A_SUB = BM * 64 * 2, B_SUB = BN * 64 * 2, SLOT = A_SUB + B_SUB;
-constexpr int ACC_BYTES = BM * ALD * 4;
-constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES;  // 138 KiB: one workgroup per CU
-constexpr int VPT = BM * BN / 4 / 256;                    // f32x4 vectors per stream thread per tile (8)
+constexpr int VPT = BM * BN / 4 / 256;  // f32x4 vectors per stream thread per tile (8)
+// STAGES-deep LDS-DMA ring for the math waves + two fp32 tile buffers (math -> stream hand-off).
+//   3 stages: row stride BN + 4 (conflict-free accumulator stores), 138 KiB;
+//   4 stages: one more 24 KiB stage in flight (the math side's K-steps are L2->LDS latency bound with
+//             only 4 DMA-issuing waves), which fits the 160 KiB LDS only with unpadded rows (4-way
+//             conflicts on the once-per-tile accumulator store).
+template <int STAGES>
+struct Cfg {
+  static constexpr int ALD = STAGES >= 4 ? BN : BN + 4;
+  static constexpr int ACC_BYTES = BM * ALD * 4;
+  static constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
 
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
+template <int STAGES>
 __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
+  constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -92,7 +105,9 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
           if (s < nk) issue(s);
         for (int t = 0; t < nk; ++t) {
           const int ahead = min(STAGES - 2, nk - 1 - t);
-          if (ahead >= 1) pipe::wait_vmcnt<LPW>();
+          // stage t landed: everything but the (up to STAGES - 2) younger stages' DMAs
+          if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LPW>();
+          else if (ahead >= 1) pipe::wait_vmcnt<LPW>();
           else pipe::wait_vmcnt<0>();
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -200,10 +215,22 @@ static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
          p.sgd.p && p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf);
 }
 
+// Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:
+// 2.434 vs 2.469 ms/step) and 3 below (toy MLP, 14 tiles per CU: 0.2398 vs 0.2502 ms/step; profiles/r2_stages).
+static inline int stages(long long ntiles = 0, int num_cus = 256) {
+  static const int forced = [] {
+    const char* e = getenv("DDPX_WSGD_STAGES");
+    return e && e[0] == '3' ? 3 : (e && e[0] == '4' ? 4 : 0);
+  }();
+  if (forced) return forced;
+  return ntiles >= 64LL * num_cus ? 4 : 3;
+}
+
 static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p, p, 0);
+  if (stages(ntiles, num_cus) == 4) hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p, p, 0);
+  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p, p, 0);
   return hipGetLastError();
 }
 
@@ -217,7 +244,9 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int nt1 = (p1.M / BM) * (p1.N / BN);
   const int ntiles = (p0.M / BM) * (p0.N / BN) + nt1;
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  hipLaunchKernelGGL(wgrad_sgd_ws_kernel, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
+  if (stages(ntiles, num_cus) == 4)
+    hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
+  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
   return hipGetLastError();
 }
 
