@@ -46,7 +46,7 @@ struct Cfg {
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
 template <int STAGES>
-__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
+__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int spread) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
@@ -171,7 +171,10 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
         __builtin_amdgcn_s_barrier();
         if (i == 0) continue;
         // this K-step's share of tile i-1's update
-        const int v0 = t * VPT / nk, v1 = (t + 1) * VPT / nk;
+        // spread = 1: one share per K-step; spread = s > 1: the update in the first ceil(nk / s) K-steps
+        // (more stores in flight early in the tile period)
+        const int nks = (nk + spread - 1) / spread;
+        const int v0 = t < nks ? t * VPT / nks : VPT, v1 = t < nks ? (t + 1) * VPT / nks : VPT;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
           if (v < v0 || v >= v1) continue;
@@ -226,11 +229,22 @@ static inline int stages(long long ntiles = 0, int num_cus = 256) {
   return ntiles >= 64LL * num_cus ? 4 : 3;
 }
 
+// DDPX_WSGD_SPREAD=s: the stream waves update each tile in the first ceil(nk / s) K-steps (default 1: one
+// share per K-step; front-loading measured slower, profiles/r2_spread)
+static inline int spread() {
+  static const int v = [] {
+    const char* e = getenv("DDPX_WSGD_SPREAD");
+    const int x = e ? atoi(e) : 1;
+    return x >= 1 ? x : 1;
+  }();
+  return v;
+}
+
 static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  if (stages(ntiles, num_cus) == 4) hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p, p, 0);
-  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p, p, 0);
+  if (stages(ntiles, num_cus) == 4) hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p, p, 0, spread());
   return hipGetLastError();
 }
 
@@ -245,8 +259,8 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int ntiles = (p0.M / BM) * (p0.N / BN) + nt1;
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   if (stages(ntiles, num_cus) == 4)
-    hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
-  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p0, p1, nt1);
+    hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
   return hipGetLastError();
 }
 
