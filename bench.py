@@ -15,16 +15,23 @@ Weak scaling: per-GPU batch fixed as N grows.
     python bench.py --gpus 2 --comm host         # 2 ranks sharing ONE GPU (logic rehearsal, not perf)
     python bench.py --device cpu [--gpus 2]      # BASELINE config 1 (CPU, gloo for N > 1)
 
-N > 1 runs the stock DDP algorithm (reference ``multigpu.py:89``): every rank keeps the full fp32
-replica, gradients are averaged with an fp32 RCCL all-reduce (``ncclAvg``) bucket by bucket while
-backward runs, and each bucket's SGD update starts as soon as its all-reduce lands.  bf16 gradient
-communication (``--grad_dtype bf16``) and ZeRO-1 (``--shard_optimizer 1``) are opt-in and are labelled
-in the output line.
+N > 1 averages fp32 gradients across ranks bucket by bucket while backward runs (reference
+``multigpu.py:89``).  Before the first step the gradient-communication plan is calibrated on the node's own
+links (``ddpx.parallel.calibrate``; ``--bucket_plan default`` skips it): the collective sequence of every
+candidate — fp32 all-reduce per bucket with torch's greedy size rule at several caps (replicated optimizer,
+stock DDP), or fp32 reduce-scatter + bf16 shadow all-gather per bucket (ZeRO-1: same fp32 gradients and
+update, 0.75x the bytes, 1/N of the optimizer stream per rank) — is timed and rank 0's choice is used by
+every rank; the line reports the plan and every timing (``bucket_plan``, ``calibration``).  bf16 gradient
+communication (``--grad_dtype bf16``) is opt-in only.
 
 Every timed step does the whole job: batch gather+augment, forward, loss, backward, bucketed gradient
-all-reduce (N > 1), optimizer step and LR update.  ``--impl torch`` runs the stock PyTorch-ROCm recipe
-(nn.Linear + autocast, torch DDP over RCCL, foreach SGD) on the same data; at N = 1 the ddpx line also
-carries that recipe measured in the same process (``stock_same_run``).
+communication (N > 1), optimizer step and LR update.  The step is captured in a HIP graph; if capture fails
+on any rank (agreed over the CPU group) every rank continues eagerly in the same process and the line says
+so (``graph``: false, ``graph_error``).  After the timed region the replicas' fp32 master weights and
+optimizer state are compared byte for byte (SHA-256 digests, ``replicas_consistent``), and the stock
+PyTorch-ROCm recipe (nn.Linear + autocast + foreach SGD, torch DDP over its own RCCL group at N > 1) is
+timed in the same job on the same data (``stock_same_run``, ``vs_stock_same_run``).  ``--impl torch`` runs
+only the stock recipe.
 """
 from __future__ import annotations
 
@@ -65,14 +72,20 @@ def parse(argv=None):
     p.add_argument("--overlap_optimizer", type=int, default=None,
                    help="1: per-bucket optimizer as each collective lands (default 1 for N>1)")
     p.add_argument("--shard_optimizer", type=int, default=None,
-                   help="1: ZeRO-1 reduce-scatter / shard update / all-gather (opt-in, default 0)")
+                   help="1: ZeRO-1 reduce-scatter / shard update / all-gather; default: chosen by the start-up "
+                        "calibration at N > 1 (--bucket_plan calibrated), else 0")
     p.add_argument("--no_fused_optimizer", action="store_true", help="N=1: separate SGD pass instead of fused")
     p.add_argument("--fused_optimizer", type=int, default=None,
                    help="N=1: 1 = SGD inside the backward kernels (default), 0 = fp32 gradients then one "
                         "non-temporal flat SGD pass")
     p.add_argument("--grad_dtype", default="auto", choices=["auto", "fp32", "bf16"],
                    help="gradient buffer / all-reduce dtype; auto = fp32 at every N (stock DDP precision)")
-    p.add_argument("--bucket_cap_mb", type=float, default=25.0)
+    p.add_argument("--bucket_cap_mb", type=float, default=None,
+                   help="DDP bucket cap (default: calibrated on this node at N > 1, else torch's 25)")
+    p.add_argument("--bucket_plan", default="calibrated", choices=["calibrated", "default"],
+                   help="N > 1: time every candidate gradient-communication plan (bucket caps; replicated "
+                        "all-reduce vs ZeRO-1 reduce-scatter + all-gather) on this node's links before the first "
+                        "step and use the fastest (ddpx.parallel.calibrate); default = torch's 25 / 1 MiB caps")
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this into row-chunk buckets, each reduced as soon as its "
                         "slice of the weight gradient is written (opt-in; default off)")
@@ -80,7 +93,7 @@ def parse(argv=None):
                    help="ZeRO-1 only: all-gathers issued at the start of the next step, waited per chunk")
     p.add_argument("--comm_side_optimizer", type=int, default=None,
                    help="ZeRO-1 only: shard updates on the RCCL stream behind each reduce-scatter")
-    p.add_argument("--first_bucket_mb", type=float, default=1.0)
+    p.add_argument("--first_bucket_mb", type=float, default=None)
     p.add_argument("--train_size", type=int, default=50000)
     p.add_argument("--json_out", default=None)
     p.add_argument("--ddp_single", action="store_true",
@@ -89,7 +102,8 @@ def parse(argv=None):
                    help="host: gloo-staged collectives so several ranks can share one GPU (logic rehearsal on a "
                         "1-GPU box; not graph-capturable, not a performance path)")
     p.add_argument("--stock_ref", type=int, default=None,
-                   help="1: also time the stock PyTorch recipe in this process (default 1 at N=1 on the GPU)")
+                   help="1: also time the stock PyTorch recipe (torch.nn + torch DDP over RCCL at N > 1) in this "
+                        "job, after the ddpx timing, on the same data (default 1)")
     p.add_argument("--stock_steps", type=int, default=30)
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args(argv)
@@ -200,8 +214,16 @@ def resolve_defaults(args, world):
         args.grad_dtype = "fp32"
     if args.overlap_optimizer is None:
         args.overlap_optimizer = int(multi)
-    if args.shard_optimizer is None:
-        args.shard_optimizer = 0  # ZeRO-1 is opt-in: the default is the replicated (stock DDP) optimizer
+    # N > 1 ddpx: bucket caps and replicated-vs-ZeRO-1 come from the start-up calibration unless given
+    args.calibrate = bool(world > 1 and args.impl == "ddpx" and args.bucket_plan == "calibrated"
+                          and (args.shard_optimizer is None or args.bucket_cap_mb is None
+                               or args.first_bucket_mb is None))
+    if args.shard_optimizer is None and not args.calibrate:
+        args.shard_optimizer = 0  # the replicated (stock DDP) optimizer
+    if args.bucket_cap_mb is None and not args.calibrate:
+        args.bucket_cap_mb = 25.0
+    if args.first_bucket_mb is None and not args.calibrate:
+        args.first_bucket_mb = 1.0
     if args.chunk_mb is None:
         args.chunk_mb = 0.0
     if args.fused_optimizer is None:
@@ -210,13 +232,19 @@ def resolve_defaults(args, world):
         args.fused_optimizer = 1
     if args.no_fused_optimizer:
         args.fused_optimizer = 0
+    resolve_zero_defaults(args)
+    if args.stock_ref is None:
+        args.stock_ref = int(args.impl == "ddpx" and not args.ddp_single and args.comm == "rccl")
+
+
+def resolve_zero_defaults(args):
+    """ZeRO-1 companions (known once shard_optimizer is: after the calibration at N > 1)."""
+    if args.shard_optimizer is None:
+        return
     if args.comm_side_optimizer is None:
         args.comm_side_optimizer = int(bool(args.shard_optimizer))
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
-    if args.stock_ref is None:
-        args.stock_ref = int(world == 1 and args.impl == "ddpx" and args.device == "cuda" and not args.ddp_single
-                             and args.comm == "rccl")
 
 
 def build_ddpx(args, device, world):
@@ -243,6 +271,23 @@ def build_ddpx(args, device, world):
             comm = TorchComm()
         else:
             comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
+        if getattr(args, "calibrate", False):
+            from ddpx.parallel.calibrate import calibrate
+            from ddpx.runtime.flat_params import flat_of
+            f = flat_of(model)
+            shadow_only = [id(p) in f.shadow_only for p in f.params]
+            allow = (args.shard_optimizer is None and f.shadow is not None and any(shadow_only)
+                     and args.comm == "rccl")
+            plan, table = calibrate(comm, list(f.numels), shadow_only, device, allow_shard=allow,
+                                    reps=1 if cpu else 3)
+            if args.shard_optimizer is None:
+                args.shard_optimizer = int(plan["shard"])
+            if args.bucket_cap_mb is None:
+                args.bucket_cap_mb = plan["bucket_cap_mb"]
+            if args.first_bucket_mb is None:
+                args.first_bucket_mb = plan["first_bucket_mb"]
+            args.calibration = {"chosen": plan["name"], "ms": table}
+            resolve_zero_defaults(args)
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
@@ -256,8 +301,9 @@ def build_ddpx(args, device, world):
     return model, net, opt, sched
 
 
-def build_torch(args, device, world):
-    """Stock PyTorch-ROCm recipe (the baseline to beat)."""
+def build_torch(args, device, world, group=None):
+    """Stock PyTorch-ROCm recipe (the baseline to beat): torch.nn model, torch DDP (over RCCL on the GPU,
+    ``group``: its process group) at N > 1, foreach SGD, LambdaLR."""
     import torch
     import torch.nn as nn
     from torch.nn.parallel import DistributedDataParallel as TDDP
@@ -276,19 +322,20 @@ def build_torch(args, device, world):
             if i < args.layers - 1:
                 layers.append(nn.ReLU())
         model = nn.Sequential(nn.Flatten(), *layers).to(device)
-    net = TDDP(model, device_ids=[device.index] if device.type == "cuda" else None) if world > 1 else model
+    net = (TDDP(model, device_ids=[device.index] if device.type == "cuda" else None, process_group=group)
+           if world > 1 else model)
     opt = torch.optim.SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, OneCycleLambda(resolve_steps_per_epoch("compat", 0, world > 1)))
     return model, net, opt, sched
 
 
-def torch_runner(args, device, world, loader, idx_all, full):
-    """Eager step loop of the stock recipe (and of the ddpx engine on the CPU)."""
+def torch_runner(args, device, world, loader, idx_all, full, group=None):
+    """Eager step loop of the stock recipe."""
     import torch
     bs = args.batch_size
     amp = (device.type == "cuda" and (args.model not in ("vgg", "deepnn") or args.torch_amp)
            and getattr(args, "dtype", "auto") != "fp32")
-    model, net, opt, sched = build_torch(args, device, world)
+    model, net, opt, sched = build_torch(args, device, world, group=group)
 
     def one_step(k):
         b = full[k % len(full)]
@@ -311,23 +358,55 @@ def torch_runner(args, device, world, loader, idx_all, full):
     return model, net, opt, sched, run
 
 
-def measure_stock_same_run(args, device, loader, idx_all, full):
-    """Stock PyTorch-ROCm recipe (nn.Linear + bf16 autocast + foreach SGD; fp32 without autocast when
-    --dtype fp32), same data, same process."""
+def measure_stock_same_run(args, device, world, rank, idx_all, full):
+    """The stock PyTorch-ROCm recipe timed in this job after the ddpx measurement, on the same data:
+    torch.nn model + bf16 autocast (fp32 when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its
+    own RCCL process group (the reference's ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same
+    timing rule as the ddpx line: barrier + synchronize on both sides, max over ranks.  Collective."""
     import torch
+    import torch.distributed as dist
     a = argparse.Namespace(**vars(args))
     a.impl, a.torch_amp = "torch", args.dtype != "fp32"
-    loader = make_data(a, device, 0, 1)  # the stock model's own (NCHW / flat fp32) input layout
-    _, _, _, _, run = torch_runner(a, device, 1, loader, idx_all, full)
+    cuda = device.type == "cuda"
+    loader = make_data(a, device, rank, world)  # the stock model's own (NCHW / flat fp32) input layout
+    group = dist.new_group(backend="nccl" if cuda else "gloo") if world > 1 else None
+    _, _, _, _, run = torch_runner(a, device, world, loader, idx_all, full, group=group)
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
     run(0, 5)
-    torch.cuda.synchronize()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
     t0 = time.perf_counter()
     run(5, args.stock_steps)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.stock_steps
-    return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(args.batch_size / dt, 2),
-            "recipe": "torch.nn + " + ("fp32" if args.dtype == "fp32" else "bf16 autocast") + " + foreach SGD",
-            "steps": args.stock_steps}
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.destroy_process_group(group)
+    dt /= args.stock_steps
+    recipe = "torch.nn + " + ("fp32" if args.dtype == "fp32" or not cuda else "bf16 autocast") + " + foreach SGD"
+    if world > 1:
+        recipe += " + torch DDP (" + ("RCCL" if cuda else "gloo") + ", 25/1 MiB buckets)"
+    return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(world * args.batch_size / dt, 2),
+            "recipe": recipe, "steps": args.stock_steps}
+
+
+def replica_digest(net):
+    """SHA-256 of this rank's fp32 master weights and optimizer state, byte for byte (after consolidate)."""
+    import hashlib
+    f = net.flat
+    h = hashlib.sha256()
+    for t in [f.master] + [f.state_tensors[k] for k in sorted(f.state_tensors)]:
+        h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
 
 
 def main(argv=None):
@@ -356,8 +435,9 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     net = model = None
+    runner = None
     if args.impl == "ddpx" and not cpu:
-        from ddpx.runtime.graphs import CapturedStep
+        from ddpx.runtime.graphs import CapturedStep, GraphedSteps
         model, net, opt, sched = build_ddpx(args, device, world)
         static_x, static_y = loader.make_batch(idx_all[:bs], 0)
 
@@ -384,7 +464,6 @@ def main(argv=None):
             opt.step()
             return loss
 
-        graphs = {}
         use_graph = not args.no_graph
         S = max(1, args.graph_steps) if use_graph else 1
 
@@ -395,29 +474,41 @@ def main(argv=None):
             return loss
 
         comm_obj = getattr(net, "comm", None)
+        snap = {}
+
+        def make_graphs():
+            # host-side step state a failed capture could leave half-done (restored by the fallback)
+            snap["ddp"] = net.iteration_state() if hasattr(net, "iteration_state") else None
+            snap["step_count"] = opt.step_count
+            g = {1: CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)}
+            if S > 1:
+                g[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)
+            return g
+
+        def fallback():
+            # nothing of the aborted capture ran on the device: put the host bookkeeping back to where the
+            # last eager step left it and continue eagerly (same process, same communicator)
+            torch.cuda.synchronize()
+            if snap.get("ddp") is not None:
+                net.restore_iteration_state(snap["ddp"])
+            opt.flat.pending_lr = None
+            opt.step_count = snap.get("step_count", opt.step_count)
+
+        def agree(ok):
+            if world == 1:
+                return ok
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)  # gloo group: CPU tensors
+            return bool(t.item())
+
+        runner = GraphedSteps(lambda: step_body(static_x, static_y), make_graphs, steps_per_graph=S,
+                              use_graph=use_graph, agree=agree, on_fallback=fallback,
+                              after=lambda m: [sched.step() for _ in range(m)])
 
         def run(k, n):
-            """Steps k .. k+n-1: eager for the first two (allocator / lazy-init warm-up), then replays of
-            an S-step graph and of a 1-step graph for the remainder."""
-            loss = None
-            while n > 0:
-                if not use_graph or k < 2:
-                    loss = step_body(static_x, static_y)
-                    m = 1
-                else:
-                    if not graphs:
-                        graphs[1] = CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True,
-                                                 comm=comm_obj)
-                        if S > 1:
-                            graphs[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True,
-                                                     comm=comm_obj)
-                    m = S if n >= S else 1
-                    loss = graphs[m]()
-                for _ in range(m):
-                    sched.step()
-                k += m
-                n -= m
-            return loss
+            """Steps k .. k+n-1: eager for the first two (allocator / lazy-init warm-up), then replays of an
+            S-step graph and of a 1-step graph for the remainder (eager if capture failed on any rank)."""
+            return runner.run(k, n)
     elif args.impl == "ddpx":  # CPU: the ddpx engine (flat store, flat SGD, DDP over gloo) on torch CPU kernels
         model, net, opt, sched = build_ddpx(args, device, world)
 
@@ -464,17 +555,16 @@ def main(argv=None):
     consistent = None
     buckets_mb = None
     if ddpx_ddp:
-        # outside the timed region: replicas must hold identical weights after K steps
+        # outside the timed region: replicas must hold bit-identical fp32 weights and optimizer state
         net.consolidate()
-        ck = [float(net.flat.master.double().sum().item()), float(net.flat.master.double().abs().sum().item())]
         allck = [None] * world
-        dist.all_gather_object(allck, ck)
+        dist.all_gather_object(allck, replica_digest(net))
         consistent = all(c == allck[0] for c in allck)
         esz = net.flat.grad.element_size()
         buckets_mb = [round((e - s) * esz / 2 ** 20, 3) for s, e in net.bucket_ranges]
     stock = None
-    if args.stock_ref and rank == 0 and not cpu:
-        stock = measure_stock_same_run(args, device, loader, idx_all, full)
+    if args.stock_ref:
+        stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
@@ -504,13 +594,17 @@ def main(argv=None):
                    "parallelism": f"dp{world}", "device": args.device, "impl": args.impl,
                    "launcher": os.environ.get(LAUNCHER_ENV, "torchrun/external" if world > 1 else "none"),
                    "comm": (args.comm if ddpx_ddp else None),
-                   "graph": (args.impl == "ddpx" and not args.no_graph),
-                   "graph_steps": (args.graph_steps if args.impl == "ddpx" and not args.no_graph else None),
+                   "graph": bool(runner is not None and runner.use_graph),
+                   "graph_steps": (args.graph_steps if (runner is not None and runner.use_graph) else None),
+                   "graph_error": (runner.graph_error if runner is not None else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
                        " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer
                                                   and not cpu) else ""),
                    "grad_comm": grad_comm, "grad_dtype": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "first_bucket_mb": args.first_bucket_mb,
+                   "bucket_plan": (("calibrated" if getattr(args, "calibration", None) else "explicit")
+                                   if ddpx_ddp else None),
+                   "calibration": getattr(args, "calibration", None),
                    "buckets_mb": buckets_mb, "chunk_mb": args.chunk_mb or None,
                    "sharded_optimizer": bool(args.shard_optimizer) if ddpx_ddp else None,
                    "defer_gather": bool(args.defer_gather) if (ddpx_ddp and args.shard_optimizer) else None,

@@ -51,19 +51,19 @@ def main():
     dy = rnd(B, H)
     dw1, dw2 = torch.empty(H, I, device=dev), torch.empty(H, H, device=dev)
     cases = {
-        "fwd1": (2 * B * H * I, lambda t, impl: G.gemm_raw(x, w1, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
+        "fwd1": (2 * B * H * I, lambda t: G.gemm_raw(x, w1, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
                  M=B, N=H, K=I, lda=I, ldb=I, ldc=H, a_kcontig=True, b_kcontig=True, epi=G.EPI_BIAS_RELU_BF16,
-                 bias=b, tile=t, impl=impl), lambda: torch.relu(torch.nn.functional.linear(x, w1, b.to(torch.bfloat16)))),
-        "fwd2": (2 * B * H * H, lambda t, impl: G.gemm_raw(h1, w2, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
+                 bias=b, tile=t), lambda: torch.relu(torch.nn.functional.linear(x, w1, b.to(torch.bfloat16)))),
+        "fwd2": (2 * B * H * H, lambda t: G.gemm_raw(h1, w2, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
                  M=B, N=H, K=H, lda=H, ldb=H, ldc=H, a_kcontig=True, b_kcontig=True, epi=G.EPI_BIAS_RELU_BF16,
-                 bias=b, tile=t, impl=impl), lambda: torch.relu(torch.nn.functional.linear(h1, w2, b.to(torch.bfloat16)))),
-        "dgrad2": (2 * B * H * H, lambda t, impl: G.gemm_raw(dy, w2, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
+                 bias=b, tile=t), lambda: torch.relu(torch.nn.functional.linear(h1, w2, b.to(torch.bfloat16)))),
+        "dgrad2": (2 * B * H * H, lambda t: G.gemm_raw(dy, w2, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
                    M=B, N=H, K=H, lda=H, ldb=H, ldc=H, a_kcontig=True, b_kcontig=False, epi=G.EPI_RELUMASK_BF16,
-                   aux=h1, ldaux=H, tile=t, impl=impl), lambda: (dy @ w2) * (h1 > 0)),
-        "wgrad1": (2 * B * H * I, lambda t, impl: G.gemm_raw(dy, x, dw1, M=H, N=I, K=B, lda=H, ldb=I, ldc=I,
-                   a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t, impl=impl), lambda: dy.t() @ x),
-        "wgrad2": (2 * B * H * H, lambda t, impl: G.gemm_raw(dy, h1, dw2, M=H, N=H, K=B, lda=H, ldb=H, ldc=H,
-                   a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t, impl=impl), lambda: dy.t() @ h1),
+                   aux=h1, ldaux=H, tile=t), lambda: (dy @ w2) * (h1 > 0)),
+        "wgrad1": (2 * B * H * I, lambda t: G.gemm_raw(dy, x, dw1, M=H, N=I, K=B, lda=H, ldb=I, ldc=I,
+                   a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t), lambda: dy.t() @ x),
+        "wgrad2": (2 * B * H * H, lambda t: G.gemm_raw(dy, h1, dw2, M=H, N=H, K=B, lda=H, ldb=H, ldc=H,
+                   a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t), lambda: dy.t() @ h1),
     }
     res = {}
     for name, (flop, ours, ref) in cases.items():
@@ -71,9 +71,7 @@ def main():
         t = timeit(ref)
         row["hipblaslt"] = round(t, 2)
         for cfg in range(8):
-            row[f"pipe{cfg}"] = round(timeit(lambda: ours(cfg, "pipe")), 2)
-        for cfg in range(4):
-            row[f"v1_{cfg}"] = round(timeit(lambda: ours(cfg, "v1")), 2)
+            row[f"pipe{cfg}"] = round(timeit(lambda: ours(cfg)), 2)
         best = min((v, k) for k, v in row.items() if k != "hipblaslt")
         row["best"] = best[1]
         row["best_tflops"] = round(flop / best[0] / 1e6, 1)

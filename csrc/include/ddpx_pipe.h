@@ -182,42 +182,75 @@ __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rs, char* slot
   }
 }
 
-template <int ROWS, bool KC>
-__device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kbase, int lane) {
-  if constexpr (KC) {
-    const int row = rbase + (lane & 15);
-    const int chunk = (kbase >> 3) + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
-  } else {
-    constexpr int ROWB = ROWS * 2;
-    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    const int chunk32 = rbase >> 4;
-    const int k0 = kbase + 8 * g + q;
-    const int k1 = k0 + 4;
-    const int off0 = k0 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k0)) << 5) + p * 8;
-    const int off1 = k1 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k1)) << 5) + p * 8;
-    // Inline asm, not __builtin_amdgcn_ds_read_tr16_b64: hipcc (ROCm 7.2) treats the builtin as a possible
-    // reader of every pending LDS-DMA write and puts an `s_waitcnt vmcnt(0)` in front of it, draining the
-    // stage that was just issued for t + STAGES - 1 and collapsing every >= 3-stage ring into a 1-stage one.
-    // The ring's own counted vmcnt + barrier order these reads; the caller waits lgkmcnt before use
-    // (tr_wait()).
-    short4v lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"((LDS_AS const char*)(lds + off0)) : "memory");
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"((LDS_AS const char*)(lds + off1)) : "memory");
-    short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
+// K-contig fragment (ds_read_b128 of the swizzled [row][64] image): an ordinary LDS load the compiler's
+// waitcnt pass tracks.
+template <int ROWS>
+__device__ __forceinline__ bf16x8 frag_kc(const char* lds, int rbase, int kbase, int lane) {
+  const int row = rbase + (lane & 15);
+  const int chunk = (kbase >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
 }
 
-// After a batch of frag() reads, before their values are used: the transposing reads are inline asm
-// (invisible to the compiler's waitcnt pass), so wait for LDS here and keep the MFMAs behind the wait
-// (cdna_hip_programming §5.4 rule 18).
-template <bool ANY_TR>
-__device__ __forceinline__ void tr_wait() {
-  if constexpr (ANY_TR) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
+// M/N-contig fragment: two ds_read_b64_tr_b16 of the [k][row] image, ISSUED here and settled by frag_settle.
+// Inline asm, not __builtin_amdgcn_ds_read_tr16_b64: hipcc (ROCm 7.2) treats the builtin as a possible
+// reader of every pending LDS-DMA write and puts an `s_waitcnt vmcnt(0)` in front of it, draining the
+// stage that was just issued for t + STAGES - 1 and collapsing every >= 3-stage ring into a 1-stage one.
+// The ring's own counted vmcnt + barrier order these reads against the DMA.
+struct TrFrag {
+  short4v lo, hi;
+};
+
+template <int ROWS>
+__device__ __forceinline__ TrFrag frag_tr(const char* lds, int rbase, int kbase, int lane) {
+  constexpr int ROWB = ROWS * 2;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int chunk32 = rbase >> 4;
+  const int k0 = kbase + 8 * g + q;
+  const int k1 = k0 + 4;
+  const int off0 = k0 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k0)) << 5) + p * 8;
+  const int off1 = k1 * ROWB + ((chunk32 ^ tr_swz<ROWB>(k1)) << 5) + p * 8;
+  TrFrag f;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"((LDS_AS const char*)(lds + off0)) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"((LDS_AS const char*)(lds + off1)) : "memory");
+  return f;
+}
+
+// The wait for a transposed fragment, in the SAME asm statement that redefines both of its halves: the
+// compiler sees the halves' values come into existence only after `s_waitcnt lgkmcnt(0)`, so neither the
+// combine below nor any copy or spill can read a VGPR the LDS read has not written yet (the asm outputs of
+// frag_tr are otherwise "ready" the moment their asm line ends — round-2 advisor finding).  The first settle
+// of a batch does the real wait; the rest find lgkmcnt already 0 (one issue cycle each).
+__device__ __forceinline__ bf16x8 frag_settle(TrFrag& f) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.lo), "+v"(f.hi) : : "memory");
+  short8v v = {f.lo[0], f.lo[1], f.lo[2], f.lo[3], f.hi[0], f.hi[1], f.hi[2], f.hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Fragments of one K-slice for a wave: FA A-fragments (rows ra0 + 16 i) and FB B-fragments (rows rb0 + 16 j),
+// every read issued before any wait; MFMAs are kept behind the settles.
+template <int BMR, bool AKC, int FA, int BNR, bool BKC, int FB>
+__device__ __forceinline__ void load_frags(const char* sa, int ra0, const char* sb, int rb0, int kk, int lane,
+                                           bf16x8 (&a)[FA], bf16x8 (&b)[FB]) {
+  TrFrag ta[AKC ? 1 : FA], tb[BKC ? 1 : FB];
+#pragma unroll
+  for (int i = 0; i < FA; ++i) {
+    if constexpr (AKC) a[i] = frag_kc<BMR>(sa, ra0 + i * 16, kk, lane);
+    else ta[i] = frag_tr<BMR>(sa, ra0 + i * 16, kk, lane);
   }
+#pragma unroll
+  for (int j = 0; j < FB; ++j) {
+    if constexpr (BKC) b[j] = frag_kc<BNR>(sb, rb0 + j * 16, kk, lane);
+    else tb[j] = frag_tr<BNR>(sb, rb0 + j * 16, kk, lane);
+  }
+  if constexpr (!AKC) {
+#pragma unroll
+    for (int i = 0; i < FA; ++i) a[i] = frag_settle(ta[i]);
+  }
+  if constexpr (!BKC) {
+#pragma unroll
+    for (int j = 0; j < FB; ++j) b[j] = frag_settle(tb[j]);
+  }
+  if constexpr (!AKC || !BKC) __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int N>
@@ -512,11 +545,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
       const char* sa = sa0 + u * A_SUB;
       const char* sb = sb0 + u * B_SUB;
       bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = frag<BM, AK>(sa, wm * (BM / WGM) + i * 16, kk, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = frag<BN, BKc>(sb, wn * (BN / 2) + j * 16, kk, lane);
-      tr_wait<!AK || !BKc>();
+      load_frags<BM, AK, FM, BN, BKc, FN>(sa, wm * (BM / WGM), sb, wn * (BN / 2), kk, lane, a, b);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

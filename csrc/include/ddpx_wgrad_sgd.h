@@ -117,11 +117,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
 #pragma unroll
           for (int kk = 0; kk < 64; kk += 32) {
             bf16x8 af[FM], bfr[FN];
-#pragma unroll
-            for (int a = 0; a < FM; ++a) af[a] = pipe::frag<BM, false>(sa, wm * 32 + a * 16, kk, lane);
-#pragma unroll
-            for (int b = 0; b < FN; ++b) bfr[b] = pipe::frag<BN, false>(sb, wn * 64 + b * 16, kk, lane);
-            pipe::tr_wait<true>();
+            pipe::load_frags<BM, false, FM, BN, false, FN>(sa, wm * 32, sb, wn * 64, kk, lane, af, bfr);
 #pragma unroll
             for (int a = 0; a < FM; ++a)
 #pragma unroll

@@ -1,7 +1,12 @@
 // ddpx — pipelined bf16 MFMA GEMM for gfx950: LDS-DMA multi-stage ring.
 //
-// Same contract and operand layouts as gemm_bf16.hip (see there), re-built
-// for the regime the MLP shapes live in (M = 512 rows against N, K = 3-16 K):
+// Operand layouts (chosen per call so forward, dgrad and wgrad of a Linear never
+// materialise a transpose; reference equivalent: the implicit cuBLAS addmm/mm of
+// nn.Linear, /root/reference/singlegpu.py:73):
+//   A "K-contig" A[m*lda + k] / "M-contig" A[k*lda + m];  B "K-contig" B[n*ldb + k] / "N-contig" B[k*ldb + n]
+//   forward Y = X W^T (A=X K-contig, B=W K-contig); dgrad dX = dY W (A=dY K-contig, B=W N-contig);
+//   wgrad dW = dY^T X (A=dY M-contig, B=X N-contig).
+// Built for the regime the MLP shapes live in (M = 512 rows against N, K = 3-16 K):
 // a 64x128 / 128x128 tile gives only 256 / 128 workgroups, one per CU, so the
 // kernel is bound by how many bytes each CU keeps in flight, not by MFMA.
 //
@@ -14,12 +19,14 @@
 //    DMA queue, §5 "Pipelining across barriers") -> issue the next stage into
 //    the slot freed one iteration ago -> ds_read + MFMA on the landed slot.
 //  * LDS images are lane-linear (DMA writes base + lane*16), so the bank
-//    swizzles of gemm_bf16.hip are applied to the per-lane SOURCE address and
-//    undone on the read (rule 21): same images, same fragment readers.
+//    swizzles (K-contig [row][64] tiles: 16-B chunk ^= (row>>1)&7; M/N-contig
+//    [k][row] tiles read by ds_read_b64_tr_b16: a 32-B-chunk XOR per row
+//    stride) are applied to the per-lane SOURCE address and undone on the
+//    read (rule 21).
 //  * Buffer-resource bounds checking returns zeros for out-of-range lanes
 //    (voffset forced past num_records), which handles ragged M/N/K tails with
 //    no branches in the load path.
-//  * XCD-aware workgroup remap (T1) as in v1.
+//  * XCD-aware workgroup remap (T1): tiles sharing a B panel run on one XCD.
 //  * Epilogues: bias (+ReLU) -> bf16, fp32 (+accumulate) for gradients
 //    written straight into DDP buckets, bf16 (+accumulate), ReLU-mask
 //    backward, and an optional per-tile column sum of the stored output (the

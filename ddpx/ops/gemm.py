@@ -1,4 +1,4 @@
-"""Host wrappers for the gfx950 bf16 MFMA GEMM (``csrc/kernels/gemm_bf16.hip``).
+"""Host wrappers for the gfx950 bf16 MFMA GEMM (``csrc/kernels/gemm_pipe.hip`` on ``csrc/include/ddpx_pipe.h``).
 
 Every wrapper validates shapes, dtypes, contiguity and alignment on the host
 before launching: the kernel's grid and loaders assume exactly these layouts.
@@ -15,14 +15,10 @@ wgrad      dW[N,K] = dY[M,N]ᵀ · X[M,K]   M-contig     N-contig
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from ..runtime import native
 
-# "pipe" (LDS-DMA multi-stage ring, default) or "v1" (register-staged, 2 LDS buffers)
-GEMM_IMPL = os.environ.get("DDPX_GEMM", "pipe")
 # In-launch split-K for the M=512-row products (forward / dgrad): 128x128 tiles, K split over 2-4
 # workgroups whose fp32 partials are combined by the last split of each tile inside the same launch
 # (``csrc/include/ddpx_pipe.h``).  Planned by the native side; DDPX_SPLITK=0 turns it off there.
@@ -71,6 +67,9 @@ def plan(M, N, K, a_kcontig, b_kcontig, epi):
 
 _TICKETS: dict = {}
 _CS_TICKETS: dict = {}
+# superseded ticket buffers stay allocated: a HIP graph captured earlier keeps their addresses and its
+# replays still take tickets there (freeing them would hand those replays recycled, non-zero memory)
+_RETIRED: list = []
 
 
 def _tickets(dev, n, pool=None):
@@ -81,6 +80,8 @@ def _tickets(dev, n, pool=None):
     if t is None or t.numel() < n:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("GEMM tickets: first launch of this size must happen outside graph capture")
+        if t is not None:
+            _RETIRED.append(t)
         t = pool[dev] = torch.zeros((max(n, 4096),), dtype=torch.int32, device=dev)
     return t
 
@@ -92,7 +93,7 @@ def tile_dims(cfg):
 
 
 def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias=None, aux=None, ldaux=0,
-             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, impl=None, sgd=None, splits=None,
+             accumulate=False, alpha=1.0, tile=-1, colsum=None, stream=None, sgd=None, splits=None,
              cs_out=None, cs_accumulate=False, cs_sgd=None):
     """``splits`` (with an explicit ``tile``): force the in-launch split-K on that tile config.
 
@@ -100,42 +101,34 @@ def gemm_raw(a, b, c, *, M, N, K, lda, ldb, ldc, a_kcontig, b_kcontig, epi, bias
     sums of the stored output are finished inside the launch (the last row tile of each column tile adds
     the partials in order) and stored / accumulated into ``cs_out`` or applied as an SGD update."""
     lib = native.kernels()
-    impl = impl or GEMM_IMPL
     s = native.stream_handle(stream)
-    if impl == "v1":
-        if colsum is not None or sgd is not None:
-            raise ValueError("v1 GEMM has no fused column sum / optimizer epilogue")
-        rc = lib.ddpx_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux), M, N, K,
-                                lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi, int(accumulate),
-                                float(alpha), tile, s)
+    slab, sf, tk = None, 0, None
+    nt = 0
+    if splits is not None and splits > 1:
+        _req(tile >= 0 and sgd is None, "forced split-K needs an explicit tile and no fused optimizer")
+        bm, bn = tile_dims(tile)
+        nt = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+        sf = splits * nt * bm * bn
     else:
-        slab, sf, tk = None, 0, None
-        nt = 0
-        if splits is not None and splits > 1:
-            _req(tile >= 0 and sgd is None, "forced split-K needs an explicit tile and no fused optimizer")
-            bm, bn = tile_dims(tile)
-            nt = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
-            sf = splits * nt * bm * bn
-        else:
-            splits = 1
-            if tile < 0 and sgd is None:
-                splits, cfg, sf, nt = plan(M, N, K, a_kcontig, b_kcontig, epi)
-                if splits > 1:
-                    tile = cfg
-        if splits > 1:
-            slab = torch.empty(sf, dtype=torch.float32, device=a.device)
-            tk = _tickets(a.device, nt)
-        cs_t, cs_flags = None, 0
-        if cs_out is not None or cs_sgd is not None:
-            _req(colsum is not None and sgd is None, "in-launch column sums need the colsum scratch, no EPI_SGD")
-            cs_t = _tickets(a.device, N, pool=_CS_TICKETS)
-            cs_flags = int(cs_out is not None and cs_out.dtype == torch.bfloat16) | (2 if cs_accumulate else 0)
-            sgd = cs_sgd  # the bias SGD rides on the (otherwise unused) optimizer arguments
-        rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
-                                native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
-                                int(accumulate), float(alpha), tile, *native.sgd_args(sgd), splits, native.ptr(slab), sf,
-                                native.ptr(tk), native.ptr(cs_out), cs_flags, native.ptr(cs_t), s)
-    native.check(rc, f"ddpx_gemm_{impl}(M={M},N={N},K={K},epi={epi})")
+        splits = 1
+        if tile < 0 and sgd is None:
+            splits, cfg, sf, nt = plan(M, N, K, a_kcontig, b_kcontig, epi)
+            if splits > 1:
+                tile = cfg
+    if splits > 1:
+        slab = torch.empty(sf, dtype=torch.float32, device=a.device)
+        tk = _tickets(a.device, nt)
+    cs_t, cs_flags = None, 0
+    if cs_out is not None or cs_sgd is not None:
+        _req(colsum is not None and sgd is None, "in-launch column sums need the colsum scratch, no EPI_SGD")
+        cs_t = _tickets(a.device, N, pool=_CS_TICKETS)
+        cs_flags = int(cs_out is not None and cs_out.dtype == torch.bfloat16) | (2 if cs_accumulate else 0)
+        sgd = cs_sgd  # the bias SGD rides on the (otherwise unused) optimizer arguments
+    rc = lib.ddpx_gemm_pipe(a.data_ptr(), b.data_ptr(), c.data_ptr(), native.ptr(bias), native.ptr(aux),
+                            native.ptr(colsum), M, N, K, lda, ldb, ldc, ldaux, int(a_kcontig), int(b_kcontig), epi,
+                            int(accumulate), float(alpha), tile, *native.sgd_args(sgd), splits, native.ptr(slab), sf,
+                            native.ptr(tk), native.ptr(cs_out), cs_flags, native.ptr(cs_t), s)
+    native.check(rc, f"ddpx_gemm_pipe(M={M},N={N},K={K},epi={epi})")
     return c
 
 
@@ -203,7 +196,7 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
     gemm_raw(dy, w, out, M=M, N=K, K=N, lda=dy.stride(0), ldb=w.stride(0), ldc=K, a_kcontig=True,
              b_kcontig=False, epi=epi, aux=relu_mask_of,
              ldaux=(relu_mask_of.stride(0) if relu_mask_of is not None else 0), tile=tile, colsum=part,
-             impl=None if part is None else "pipe", splits=splits,
+             splits=splits,
              cs_out=bias_grad if in_launch else None, cs_accumulate=bias_grad_accumulate,
              cs_sgd=bias_sgd if in_launch else None)
     if part is not None and not in_launch and bias_grad is not None:
@@ -228,7 +221,7 @@ def linear_wgrad(dy, x, out, accumulate=False, tile=-1, sgd=None):
         _, K = x.shape
         _req(sgd[0].numel() == N * K, "sgd target size mismatch")
         return gemm_raw(dy, x, sgd[0], M=N, N=K, K=M, lda=dy.stride(0), ldb=x.stride(0), ldc=K, a_kcontig=False,
-                        b_kcontig=False, epi=EPI_SGD, tile=tile, impl="pipe", sgd=sgd)
+                        b_kcontig=False, epi=EPI_SGD, tile=tile, sgd=sgd)
     _check_bf16_2d(dy, "dy")
     _check_bf16_2d(x, "x")
     M, N = dy.shape
@@ -237,12 +230,11 @@ def linear_wgrad(dy, x, out, accumulate=False, tile=-1, sgd=None):
     _req(out.dtype in (torch.float32, torch.bfloat16), "dW must be fp32 or bf16")
     _req(tuple(out.shape) == (N, K) and out.is_contiguous(), f"dW must be contiguous [{N},{K}]")
     epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
-    _req(not (accumulate and epi == EPI_BF16 and GEMM_IMPL == "v1"), "v1 GEMM cannot accumulate bf16")
     return gemm_raw(dy, x, out, M=N, N=K, K=M, lda=dy.stride(0), ldb=x.stride(0), ldc=K, a_kcontig=False,
                     b_kcontig=False, epi=epi, accumulate=accumulate, tile=tile)
 
 
-def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-1, impl=None):
+def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-1):
     """General C = A·B for tests: A given as [M,K] (K-contig) or [K,M]; B as [N,K] or [K,N]."""
     _check_bf16_2d(a, "a")
     _check_bf16_2d(b, "b")
@@ -252,7 +244,7 @@ def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-
     epi = EPI_F32 if out_dtype == torch.float32 else EPI_BF16
     out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     return gemm_raw(a, b, out, M=M, N=N, K=K, lda=a.stride(0), ldb=b.stride(0), ldc=N, a_kcontig=a_kcontig,
-                    b_kcontig=b_kcontig, epi=epi, tile=tile, impl=impl)
+                    b_kcontig=b_kcontig, epi=epi, tile=tile)
 
 
 native.register_kernel_sig("ddpx_wgrad_sgd_pair", native.c_int, *([native.c_void_p, native.c_void_p] + [native.c_int] * 5

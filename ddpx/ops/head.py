@@ -62,6 +62,7 @@ def head_forward(h, w, b, targets=None, want_logits=True, want_grad=True, correc
 
 
 _TICKETS: dict = {}
+_RETIRED: list = []
 
 
 def _tickets(dev, n):
@@ -71,6 +72,8 @@ def _tickets(dev, n):
     if t is None or t.numel() < n:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("head_forward: first call for this batch size must happen outside graph capture")
+        if t is not None:
+            _RETIRED.append(t)  # a captured graph may still take tickets at the old address: keep it
         t = _TICKETS[dev] = torch.zeros((max(n, 1025),), dtype=torch.int32, device=dev)
     return t
 

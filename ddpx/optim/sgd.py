@@ -28,20 +28,20 @@ from ..runtime.flat_params import FlatParams, flat_of
 # Device LR-schedule advance waiting for a kernel to carry it (SGD.device_lr_step): the classifier head's
 # forward launch takes it (take_lr_advance), which saves the training step a separate 1-thread kernel;
 # anything that reads lr before a head forward took it launches it on its own first (SGD._flush_lr).
+# The pending advance is a field of the parameter store the optimizer owns (``FlatParams.pending_lr``),
+# so optimizers of different models in one process never hand their advances to each other.
 # DDPX_LR_IN_HEAD=0 always launches the separate kernel.
-_PENDING_LR = None
 _LR_IN_HEAD = os.environ.get("DDPX_LR_IN_HEAD", "1") != "0"
 
 
 def take_lr_advance(flat):
     """(table, counter, lr) if the optimizer of ``flat`` has an LR advance pending (it is then the caller's
     launch that performs it), else None."""
-    global _PENDING_LR
-    p = _PENDING_LR
-    if p is None or p[0].flat is not flat:
+    p = getattr(flat, "pending_lr", None)
+    if p is None:
         return None
-    _PENDING_LR = None
-    return p[1:]
+    flat.pending_lr = None
+    return p
 
 
 class SGD(Optimizer):
@@ -140,18 +140,16 @@ class SGD(Optimizer):
     def device_lr_step(self):
         if self._lr_table is None:
             return
-        global _PENDING_LR
         self._flush_lr()
         if _LR_IN_HEAD:
-            _PENDING_LR = (self, self._lr_table, self._lr_counter, self._lr_dev)
+            self.flat.pending_lr = (self._lr_table, self._lr_counter, self._lr_dev)
             return
         self._launch_lr_advance()
 
     def _flush_lr(self):
         """Launch this optimizer's pending LR advance if no kernel took it (before anything reads lr)."""
-        global _PENDING_LR
-        if _PENDING_LR is not None and _PENDING_LR[0] is self:
-            _PENDING_LR = None
+        if getattr(self.flat, "pending_lr", None) is not None:
+            self.flat.pending_lr = None
             self._launch_lr_advance()
 
     def _launch_lr_advance(self):

@@ -695,6 +695,24 @@ class DistributedDataParallel(nn.Module):
             return None
         return self.reducer.comm_stats()
 
+    # ------------------------------------------------- aborted-iteration recovery
+    def iteration_state(self):
+        """Host-side bucket bookkeeping between iterations (see :meth:`restore_iteration_state`)."""
+        return {"gather_todo": list(self._gather_todo), "gather_wait": set(self._gather_wait)}
+
+    def restore_iteration_state(self, st):
+        """Forget an iteration that never ran on the device (a HIP-graph capture that failed part-way): the
+        bucket state goes back to ``st`` (taken by :meth:`iteration_state` before it), no collective is
+        waited for, and deferred ZeRO-1 all-gathers the aborted capture consumed are owed again."""
+        self._overlap_pending = False
+        self._queued = False
+        self._completion_order = []
+        self._marks = [0] * len(self.bucket_ranges)
+        self._gather_todo = list(st["gather_todo"])
+        self._gather_wait = set(st["gather_wait"])
+        if self.reducer is not None:
+            self.reducer.prepare()
+
     # ----------------------------------------------------------------- misc
     def state_dict(self, *args, **kwargs):
         return super().state_dict(*args, **kwargs)

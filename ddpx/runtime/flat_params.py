@@ -82,6 +82,9 @@ class FlatParams:
         self.fused_opt = None  # set by ddpx.optim.SGD(fused_backward=True)
         self.sink = None
         self.optimizer = None  # the ddpx SGD that owns this store (set by SGD)
+        # device LR-schedule advance of that optimizer not launched yet: (table, counter, lr) until a kernel
+        # (the classifier head's forward) carries it or the optimizer launches it itself (ddpx.optim.sgd)
+        self.pending_lr = None
         # params whose forward/backward read ONLY the bf16 shadow (never the fp32 master) —
         # a sharded optimizer may then all-gather just the shadow for them
         self.shadow_only = set()

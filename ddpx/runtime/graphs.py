@@ -70,3 +70,65 @@ class CapturedStep:
         if self.comm is not None:
             self.comm.track(what="graph replay")
         return self.static_loss
+
+
+class GraphedSteps:
+    """Training steps: eager for the first ``eager_first`` (allocator / lazy-init warm-up), then replays of
+    captured graphs — or, if capture fails on ANY rank, eager steps on every rank in the same process.
+
+    ``eager_step()`` runs one step and returns its loss; ``make_graphs()`` captures and returns
+    ``{steps_per_graph: callable}`` (each call replays that many steps and returns the last loss).  A
+    failed capture is never retried and never restarts anything: the exception text is kept in
+    ``graph_error``, ``on_fallback()`` (if given) resets whatever step state the aborted capture left
+    half-done, and the loop continues eagerly.  ``agree(ok) -> bool`` turns one rank's capture outcome into
+    the job's (all ranks must take the same path: a graph replay on one rank and eager collectives on
+    another would pair different collectives); default: the local outcome.  ``after(m)`` is called after
+    every ``m`` executed steps (host bookkeeping such as ``scheduler.step()``).
+    """
+
+    def __init__(self, eager_step, make_graphs, steps_per_graph: int = 1, use_graph: bool = True, eager_first: int = 2,
+                 agree=None, on_fallback=None, after=None):
+        self.eager_step = eager_step
+        self.make_graphs = make_graphs
+        self.S = max(1, int(steps_per_graph))
+        self.use_graph = bool(use_graph)
+        self.eager_first = eager_first
+        self.agree = agree
+        self.on_fallback = on_fallback
+        self.after = after
+        self.graphs = None
+        self.graph_error = None
+
+    def _capture(self):
+        ok, err, graphs = True, None, None
+        try:
+            graphs = self.make_graphs()
+        except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager steps
+            ok, err = False, f"{type(e).__name__}: {e}"
+        all_ok = self.agree(ok) if self.agree is not None else ok
+        if all_ok:
+            self.graphs = graphs
+            return
+        self.graphs = None
+        self.use_graph = False
+        self.graph_error = err or "graph capture failed on another rank"
+        if self.on_fallback is not None:
+            self.on_fallback()
+
+    def run(self, k: int, n: int):
+        """Steps k .. k+n-1; returns the last step's loss."""
+        loss = None
+        while n > 0:
+            if self.use_graph and k >= self.eager_first and self.graphs is None:
+                self._capture()
+            if not self.use_graph or k < self.eager_first:
+                loss = self.eager_step()
+                m = 1
+            else:
+                m = self.S if (n >= self.S and self.S in self.graphs) else 1
+                loss = self.graphs[m]()
+            if self.after is not None:
+                self.after(m)
+            k += m
+            n -= m
+        return loss

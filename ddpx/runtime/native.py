@@ -45,7 +45,6 @@ def _sig(lib, name, restype, *argtypes):
 
 def _declare_kernels(lib):
     P, I, I64, F = c_void_p, c_int, c_int64, c_float
-    _sig(lib, "ddpx_gemm_bf16", I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P)
     _sig(lib, "ddpx_sgd_flat", I, P, P, P, I, P, I64, P, F, F, F, F, I, I, P)
     _sig(lib, "ddpx_cast_f32_bf16", I, P, P, I64, P)
     _sig(lib, "ddpx_colsum_bf16", I, P, P, I, I, I, F, I, P)

@@ -43,15 +43,29 @@ def test_single_gpu_toy_mlp_defaults():
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_multi_gpu_toy_mlp_defaults(world):
     a = _resolved(["--gpus", str(world)], world)
-    assert a.grad_dtype == "fp32"
-    assert a.shard_optimizer == 0 and a.overlap_optimizer == 1
-    assert a.comm_side_optimizer == 0 and a.defer_gather == 0 and a.chunk_mb == 0.0
-    assert a.stock_ref == 0 and a.fp8 == 0
+    assert a.grad_dtype == "fp32" and a.overlap_optimizer == 1 and a.chunk_mb == 0.0
+    # bucket caps and replicated-vs-ZeRO-1 are left to the start-up calibration on the node
+    assert a.calibrate and a.shard_optimizer is None and a.bucket_cap_mb is None and a.first_bucket_mb is None
+    assert a.stock_ref == 1 and a.fp8 == 0
+    # the calibration's ZeRO-1 choice brings its companions
+    import bench
+    a.shard_optimizer = 1
+    bench.resolve_zero_defaults(a)
+    assert a.comm_side_optimizer == 1 and a.defer_gather == 1
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_multi_gpu_uncalibrated_defaults(world):
+    a = _resolved(["--gpus", str(world), "--bucket_plan", "default"], world)
+    assert not a.calibrate and a.shard_optimizer == 0 and a.bucket_cap_mb == 25.0 and a.first_bucket_mb == 1.0
+    assert a.comm_side_optimizer == 0 and a.defer_gather == 0
 
 
 def test_zero1_opt_in():
     a = _resolved(["--gpus", "8", "--shard_optimizer", "1"], 8)
     assert a.shard_optimizer == 1 and a.comm_side_optimizer == 1 and a.defer_gather == 1
+    b = _resolved(["--gpus", "8", "--shard_optimizer", "1", "--bucket_cap_mb", "25", "--first_bucket_mb", "1"], 8)
+    assert not b.calibrate
 
 
 def test_every_model_fuses_the_single_gpu_optimizer():
@@ -59,7 +73,7 @@ def test_every_model_fuses_the_single_gpu_optimizer():
         a = _resolved(["--model", m], 1)
         assert a.fused_optimizer == 1, m
     assert _resolved(["--model", "mlp_wide"], 1).hidden == 16384
-    v = _resolved(["--model", "vgg"], 8)
+    v = _resolved(["--model", "vgg", "--bucket_plan", "default"], 8)
     assert v.shard_optimizer == 0 and v.comm_side_optimizer == 0 and v.defer_gather == 0
 
 
@@ -112,3 +126,10 @@ def test_bench_cpu_two_ranks_self_launched():
     assert c["grad_dtype"] == "fp32" and c["grad_comm"].startswith("fp32 all-reduce")
     assert c["replicas_consistent"] is True and c["sharded_optimizer"] is False
     assert c["buckets_mb"] and rec["value"] > 0
+    # bucket caps timed on this node before the first step (no ZeRO-1 candidate on the CPU: no bf16 shadow)
+    assert c["bucket_plan"] == "calibrated" and c["calibration"]["chosen"].startswith("allreduce")
+    assert all(v > 0 for v in c["calibration"]["ms"].values())
+    # the stock recipe (torch DDP over gloo here, RCCL on the GPU) timed in the same job
+    st = c["stock_same_run"]
+    assert st["ms_per_step"] > 0 and "torch DDP" in st["recipe"] and c["vs_stock_same_run"] > 0
+    assert c["graph"] is False and c["graph_error"] is None

@@ -13,13 +13,11 @@ def _rand_bf16(*shape, dev):
     return (torch.randn(*shape, device=dev) * 0.5).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("impl_tile", [("v1", -1), ("v1", 0), ("v1", 1), ("v1", 2), ("v1", 3)] +
-                         [("pipe", t) for t in range(-1, 14)])
+@pytest.mark.parametrize("tile", list(range(-1, 14)))
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
                                  (200, 136, 1000), (2048, 4096, 512)])
-def test_gemm_layouts(gpu, impl_tile, layout, MNK):
-    impl, tile = impl_tile
+def test_gemm_layouts(gpu, tile, layout, MNK):
     from ddpx.ops.gemm import matmul
     M, N, K = MNK
     ak, bk = layout
@@ -30,7 +28,7 @@ def test_gemm_layouts(gpu, impl_tile, layout, MNK):
     B = _rand_bf16(K, N, dev=gpu)  # logical [K,N]
     a_store = A if ak else A.t().contiguous()        # [M,K] or [K,M]
     b_store = B.t().contiguous() if bk else B         # [N,K] or [K,N]
-    C = matmul(a_store, b_store, a_kcontig=ak, b_kcontig=bk, tile=tile, impl=impl)
+    C = matmul(a_store, b_store, a_kcontig=ak, b_kcontig=bk, tile=tile)
     ref = A.float() @ B.float()
     assert _rel(C, ref) < 2e-3
 
@@ -41,12 +39,10 @@ def test_gemm_identity_asymmetric(gpu):
     n = 128
     A = torch.eye(n, device=gpu, dtype=torch.bfloat16)
     B = (torch.arange(n * n, device=gpu, dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
-    for impl in ("v1", "pipe"):
-        for ak in (True, False):
-            for bk in (True, False):
-                C = matmul(A if ak else A.t().contiguous(), B.t().contiguous() if bk else B, a_kcontig=ak,
-                           b_kcontig=bk, impl=impl)
-                assert torch.equal(C, B.float()), (impl, ak, bk)
+    for ak in (True, False):
+        for bk in (True, False):
+            C = matmul(A if ak else A.t().contiguous(), B.t().contiguous() if bk else B, a_kcontig=ak, b_kcontig=bk)
+            assert torch.equal(C, B.float()), (ak, bk)
 
 
 def test_linear_fwd_dgrad_wgrad(gpu):
