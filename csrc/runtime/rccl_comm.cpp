@@ -76,17 +76,24 @@ struct Comm {
 int check(ncclResult_t r) { return r == ncclSuccess ? 0 : 1000 + (int)r; }
 
 // Abort the communicator from the watchdog thread.  Waits (bounded) for an in-flight issue call to
-// return; a call stuck inside RCCL (e.g. a connection handshake with a dead peer) is exactly what
-// ncclCommAbort exists to unblock, so after the bound the abort proceeds without the lock.  The handle
-// itself is never cleared without the lock: issuers test `aborted` under issue_mu instead.
+// return.  If the owning thread is still inside an RCCL call after the bound (e.g. a connection handshake
+// with a dead peer), aborting under it would free the communicator that call is using, so the watchdog
+// escalates to the exit action instead: the process ends with exit code 3 (what ACT_EXIT does for any
+// timeout).  The handle is never touched without the lock: issuers test `aborted` under issue_mu.
 void abort_comm(Comm* c) {
   bool locked = false;
   for (int i = 0; i < 200 && !locked; ++i) {  // ~2 s
     locked = c->issue_mu.try_lock();
     if (!locked) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   }
+  if (!locked) {
+    fprintf(stderr, "[ddpx rank %d] abort: a collective call is stuck inside RCCL; terminating (exit code 3)\n",
+            c->rank);
+    fflush(stderr);
+    std::_Exit(3);
+  }
   if (!c->aborted.exchange(true) && c->nccl) ncclCommAbort(c->nccl);
-  if (locked) c->issue_mu.unlock();
+  c->issue_mu.unlock();
 }
 
 void on_failure(Comm* c, int code, const char* what) {
@@ -394,8 +401,20 @@ DDPX_API int ddpx_comm_allgather(void* h, const void* send, void* recv, size_t s
   return e;
 }
 
-DDPX_API int ddpx_comm_group_start() { return check(ncclGroupStart()); }
-DDPX_API int ddpx_comm_group_end() { return check(ncclGroupEnd()); }
+// Grouped collectives of one communicator (RCCL launches them at ncclGroupEnd): both ends run under the
+// issue guard, so an abort can never free the communicator while the group is being launched.
+DDPX_API int ddpx_comm_group_start(void* h) {
+  Comm* c = static_cast<Comm*>(h);
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
+  return check(ncclGroupStart());
+}
+DDPX_API int ddpx_comm_group_end(void* h) {
+  Comm* c = static_cast<Comm*>(h);
+  IssueGuard ig(c);
+  if (!ig.ok()) return 3;
+  return check(ncclGroupEnd());
+}
 
 // ---------------------------------------------------------------------------
 DDPX_API void* ddpx_reducer_create(void* comm, int nbuckets, int op) {

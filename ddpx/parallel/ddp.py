@@ -613,13 +613,23 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         if self.reducer is None:
             return
+        skip = []
         if self.find_unused_parameters:
             # every bucket is issued here, in bucket order (identical on every rank); gradients of
             # parameters this rank did not use are zeros
-            self.flat.fix_unwritten(mark_written=True)
+            f = self.flat
+            local_used = [1 if (w or u) else 0 for w, u in zip(f.written, f.updated)]
+            f.fix_unwritten(mark_written=True)
             for b in range(len(self.bucket_ranges)):
                 self.reducer.mark_ready(b, self.bucket_expected[b])
             self._completion_order = list(range(len(self.bucket_ranges)))
+            # torch's local_used_map: a parameter NO rank used this iteration has no gradient (None in torch),
+            # so the optimizer must not apply weight decay / momentum to it (one small MAX all-reduce + a host
+            # read: this opt-in path is not graph-capturable, as in torch)
+            used = torch.tensor(local_used, dtype=torch.int32, device=f.master.device)
+            if self.world_size > 1:
+                self.comm.allreduce_(used, op="max")
+            skip = [i for i, v in enumerate(used.tolist()) if v == 0]
         elif len(self._completion_order) < len(self.bucket_ranges):
             unused = self._unused_names()
             if self.world_size > 1:
@@ -636,6 +646,12 @@ class DistributedDataParallel(nn.Module):
                 if other != order:
                     raise RuntimeError(f"DDP debug: bucket completion order {order} on rank {self.rank} "
                                        f"!= {other} on rank {r}")
+        if skip:
+            # the optimizer steps parameter ranges around the skipped ones: every bucket must be joined first
+            self.reducer.finalize(join=True)
+            for i in skip:
+                self.flat.updated[i] = True
+            return
         if self.overlap_optimizer:
             self._overlap_pending = True
             # launch stragglers but do not join: the optimizer waits per bucket

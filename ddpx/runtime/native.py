@@ -120,8 +120,8 @@ def _declare_rt(lib):
     _sig(lib, "ddpx_hostflag_create", I, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p))
     _sig(lib, "ddpx_hostflag_set", None, P, I)
     _sig(lib, "ddpx_hostflag_destroy", I, P)
-    _sig(lib, "ddpx_comm_group_start", I)
-    _sig(lib, "ddpx_comm_group_end", I)
+    _sig(lib, "ddpx_comm_group_start", I, P)
+    _sig(lib, "ddpx_comm_group_end", I, P)
     _sig(lib, "ddpx_reducer_create", P, P, I, I)
     _sig(lib, "ddpx_reducer_set_bucket", I, P, I, P, S, I, I, I)
     _sig(lib, "ddpx_reducer_set_gather", I, P, I, P, S, I)

@@ -77,6 +77,53 @@ def test_find_unused_parameters_matches_torch_ddp():
     mp.spawn(_unused_worker, args=(2, free_port(), True), nprocs=2, join=True)
 
 
+def _all_skip_worker(rank, ws, port, overlap):
+    """Both ranks skip branch b at step 1, weight decay and momentum on: torch leaves b's gradient None and its
+    SGD does not touch b (no decay, no momentum step); ours must do the same, replicas bit-identical."""
+    import ddpx
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import TorchComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from torch.nn.parallel import DistributedDataParallel as TorchDDP
+    init_gloo(rank, ws, port)
+    try:
+        torch.manual_seed(0)
+        ours, ref = TwoBranch(), TwoBranch()
+        ref.load_state_dict(ours.state_dict())
+        ddpx.prepare_model(ours, "cpu")
+        d_ours = DistributedDataParallel(ours, comm=TorchComm(), bucket_cap_mb=1e-4, first_bucket_mb=1e-4,
+                                         find_unused_parameters=True, overlap_optimizer=overlap)
+        d_ref = TorchDDP(ref, find_unused_parameters=True)
+        o_ours = SGD(ours.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-2)
+        if overlap:
+            d_ours.attach_optimizer(o_ours)
+        o_ref = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-2)
+        g = torch.Generator().manual_seed(rank)
+        b_before = None
+        for step in range(3):
+            x = torch.rand((4, 16), generator=g)
+            t = torch.randint(0, 4, (4,), generator=g)
+            use_b = step != 1
+            if step == 1:
+                b_before = ours.b.weight.detach().clone()
+            for net, opt in ((d_ours, o_ours), (d_ref, o_ref)):
+                opt.zero_grad()
+                F.cross_entropy(net(x, use_b), t).backward()
+                opt.step()
+            if step == 1:
+                assert torch.equal(ours.b.weight, b_before), "a parameter no rank used was stepped"
+        for (n, p), (_, q) in zip(ours.named_parameters(), ref.named_parameters()):
+            assert torch.allclose(p, q, atol=1e-6, rtol=1e-5), (rank, n, (p - q).abs().max().item())
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_parameter_unused_on_every_rank_is_not_stepped(overlap):
+    mp.spawn(_all_skip_worker, args=(2, free_port(), overlap), nprocs=2, join=True)
+
+
 def _both_skip_worker(rank, ws, port):
     import ddpx
     from ddpx.optim.sgd import SGD
