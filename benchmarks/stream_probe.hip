@@ -74,6 +74,39 @@ __global__ void stream(float* __restrict__ p, float* __restrict__ m, unsigned sh
   }
 }
 
+// The same stream in the order the warp-specialised weight-gradient kernel walks it: tiles of TR rows x TC
+// columns of a row-major [rows][cols] fp32 matrix, tile g at (g % tiles_m, g / tiles_m), each thread owning
+// 16-B column groups of every (256 / (TC / 4))-th row; a workgroup sweeps its tiles g = blockIdx.x + i gridDim.x.
+template <int TR, int TC>
+__global__ void __launch_bounds__(256) stream_tiled(float* __restrict__ p, float* __restrict__ m,
+                                                    unsigned short* __restrict__ sh, int rows, int cols, float lr) {
+  constexpr int TPR = TC / 4;            // threads per tile row
+  constexpr int RSTEP = 256 / TPR;       // rows between a thread's vectors
+  constexpr int VPT = TR / RSTEP;        // vectors per thread per tile
+  const int tiles_m = rows / TR, ntiles = tiles_m * (cols / TC);
+  const int r0 = threadIdx.x / TPR, c = 4 * (threadIdx.x % TPR);
+  for (int g = blockIdx.x; g < ntiles; g += gridDim.x) {
+    const int m0 = (g % tiles_m) * TR, n0 = (g / tiles_m) * TC;
+    f32x4 pv[VPT], mv[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const size_t off = (size_t)(m0 + r0 + RSTEP * v) * cols + n0 + c;
+      pv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + off));
+      mv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m + off));
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const size_t off = (size_t)(m0 + r0 + RSTEP * v) * cols + n0 + c;
+      f32x4 g4 = pv[v] * 1e-3f;
+      f32x4 mo = mv[v] * 0.9f + g4;
+      f32x4 po = pv[v] - lr * mo;
+      __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(p + off));
+      __builtin_nontemporal_store(mo, reinterpret_cast<f32x4*>(m + off));
+      *reinterpret_cast<u32x2*>(sh + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+    }
+  }
+}
+
 template <typename F>
 static float time_ms(F launch, int iters) {
   hipEvent_t a, b;
@@ -117,6 +150,16 @@ int main() {
   run<8, false>(ncu, p, m, sh, n, "plain");
   run<2, true>(ncu, p, m, sh, n, "pref");
   run<4, true>(ncu, p, m, sh, n, "pref");
-  run<8, true>(ncu, p, m, sh, n, "pref");
+  // tile-ordered sweeps of a [4096][7168] matrix (the toy MLP's fc1 | fc0 weights side by side)
+  const int rows = 4096, cols = 7168;
+  const double tb = (double)rows * cols * 18;
+  for (int gm : {1, 2, 4}) {
+    float t1 = time_ms([&] { stream_tiled<64, 128><<<ncu * gm, 256>>>(p, m, sh, rows, cols, 0.01f); }, 20);
+    float t2 = time_ms([&] { stream_tiled<32, 256><<<ncu * gm, 256>>>(p, m, sh, rows, cols, 0.01f); }, 20);
+    float t3 = time_ms([&] { stream_tiled<16, 512><<<ncu * gm, 256>>>(p, m, sh, rows, cols, 0.01f); }, 20);
+    float t4 = time_ms([&] { stream_tiled<8, 1024><<<ncu * gm, 256>>>(p, m, sh, rows, cols, 0.01f); }, 20);
+    printf("tiled wg/cu %d: 64x128 %.2f  32x256 %.2f  16x512 %.2f  8x1024 %.2f TB/s\n", gm, tb / t1 / 1e9,
+           tb / t2 / 1e9, tb / t3 / 1e9, tb / t4 / 1e9);
+  }
   return 0;
 }

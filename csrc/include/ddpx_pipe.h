@@ -151,6 +151,30 @@ __device__ __forceinline__ unsigned src_off(const ConvGeom& g, int ld, int row, 
   }
 }
 
+// Source offset (bytes; kOOB = zero fill) of wave-instruction j of a ROWS x 64 operand tile: every
+// wave-instruction moves 1 KiB, lane l its 16 B at LDS byte (j * NW + wave) * 1024 + 16 l of the slot.
+template <int ROWS, bool KC, int MODE, int NW = 4>
+__device__ __forceinline__ unsigned tile_voff(const ConvGeom& g, int ld, int row0, int nrows, int k0, int kend,
+                                              int wave, int lane, int j) {
+  const int inst = j * NW + wave;
+  if constexpr (KC) {
+    const int r = inst * 8 + (lane >> 3);
+    const int pch = lane & 7;
+    const int c = pch ^ ((r >> 1) & 7);
+    const int gr = row0 + r, gk = k0 + c * 8;
+    return (gr < nrows && gk < kend) ? src_off<MODE, true>(g, ld, gr, gk) : kOOB;
+  } else {
+    constexpr int ROWB = ROWS * 2;
+    constexpr int CPR = ROWB / 16;
+    const int kr = inst * (1024 / ROWB) + lane / CPR;
+    const int q = lane % CPR;
+    const int L = (q >> 1) ^ tr_swz<ROWB>(kr);
+    const int col = L * 16 + (q & 1) * 8;
+    const int gk = k0 + kr, gr = row0 + col;
+    return (gk < kend && gr < nrows) ? src_off<MODE, false>(g, ld, gr, gk) : kOOB;
+  }
+}
+
 // Stage one ROWS x 64 operand tile into an LDS slot with LDS-DMA (ROWS/8 wave-instructions of 1 KiB,
 // spread over NW waves).
 template <int ROWS, bool KC, int MODE, int NW = 4>
@@ -159,27 +183,8 @@ __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rs, char* slot
   constexpr int NI = ROWS / (8 * NW);
   static_assert(NI * 8 * NW == ROWS, "tile rows must split evenly over the waves");
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int inst = j * NW + wave;
-    if constexpr (KC) {
-      const int r = inst * 8 + (lane >> 3);
-      const int pch = lane & 7;
-      const int c = pch ^ ((r >> 1) & 7);
-      const int gr = row0 + r, gk = k0 + c * 8;
-      const unsigned voff = (gr < nrows && gk < kend) ? src_off<MODE, true>(g, ld, gr, gk) : kOOB;
-      dma16(rs, slot + inst * 1024, voff);
-    } else {
-      constexpr int ROWB = ROWS * 2;
-      constexpr int CPR = ROWB / 16;
-      const int kr = inst * (1024 / ROWB) + lane / CPR;
-      const int q = lane % CPR;
-      const int L = (q >> 1) ^ tr_swz<ROWB>(kr);
-      const int col = L * 16 + (q & 1) * 8;
-      const int gk = k0 + kr, gr = row0 + col;
-      const unsigned voff = (gk < kend && gr < nrows) ? src_off<MODE, false>(g, ld, gr, gk) : kOOB;
-      dma16(rs, slot + inst * 1024, voff);
-    }
-  }
+  for (int j = 0; j < NI; ++j)
+    dma16(rs, slot + (j * NW + wave) * 1024, tile_voff<ROWS, KC, MODE, NW>(g, ld, row0, nrows, k0, kend, wave, lane, j));
 }
 
 // K-contig fragment (ds_read_b128 of the swizzled [row][64] image): an ordinary LDS load the compiler's
@@ -521,22 +526,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     }
   };
 
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s);
-
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = min(STAGES - 2, nk - 1 - t);
-    // stages 1..STAGES-1 were issued before the prefetch (t = 0): its PFW ops are younger than them
-    const bool pf_young = SGDPF && t >= 1 && t <= STAGES - 1;
-    if (ahead >= 2) { if (pf_young) wait_vmcnt<2 * LPW + PFW>(); else wait_vmcnt<2 * LPW>(); }
-    else if (ahead == 1) { if (pf_young) wait_vmcnt<LPW + PFW>(); else wait_vmcnt<LPW>(); }
-    else { if (pf_young) wait_vmcnt<PFW>(); else wait_vmcnt<0>(); }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
-    if (t == 0) prefetch_sgd();
-
+  auto mma_slot = [&](int t) {
     const char* sa0 = smem + (t % STAGES) * SLOT;
     const char* sb0 = sa0 + A_BYTES;
 #pragma unroll
@@ -552,6 +542,24 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(STAGES - 2, nk - 1 - t);
+    // stages 1..STAGES-1 were issued before the prefetch (t = 0): its PFW ops are younger than them
+    const bool pf_young = SGDPF && t >= 1 && t <= STAGES - 1;
+    if (ahead >= 2) { if (pf_young) wait_vmcnt<2 * LPW + PFW>(); else wait_vmcnt<2 * LPW>(); }
+    else if (ahead == 1) { if (pf_young) wait_vmcnt<LPW + PFW>(); else wait_vmcnt<LPW>(); }
+    else { if (pf_young) wait_vmcnt<PFW>(); else wait_vmcnt<0>(); }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    if (t == 0) prefetch_sgd();
+    mma_slot(t);
   }
 
   // ---- in-launch split-K combine (cdna_hip_programming §5 "Projection GEMM" item 2, sc1 form) ----
@@ -733,14 +741,18 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+constexpr int kNumCfgs = 16;
+// 8-wave configs whose register budget has no room for the in-launch column-sum finish
+static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
+
 // Row-parts the epilogue stages the tile in (BatchNorm statistics come out per part).
 static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {
-  static const int t[16][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {128, 64},
-                               {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
-                               {128, 128}, {128, 128}};
-  const int c = (cfg >= 0 && cfg <= 15) ? cfg : 7;
+  static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
+                                     {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
+                                     {128, 128}, {128, 128}};
+  const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
 }

@@ -46,7 +46,7 @@ struct Cfg {
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
 template <int STAGES>
-__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int spread) {
+__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
@@ -80,39 +80,46 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     const __amdgpu_buffer_rsrc_t rb0 = __builtin_amdgcn_make_buffer_rsrc((void*)p0.B, 0, p0.b_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)p1.A, 0, p1.a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rb1 = __builtin_amdgcn_make_buffer_rsrc((void*)p1.B, 0, p1.b_bytes, 0x00020000);
+    // One LDS-DMA ring across ALL of this workgroup's tiles: K-step g of the workgroup's sequence is K-step
+    // g % nk of its tile g / nk, and stage g + STAGES - 1 is issued during K-step g even when it belongs to
+    // the next tile, so the ring never drains and refills at a tile boundary (with K = 512 a tile is only
+    // nk = 8 K-steps: a per-tile refill cost ~2 of every 10 K-steps of L2 latency).
+    const int G = nt * nk;
+    auto issue = [&](int g) {
+      int m0, n0;
+      const int sel = tile_origin(g / nk, m0, n0);
+      const int kt = g % nk;
+      const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0, rb = sel ? rb1 : rb0;
+      const int lda = sel ? p1.lda : p0.lda, ldb = sel ? p1.ldb : p0.ldb;
+      const int Mg = sel ? p1.M : p0.M, Ng = sel ? p1.N : p0.N;
+      char* slot = smem + (g % STAGES) * SLOT;
+      pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, kt * 64, p.K, wave, lane);
+      pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, kt * 64, p.K, wave,
+                                                       lane);
+    };
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < G) issue(s);
     for (int i = 0; i <= nt; ++i) {
       if (i == nt) {  // drain iteration: the stream waves finish the last tile
         for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
       } else {
-        int m0, n0;
-        const int sel = tile_origin(i, m0, n0);
-        const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0, rb = sel ? rb1 : rb0;
-        const int lda = sel ? p1.lda : p0.lda, ldb = sel ? p1.ldb : p0.ldb;
-        const int Mg = sel ? p1.M : p0.M, Ng = sel ? p1.N : p0.N;
-        auto issue = [&](int t) {
-          char* slot = smem + (t % STAGES) * SLOT;
-          pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, t * 64, p.K, wave, lane);
-          pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, t * 64, p.K,
-                                                           wave, lane);
-        };
         f32x4 acc[FM][FN];
 #pragma unroll
         for (int a = 0; a < FM; ++a)
 #pragma unroll
           for (int b = 0; b < FN; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < STAGES - 1; ++s)
-          if (s < nk) issue(s);
         for (int t = 0; t < nk; ++t) {
-          const int ahead = min(STAGES - 2, nk - 1 - t);
-          // stage t landed: everything but the (up to STAGES - 2) younger stages' DMAs
+          const int g = i * nk + t;
+          const int ahead = min(STAGES - 2, G - 1 - g);
+          // stage g landed: everything but the (up to STAGES - 2) younger stages' DMAs
           if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LPW>();
           else if (ahead >= 1) pipe::wait_vmcnt<LPW>();
           else pipe::wait_vmcnt<0>();
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
-          if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
-          const char* sa = smem + (t % STAGES) * SLOT;
+          if (g + STAGES - 1 < G) issue(g + STAGES - 1);
+          const char* sa = smem + (g % STAGES) * SLOT;
           const char* sb = sa + A_SUB;
 #pragma unroll
           for (int kk = 0; kk < 64; kk += 32) {
@@ -140,78 +147,88 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     }
   } else {
     // ---------------------------------------------------------------- stream waves
+    // Vector v of tile i-1 (row row0 + 8 v, columns col..col+3 of the tile) is updated in K-step v of
+    // iteration i (nk == VPT: one vector per K-step).  Its master / momentum loads are issued DIST K-steps
+    // earlier — for the first DIST vectors of a tile, in the last K-steps of the previous iteration — into a
+    // ring of DIST register slots.  Profiled on MI355X (benchmarks/stream_probe.hip): 4 waves per CU stream the
+    // optimizer's 18 B per weight at 6.2 TB/s with 4 vectors in flight per thread, against 3.5 TB/s holding a
+    // whole tile (8 vectors, 128 VGPRs of state) ahead, which also pushed this kernel into register spills.
+    constexpr int DIST = 4;
+    static_assert(VPT % DIST == 0, "ring");
     const int st = tid - 256;
-    const int row0 = st >> 5, col = 4 * (st & 31);  // vector v: row row0 + 8 v, columns col..col+3
+    const int row0 = st >> 5, col = 4 * (st & 31);
     const float lr = *p.sgd.lr;
     const float mom = p.sgd.mom, wd = p.sgd.wd;
     const bool has_mom = mom != 0.f;
-    f32x4 pc[VPT], mc[VPT], pn[VPT], mn[VPT];
-    auto load_tile = [&](int i, f32x4 (&pv)[VPT], f32x4 (&mv)[VPT]) {
+    f32x4 rp0, rp1, rp2, rp3, rm0, rm1, rm2, rm3;  // the ring (statically indexed)
+    // load vector v of tile j into a ring slot
+    auto load_vec = [&](int j, int v, f32x4& pv, f32x4& mv) {
       int m0, n0;
-      const int sel = tile_origin(i, m0, n0);
+      const int sel = tile_origin(j, m0, n0);
       const SgdArgs& sg = sel ? p1.sgd : p0.sgd;
-      const int ldc = sel ? p1.ldc : p0.ldc;
-#pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const size_t off = (size_t)(m0 + row0 + 8 * v) * ldc + n0 + col;
-        pv[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.p + off));
-        mv[v] = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.buf + off))
-                        : (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
+      const size_t off = (size_t)(m0 + row0 + 8 * v) * (sel ? p1.ldc : p0.ldc) + n0 + col;
+      pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.p + off));
+      mv = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.buf + off))
+                   : (f32x4){0.f, 0.f, 0.f, 0.f};
     };
-    int pm0 = 0, pn0 = 0, psel = 0;  // origin / GEMM of the tile being updated (i - 1)
-    for (int i = 0; i <= nt; ++i) {
-      if (i < nt) load_tile(i, pn, mn);  // one iteration ahead of its update
-      const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
-      for (int t = 0; t < nk; ++t) {
-        __builtin_amdgcn_s_barrier();
-        if (i == 0) continue;
-        // this K-step's share of tile i-1's update
-        // spread = 1: one share per K-step; spread = s > 1: the update in the first ceil(nk / s) K-steps
-        // (more stores in flight early in the tile period)
-        const int nks = (nk + spread - 1) / spread;
-        const int v0 = t < nks ? t * VPT / nks : VPT, v1 = t < nks ? (t + 1) * VPT / nks : VPT;
+    // update vector v of tile j from the gradient tile T, then refill the slot with the vector DIST ahead
+    auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
+      int m0, n0;
+      const int sel = tile_origin(j, m0, n0);
+      const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + 8 * v) * ALD + col);
+      f32x4 po, bo;
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-          if (v < v0 || v >= v1) continue;
-          const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + 8 * v) * ALD + col);
-          f32x4 po, bo;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
-            float d = fmaf(wd, pc[v][q], g[q]);
-            if (has_mom) {
-              d = fmaf(mom, mc[v][q], d);
-              bo[q] = d;
-            }
-            po[q] = fmaf(-lr, d, pc[v][q]);
-          }
-          const SgdArgs& sg = psel ? p1.sgd : p0.sgd;
-          const size_t off = (size_t)(pm0 + row0 + 8 * v) * (psel ? p1.ldc : p0.ldc) + pn0 + col;
-          __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(sg.p + off));
-          if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sg.buf + off));
-          if (sg.shadow)
-            *reinterpret_cast<u32x2*>(sg.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
+        float d = fmaf(wd, pv[q], g[q]);
+        if (has_mom) {
+          d = fmaf(mom, mv[q], d);
+          bo[q] = d;
         }
+        po[q] = fmaf(-lr, d, pv[q]);
+      }
+      const SgdArgs& sg = sel ? p1.sgd : p0.sgd;
+      const size_t off = (size_t)(m0 + row0 + 8 * v) * (sel ? p1.ldc : p0.ldc) + n0 + col;
+      __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(sg.p + off));
+      if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sg.buf + off));
+      if (sg.shadow)
+        *reinterpret_cast<u32x2*>(sg.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1
+      const int vn = v + DIST;
+      if (vn < VPT) load_vec(j, vn, pv, mv);
+      else if (j + 1 < nt) load_vec(j + 1, vn - VPT, pv, mv);
+    };
+    // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
+    if (nt > 0) {
+      load_vec(0, 0, rp0, rm0);
+      load_vec(0, 1, rp1, rm1);
+      load_vec(0, 2, rp2, rm2);
+      load_vec(0, 3, rp3, rm3);
+    }
+    for (int i = 0; i <= nt; ++i) {
+      const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
+      for (int t = 0; t < nk; t += DIST) {
+        // K-steps t .. t+3 of iteration i: vectors t .. t+3 of tile i-1 (nk == VPT)
+        __builtin_amdgcn_s_barrier();
+        if (i > 0) update_vec(i - 1, t, T, rp0, rm0);
+        __builtin_amdgcn_s_barrier();
+        if (i > 0) update_vec(i - 1, t + 1, T, rp1, rm1);
+        __builtin_amdgcn_s_barrier();
+        if (i > 0) update_vec(i - 1, t + 2, T, rp2, rm2);
+        __builtin_amdgcn_s_barrier();
+        if (i > 0) update_vec(i - 1, t + 3, T, rp3, rm3);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (i < nt) {
-#pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-          pc[v] = pn[v];
-          mc[v] = mn[v];
-        }
-        psel = tile_origin(i, pm0, pn0);
-      }
     }
   }
 }
 
 // Eligible shapes: the plain weight-gradient layout (A M-contig, B N-contig), M % 64 == 0, N % 128 == 0,
-// K % 64 == 0 (whole K-steps: the two roles' barrier counts are nk), ldc % 4 == 0.
+// K == 512 (the batch: nk = 8 K-steps of 64, one optimizer vector per K-step; the two roles' barrier counts
+// are nk + 1 per iteration), ldc % 4 == 0.
 static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
-  return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K % 64 == 0 && p.K >= 64 && (p.ldc & 3) == 0 &&
-         p.sgd.p && p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf);
+  return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K == 64 * VPT && (p.ldc & 3) == 0 && p.sgd.p &&
+         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf);
 }
 
 // Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:

@@ -18,6 +18,7 @@
 // either stores the gradient or applies the fused SGD update.
 // The forward epilogue can emit per-tile BatchNorm statistics (mean, M2 of
 // the stored bf16 outputs) for the fused BN that follows (bn.hip).
+#include "ddpx_gemm_dispatch.h"
 #include "ddpx_pipe.h"
 
 namespace ddpx {
@@ -177,7 +178,7 @@ DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats,
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = make_geom(H, W, C, P);
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
-  return (int)dispatch<true, true, MODE_IM2COL_FWD, MODE_PLAIN>(p, cfg, 1, s);
+  return (int)dispatch_conv_fwd(p, cfg, s);
 }
 
 // dx[P][C] = dgrad(dy, W) (optionally times relu mask of aux — unused by VGG, whose
@@ -200,7 +201,7 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = make_geom(H, W, Co, P);
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
-  return (int)dispatch<true, false, MODE_IM2COL_BWD, MODE_PLAIN>(p, cfg, 1, s);
+  return (int)dispatch_conv_dgrad(p, cfg, s);
 }
 
 static int pick_wgrad(int P, int C, int Co) {
@@ -273,7 +274,7 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
     hipMemsetAsync(part + (size_t)Sreal * p.split_stride, 0, (size_t)(S - Sreal) * p.split_stride * 4, s);
   }
   const int cfg = tile_cfg >= 0 ? tile_cfg : pick_wgrad(P, C, Co);
-  return (int)dispatch<false, false, MODE_PLAIN, MODE_IM2COL_COL>(p, cfg, Sreal, s);
+  return (int)dispatch_conv_wgrad(p, cfg, Sreal, s);
 }
 
 DDPX_API int ddpx_conv_wgrad_reduce(const float* part, int S, int Co, int Cr, int Cp, void* out, int out_bf16,

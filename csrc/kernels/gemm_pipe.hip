@@ -33,6 +33,7 @@
 //    bias gradient of the layer below) written as [tiles_m][N] partials.
 #include <cstdlib>
 
+#include "ddpx_gemm_dispatch.h"
 #include "ddpx_pipe.h"
 #include "ddpx_wgrad_sgd.h"
 
@@ -142,7 +143,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   p.sgd_plain = sgd_plain;
   int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
-  if (cs_tcnt && (cfg == 8 || cfg >= 13)) return -11;  // in-launch column sums: 4-wave tiles only
+  if (cs_tcnt && pipe::eight_wave(cfg)) return -11;  // in-launch column sums: 4-wave tiles only
   if (splits > 1) {  // in-launch split-K (ddpx_gemm_pipe_plan): the caller's cfg, slab and zeroed tickets
     if (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || !slab || !tcnt || tile_cfg < 0 || !a_kcontig)
       return -7;
@@ -191,19 +192,18 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   }();
   if (epi == pipe::EPI_SGD && sgd_pf && !a_kcontig && !b_kcontig && (ldc & 3) == 0 &&
       (size_t)M * ldc * 4 < 0x80000000ull && (cfg == 3 || cfg == 5 || cfg == 7 || cfg == 12)) {
-    return (int)pipe::dispatch_sgd_prefetch<false, false>(p, cfg, stream);
+    return (int)pipe::dispatch_sgd_prefetch_mn(p, cfg, stream);
   }
   hipError_t e;
   if (splits > 1) {
-    e = b_kcontig ? pipe::dispatch_sk<true, true>(p, cfg, splits, stream)
-                  : pipe::dispatch_sk<true, false>(p, cfg, splits, stream);
+    e = b_kcontig ? pipe::dispatch_sk_kk(p, cfg, splits, stream) : pipe::dispatch_sk_kn(p, cfg, splits, stream);
     return (int)e;
   }
   const int S = 1;
-  if (a_kcontig && b_kcontig) e = pipe::dispatch<true, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
-  else if (a_kcontig) e = pipe::dispatch<true, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
-  else if (b_kcontig) e = pipe::dispatch<false, true, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
-  else e = pipe::dispatch<false, false, pipe::MODE_PLAIN, pipe::MODE_PLAIN>(p, cfg, S, stream);
+  if (a_kcontig && b_kcontig) e = pipe::dispatch_kk(p, cfg, S, stream);
+  else if (a_kcontig) e = pipe::dispatch_kn(p, cfg, S, stream);
+  else if (b_kcontig) e = pipe::dispatch_mk(p, cfg, S, stream);
+  else e = pipe::dispatch_mn(p, cfg, S, stream);
   return (int)e;
 }
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import glob
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -52,16 +53,30 @@ def _run(cmd, verbose):
     return r.stdout
 
 
+_INCLUDE = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _deps(src, inc_dir, seen=None):
+    """``src`` and the csrc/include headers it includes, transitively (quoted includes only)."""
+    seen = set() if seen is None else seen
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    with open(src, errors="replace") as f:
+        for name in _INCLUDE.findall(f.read()):
+            _deps(os.path.join(inc_dir, name), inc_dir, seen)
+    return seen
+
+
 def _compile_objs(srcs, flags, verbose, jobs):
     os.makedirs(OBJ_DIR, exist_ok=True)
-    hdrs = glob.glob(os.path.join(CSRC, "include", "*.h"))
-    hdr_t = _newest(hdrs)
+    inc_dir = os.path.join(CSRC, "include")
     hipcc = _hipcc()
     todo, objs = [], []
     for s in srcs:
         o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
+        if not os.path.exists(o) or os.path.getmtime(o) < _newest(_deps(s, inc_dir)):
             todo.append((s, o))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = [ex.submit(_run, [hipcc, *flags, "-c", s, "-o", o], verbose) for s, o in todo]
