@@ -65,6 +65,8 @@ def parse(argv=None):
     p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
                    help="compute precision of the ddpx engine on the GPU: bf16 (default) or fp32, the reference's "
                         "recipe on the exact-f32 MFMA kernels (the stock reference then runs without autocast)")
+    p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
+                   help="ddpx engine ops: auto = hand-written kernels except VGG at fp32 (MIOpen convolutions)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--graph_steps", type=int, default=1,
                    help="training steps per captured HIP graph (the launch gap between replays is paid once "
@@ -193,10 +195,14 @@ def make_data(args, device, rank, world, layout=None):
     ds = synthetic_cifar(args.train_size, seed=0)
     sampler = DistributedIndexSampler(len(ds), world, rank, shuffle=True, seed=0)
     if layout is None:
-        layout = "flat_bf16" if (args.impl == "ddpx" and args.model.startswith("mlp")) else "nchw_f32"
-        if args.impl == "ddpx" and args.model in ("vgg", "deepnn"):
+        from ddpx.models import native_kernels_for
+        fp32 = getattr(args, "dtype", "auto") == "fp32"
+        native = args.impl == "ddpx" and native_kernels_for(args.model, "fp32" if fp32 else "bf16",
+                                                            getattr(args, "kernels", "auto"))
+        layout = "flat_bf16" if (native and args.model.startswith("mlp")) else "nchw_f32"
+        if native and args.model in ("vgg", "deepnn"):
             layout = "nhwc8_bf16"
-        if args.impl == "ddpx" and getattr(args, "dtype", "auto") == "fp32":
+        if native and fp32:
             layout = {"vgg": "nhwc4_f32", "deepnn": "nchw_f32"}.get(args.model, "flat_f32")
         if device.type == "cpu":
             layout = "nchw_f32"
@@ -259,7 +265,7 @@ def build_ddpx(args, device, world):
     cpu = device.type == "cpu"
     fp32 = cpu or args.dtype == "fp32"
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="fp32" if fp32 else "bf16",
-                        device=device, fp8=bool(args.fp8))
+                        device=device, fp8=bool(args.fp8), kernels=args.kernels)
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     # single process: the SGD update may be fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4,
@@ -422,6 +428,13 @@ def main(argv=None):
     resolve_defaults(args, world)
     cpu = args.device == "cpu"
     if args.comm == "host" or cpu:
+        args.no_graph = True
+    from ddpx.models import native_kernels_for
+    if args.impl == "ddpx" and not native_kernels_for(args.model, "fp32" if args.dtype == "fp32" else "bf16",
+                                                      args.kernels):
+        # torch ops under the ddpx engine (VGG at fp32: MIOpen convolutions) run eagerly: capturing torch's
+        # autograd with AccumulateGrad nodes made by the eager warm-up steps crashed the process (exit -11);
+        # a ~20 ms step does not need the graph's launch savings
         args.no_graph = True
     device = torch.device("cpu") if cpu else torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
@@ -592,6 +605,7 @@ def main(argv=None):
                  "-resident, crop+flip augment per step; random-init weights)"),
         "config": {"model": model_name, "global_batch": bs * world, "per_gpu_batch": bs, "seq_len": None,
                    "parallelism": f"dp{world}", "device": args.device, "impl": args.impl,
+                   "kernels": (args.kernels if args.impl == "ddpx" else None),
                    "launcher": os.environ.get(LAUNCHER_ENV, "torchrun/external" if world > 1 else "none"),
                    "comm": (args.comm if ddpx_ddp else None),
                    "graph": bool(runner is not None and runner.use_graph),

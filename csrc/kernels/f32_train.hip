@@ -17,6 +17,8 @@
 //     torch) and the ReLU mask recomputed from the saved pre-BN activation;
 //   * global average pool, and the 10-class head: logits + softmax cross-entropy + dlogits, with
 //     dW / db / dfeature (+ ReLU mask for the MLP) in the backward.
+#include <cstdlib>
+
 #include "ddpx_common.h"
 
 namespace ddpx {
@@ -94,7 +96,7 @@ enum Flags { F_RELU = 1, F_ACCUM = 2, F_SPLIT = 4 };
 
 // C[m][n] (+)= sum_k A(m,k) B(k,n)  [+ bias[n]] [relu] [* (mask[m][n] > 0)]; F_SPLIT: the K range of
 // blockIdx's split z goes to the raw slab C + z * split_stride.
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, bool PLAIN>
 __global__ void __launch_bounds__(NT)
 gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C, int ldc,
                 long split_stride, const float* __restrict__ bias, const float* __restrict__ mask, int flags,
@@ -136,10 +138,17 @@ gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchun
       sa.load(A, m0, k0 + (it + 1) * BK, k1, tid);
       sb.load(B, n0, k0 + (it + 1) * BK, k1, tid);
     }
-    // blocked summation: each K step's 16 products go into a fresh accumulator that is then added to the
-    // running sum — the rounding chain is K/16 long instead of K (4x smaller error at K = 4608, where a
-    // plain MFMA chain left the conv7 output 4e-6 from fp64, enough to flip max-pool routings)
+    // blocked summation (PLAIN = false): each K step's 16 products go into a fresh accumulator that is then
+    // added to the running sum — the rounding chain is K/16 long instead of K (4x smaller error at K = 4608,
+    // where a plain MFMA chain left the conv7 output 4e-6 from fp64).  PLAIN: one MFMA chain over K, the
+    // summation order of the fp32 library kernels (held to their error vs fp64: tests/test_gpu_f32.py).
     f32x4 part[FM][FN];
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) part[i][j] = acc[i][j];
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       float a[FM], b[FN];
@@ -151,13 +160,16 @@ gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchun
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], kk ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f},
-                                                            0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a[i], b[j], (PLAIN || kk) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (PLAIN) acc[i][j] = part[i][j];
+        else acc[i][j] += part[i][j];
+      }
     if (more) {
       sa.store(As[cur ^ 1], tid);
       sb.store(Bs[cur ^ 1], tid);
@@ -187,6 +199,21 @@ gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchun
       }
 }
 
+// Summation order of the f32 core (DDPX_F32_SUM=plain|blocked|auto, default auto).  The bar is the stock fp32
+// libraries' own error vs fp64 on the same inputs (tests/test_gpu_f32.py::test_error_no_worse_than_stock,
+// MI355X: profiles/r3_f32): the plain chain matches hipBLASLt on the MLP's fc1 (1.15e-6 vs 1.15e-6 rel-L2)
+// and is 1.15-1.3x MIOpen's error on VGG's conv7 / conv4, where a few max-pool routing flips then move the
+// gradients below them 4x further than torch's own fp32 run does; the blocked form is 2-4x MORE accurate
+// than the libraries.  auto: plain for dense GEMMs (Linear layers: 1.056 vs 1.150 ms per toy-MLP step),
+// blocked for the im2col convolution GEMMs.
+static int f32_sum_mode() {  // 0 auto, 1 plain, 2 blocked
+  static const int v = [] {
+    const char* e = getenv("DDPX_F32_SUM");
+    return !e ? 0 : e[0] == 'p' ? 1 : e[0] == 'b' ? 2 : 0;
+  }();
+  return v;
+}
+
 template <int BM, int BN, int AM, int BMD>
 static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
                    long split_stride, const float* bias, const float* mask, int flags, hipStream_t s) {
@@ -194,8 +221,14 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
   int kchunk = (K + splits - 1) / splits;
   kchunk = (kchunk + BK - 1) / BK * BK;
   const int nwg = tm * tn * splits;
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AM, BMD>), dim3(nwg), dim3(NT), 0, s, A, B, M, N, K, kchunk, C, ldc,
-                     split_stride, bias, mask, flags, tm, tn);
+  const int mode = f32_sum_mode();
+  const bool conv = AM == IM2COL_KC || BMD == IM2COL_OC;
+  if (mode == 1 || (mode == 0 && !conv))
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AM, BMD, true>), dim3(nwg), dim3(NT), 0, s, A, B, M, N, K, kchunk, C,
+                       ldc, split_stride, bias, mask, flags, tm, tn);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AM, BMD, false>), dim3(nwg), dim3(NT), 0, s, A, B, M, N, K, kchunk, C,
+                       ldc, split_stride, bias, mask, flags, tm, tn);
 }
 
 template <int AM, int BMD>

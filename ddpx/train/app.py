@@ -52,7 +52,8 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--test_size", type=int, default=10000, help="synthetic test-set size")
     p.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"])
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
-    p.add_argument("--kernels", default="native", choices=["native", "torch"])
+    p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
+                   help="auto: hand-written kernels, except VGG at fp32 (MIOpen convolutions are faster there)")
     p.add_argument("--bucket_cap_mb", type=float, default=25.0)
     p.add_argument("--first_bucket_mb", type=float, default=1.0)
     p.add_argument("--steps_per_epoch", default="compat", help="'compat' (98/49 as the reference), 'auto' or N")

@@ -144,7 +144,7 @@ def _train_pair(gpu, name, steps, lr=0.05):
     from ddpx.models import build_model
     from ddpx.optim.sgd import SGD
     torch.manual_seed(4)
-    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None)
+    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None, kernels="native")
     ref = copy.deepcopy(native).to(gpu)
     ref.use_native = False
     ddpx.prepare_model(native, gpu)
@@ -177,7 +177,7 @@ def test_native_fp32_gradients_match_torch_fp32(gpu, name):
     import ddpx
     from ddpx.models import build_model
     torch.manual_seed(7)
-    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None)
+    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None, kernels="native")
     ref = copy.deepcopy(native).to(gpu)
     ref.use_native = False
     flat = ddpx.prepare_model(native, gpu)
@@ -231,7 +231,7 @@ def test_vgg_fp32_eval_logits(gpu):
     from ddpx.models import build_model
     import ddpx
     torch.manual_seed(6)
-    m = build_model("vgg", dtype="fp32", device=gpu)
+    m = build_model("vgg", dtype="fp32", device=gpu, kernels="native")
     ddpx.prepare_model(m, gpu)
     m.eval()
     x = torch.rand(32, 3, 32, 32, device=gpu)
@@ -240,3 +240,45 @@ def test_vgg_fp32_eval_logits(gpu):
         m.use_native = False
         want = m(x)
     assert _rel(got, want) < 1e-4
+
+
+def _err_vs_fp64(out, ref):
+    out, ref = out.double(), ref.double()
+    return {"rel_l2": ((out - ref).norm() / ref.norm()).item(), "max_abs": (out - ref).abs().max().item()}
+
+
+@pytest.mark.parametrize("case", ["fc1", "conv7", "conv4"])
+def test_error_no_worse_than_stock(gpu, case):
+    """The accuracy bar of the native fp32 kernels is the stock fp32 libraries' own error against fp64
+    (hipBLASLt for the MLP's fc1, MIOpen for VGG's conv7 / conv4), measured here on the same inputs: the
+    native result may not be more than 1.5x further from fp64 than torch's fp32 result."""
+    import json
+    import os
+    from ddpx.ops import f32
+    torch.manual_seed(3)
+    if case == "fc1":
+        x = torch.randn(512, 4096, device=gpu)
+        w = torch.randn(4096, 4096, device=gpu) / 64.0
+        ref = x.double() @ w.double().t()
+        stock = x @ w.t()
+        ours = f32.linear_fwd(x, w)
+    else:
+        N, H, Ci, Co = (512, 4, 512, 512) if case == "conv7" else (512, 8, 256, 512)
+        x = torch.relu(torch.randn(N, Ci, H, H, device=gpu))
+        w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+        cols = F.unfold(x.double(), 3, padding=1)                      # [N, Ci*9, H*W]
+        ref = (w.double().view(Co, -1) @ cols).view(N, Co, H, H)
+        stock = F.conv2d(x, w, padding=1)
+        Cp = f32.conv_channels(Ci)
+        xn = F.pad(x.permute(0, 2, 3, 1), (0, Cp - Ci)).contiguous()
+        wf = torch.empty(9 * Cp * Co, device=gpu)
+        f32.conv_wprep(w, wf, None)
+        ours = f32.conv_fwd(xn, wf, Co).view(N, H, H, Co).permute(0, 3, 1, 2)
+        ref, stock = ref.permute(0, 2, 3, 1), stock.permute(0, 2, 3, 1)
+        ours = ours.permute(0, 2, 3, 1)
+    e_stock, e_ours = _err_vs_fp64(stock, ref), _err_vs_fp64(ours, ref)
+    rec = {"case": case, "stock": e_stock, "native": e_ours, "sum": os.environ.get("DDPX_F32_SUM", "plain")}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/f32_error.jsonl", "a") as f:
+        f.write(json.dumps(rec) + "\n")
+    assert e_ours["rel_l2"] <= 1.5 * e_stock["rel_l2"] + 1e-9, rec
