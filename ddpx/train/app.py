@@ -207,6 +207,11 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
             if getattr(model, "native_dtype", "bf16") == "fp32":
                 model.use_native = False  # fp32 SyncBatchNorm: torch-op BatchNorm on the merged statistics
             model = convert_sync_batchnorm(model, comm)
+    if args.graph and device.type == "cuda" and not getattr(model, "use_native", True):
+        # torch-op models (e.g. VGG at fp32 on MIOpen convolutions) step eagerly: capturing torch's autograd with
+        # AccumulateGrad nodes created by the eager warm-up steps is not supported (it crashed in bench.py)
+        print("note: --graph ignored for the torch-op model path", flush=True)
+        args.graph = False
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"),
