@@ -107,6 +107,9 @@ def parse(argv=None):
                    help="1: also time the stock PyTorch recipe (torch.nn + torch DDP over RCCL at N > 1) in this "
                         "job, after the ddpx timing, on the same data (default 1)")
     p.add_argument("--stock_steps", type=int, default=30)
+    p.add_argument("--stock_first", type=int, default=None,
+                   help="1: time the stock recipe BEFORE the ddpx warm-up instead of after the ddpx timing "
+                        "(default 0)")
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args(argv)
 
@@ -241,6 +244,10 @@ def resolve_defaults(args, world):
     resolve_zero_defaults(args)
     if args.stock_ref is None:
         args.stock_ref = int(args.impl == "ddpx" and not args.ddp_single and args.comm == "rccl")
+    if args.stock_first is None:
+        # measured (profiles/r3_val): stock-first gives the stock recipe a cold GPU (0.88-0.90 vs 0.62-0.73 ms) and
+        # ddpx no clear gain, so the baseline runs last unless asked
+        args.stock_first = 0
 
 
 def resolve_zero_defaults(args):
@@ -365,7 +372,8 @@ def torch_runner(args, device, world, loader, idx_all, full, group=None):
 
 
 def measure_stock_same_run(args, device, world, rank, idx_all, full):
-    """The stock PyTorch-ROCm recipe timed in this job after the ddpx measurement, on the same data:
+    """The stock PyTorch-ROCm recipe timed in this job (after the ddpx timing unless --stock_first 1), on the
+    same data:
     torch.nn model + bf16 autocast (fp32 when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its
     own RCCL process group (the reference's ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same
     timing rule as the ddpx line: barrier + synchronize on both sides, max over ranks.  Collective."""
@@ -543,6 +551,10 @@ def main(argv=None):
     else:
         model, net, opt, sched, run = torch_runner(args, device, world, loader, idx_all, full)
 
+    stock = None
+    if args.stock_ref and args.stock_first:
+        # the baseline first (same process, same data), then the ddpx warm-up and timed steps
+        stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
     # warmup (includes graph capture for ddpx)
     loss = run(0, args.warmup) if args.warmup else None
     sync()
@@ -575,8 +587,7 @@ def main(argv=None):
         consistent = all(c == allck[0] for c in allck)
         esz = net.flat.grad.element_size()
         buckets_mb = [round((e - s) * esz / 2 ** 20, 3) for s, e in net.bucket_ranges]
-    stock = None
-    if args.stock_ref:
+    if args.stock_ref and not args.stock_first:
         stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0

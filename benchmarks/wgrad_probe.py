@@ -53,7 +53,7 @@ def main():
         row = {"hipblaslt_bf16": timeit(lambda: dy.t() @ x)}
         row["sgd_flat_f32g"] = timeit(lambda: native.check(lib.ddpx_sgd_flat(
             p.data_ptr(), buf.data_ptr(), dw.data_ptr(), 0, sh.data_ptr(), p.numel(), lr.data_ptr(), 0.0, 0.9, 5e-4,
-            1.0, 0, 0, native.stream_handle()), "sgd"))
+            1.0, 0, 0, None, None, native.stream_handle()), "sgd"))
         for c in cfgs:
             row[f"f32_t{c}"] = timeit(lambda: G.linear_wgrad(dy, x, dw, tile=c))
             row[f"sgd_t{c}"] = timeit(lambda: G.linear_wgrad(dy, x, None, tile=c, sgd=sgd))

@@ -66,11 +66,16 @@ struct SgdArgs {
   unsigned short* shadow; // bf16 compute copy (may be null)
   const float* lr;        // device scalar
   float mom, wd;
+  // MX-FP8 (e4m3) copy of the updated weights, written next to the bf16 one by the optimizer streams
+  // that support it (ddpx_mx.h): codes at the element offset, E8M0 scales at element offset / 32.
+  unsigned char* q8 = nullptr;
+  unsigned char* s8 = nullptr;
 };
 
 // Master and momentum are read-once / write-once streams: non-temporal, so the update leaves no
 // dirty L2 / MALL lines for the next forward's GEMMs to write back (profiles/r1_sgdnt).
-__device__ __forceinline__ void sgd_apply(const SgdArgs& s, size_t i, float g, float lr) {
+// Returns the updated parameter (for epilogues that also write it in a derived layout).
+__device__ __forceinline__ float sgd_apply(const SgdArgs& s, size_t i, float g, float lr) {
   float p = __builtin_nontemporal_load(s.p + i);
   float d = fmaf(s.wd, p, g);
   if (s.mom != 0.f) {
@@ -80,6 +85,7 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& s, size_t i, float g, f
   p = fmaf(-lr, d, p);
   __builtin_nontemporal_store(p, s.p + i);
   if (s.shadow) s.shadow[i] = f2bf(p);
+  return p;
 }
 
 }  // namespace ddpx

@@ -21,6 +21,7 @@
 
 #include <cstdlib>
 
+#include "ddpx_mx.h"
 #include "ddpx_pipe.h"
 
 namespace ddpx {
@@ -192,6 +193,16 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
       if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sg.buf + off));
       if (sg.shadow)
         *reinterpret_cast<u32x2*>(sg.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      if (sg.q8) {  // MX-FP8 weight copy for the next forward: 8 lanes = one 32-column block (uniform branch)
+        unsigned e8;
+        const unsigned q = mx::e4m3_group8(po, &e8);
+        *reinterpret_cast<unsigned*>(sg.q8 + off) = q;
+        // the row's 4 block scales (lanes 0/8/16/24 of each half-wave) as ONE dword store by the half-wave's
+        // first lane: byte stores scattered over the tile's rows cost more than the codes themselves
+        const unsigned e1 = __shfl_down(e8, 8, 64), e2 = __shfl_down(e8, 16, 64), e3 = __shfl_down(e8, 24, 64);
+        if ((lane & 31) == 0)
+          *reinterpret_cast<unsigned*>(sg.s8 + (off >> 5)) = e8 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+      }
       // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1
       const int vn = v + DIST;
       if (vn < VPT) load_vec(j, vn, pv, mv);
@@ -228,7 +239,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
 // are nk + 1 per iteration), ldc % 4 == 0.
 static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
   return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K == 64 * VPT && (p.ldc & 3) == 0 && p.sgd.p &&
-         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf);
+         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3)));
 }
 
 // Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:

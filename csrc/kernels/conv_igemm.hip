@@ -48,7 +48,9 @@ __global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restric
 // SGD-updated) contiguously.  Fixed summation order: deterministic.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Cr,
                                                            int Cp, void* __restrict__ out, int out_bf16,
-                                                           int accumulate, SgdArgs sgd) {
+                                                           int accumulate, SgdArgs sgd,
+                                                           unsigned short* __restrict__ wf,
+                                                           unsigned short* __restrict__ wd) {
   constexpr int CT = 64;
   __shared__ float red[9][CT + 1];
   __shared__ float sred[256];
@@ -98,7 +100,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     const float v = red[t][cc];
     const size_t i = base + q;
     if (sgd.p) {
-      sgd_apply(sgd, i, v, *sgd.lr);
+      const float pn = sgd_apply(sgd, i, v, *sgd.lr);
+      if (wf) {  // the forward / dgrad GEMM layouts of the updated weight (weight_prep's output)
+        const unsigned short h = f2bf(pn);
+        wf[((size_t)o * 9 + t) * Cp + c0 + cc] = h;
+        wd[((size_t)t * Co + o) * Cp + c0 + cc] = h;
+      }
     } else if (out_bf16) {
       unsigned short* d = reinterpret_cast<unsigned short*>(out) + i;
       *d = f2bf(accumulate ? v + bf2f(*d) : v);
@@ -279,8 +286,13 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
 
 DDPX_API int ddpx_conv_wgrad_reduce(const float* part, int S, int Co, int Cr, int Cp, void* out, int out_bf16,
                                     int accumulate, float* sgd_p, float* sgd_buf, void* sgd_shadow,
-                                    const float* sgd_lr, float sgd_mom, float sgd_wd, hipStream_t s) {
+                                    const float* sgd_lr, float sgd_mom, float sgd_wd, void* wf, void* wd,
+                                    hipStream_t s) {
+  // wf / wd (fused SGD only): also write the updated weight as the forward [Co][9][Cp] and dgrad [9][Co][Cp] bf16
+  // layouts (their padded channels keep the zeros weight_prep wrote)
+  if ((wf != nullptr) != (wd != nullptr) || (wf && !sgd_p)) return -1;
   hipLaunchKernelGGL(conv::wgrad_reduce_kernel, dim3(Co, (Cr + 63) / 64), dim3(256), 0, s, part, S, Co, Cr, Cp, out,
-                     out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
+                     out_bf16, accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
+                     (unsigned short*)wf, (unsigned short*)wd);
   return (int)hipGetLastError();
 }

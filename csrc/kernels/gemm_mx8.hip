@@ -21,42 +21,23 @@
 // its bytes 0-15 are K [16g, 16g+16) and bytes 16-31 are K [64+16g, 64+16g+16) (g = l>>4), and the
 // scale byte lane-group g supplies (opsel 0) applies to K-block g = [32g, 32g+32) — so a block's
 // data sits in two lane groups.  Epilogues are the bf16 pipe's (bias/ReLU/bf16/f32/SGD).
+#include "ddpx_mx.h"
 #include "ddpx_pipe.h"
 
 namespace ddpx {
 namespace mx8 {
 
 using namespace pipe;
+using mx::block_exp;
+using mx::cvt_pk;
+using mx::kMaxE4M3;
+using mx::kMaxE5M2;
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-
-constexpr float kMaxE4M3 = 448.f;
-constexpr float kMaxE5M2 = 57344.f;
-
-template <bool HI>
-__device__ __forceinline__ unsigned cvt_pk(float a, float b, unsigned old, bool e5m2) {
-  if (e5m2) return (unsigned)__builtin_amdgcn_cvt_pk_bf8_f32(a, b, (int)old, HI);
-  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)old, HI);
-}
-
-// E8M0 exponent e such that amax * 2^-e <= maxv (e = ceil-ish(log2(amax / maxv))), clamped.
-__device__ __forceinline__ int block_exp(float amax, float maxv) {
-  if (!(amax > 0.f)) return -127;
-  int ex;
-  (void)frexpf(amax / maxv, &ex);  // amax/maxv = m * 2^ex, m in [0.5, 1)
-  return ex < -127 ? -127 : (ex > 127 ? 127 : ex);
-}
 
 // Quantise 32 values (one MX block) to 8 packed dwords.
 __device__ __forceinline__ void quant32(const float* v, float inv, float maxv, bool e5m2, unsigned* out) {
 #pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    float x0 = fminf(fmaxf(v[4 * w + 0] * inv, -maxv), maxv);
-    float x1 = fminf(fmaxf(v[4 * w + 1] * inv, -maxv), maxv);
-    float x2 = fminf(fmaxf(v[4 * w + 2] * inv, -maxv), maxv);
-    float x3 = fminf(fmaxf(v[4 * w + 3] * inv, -maxv), maxv);
-    unsigned r = cvt_pk<false>(x0, x1, 0u, e5m2);
-    out[w] = cvt_pk<true>(x2, x3, r, e5m2);
-  }
+  for (int w = 0; w < 8; ++w) out[w] = mx::quant4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3], inv, maxv, e5m2);
 }
 
 // Row-direction quantiser: x bf16 [R][C] (ld elems) -> q [R][C] (ldq bytes), s [R][C/32].

@@ -211,21 +211,23 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
 // shared K = batch): the toy MLP's fc1 and fc0 updates, independent once fc1's data gradient has run.
 // Returns -20 when the pair is not eligible (the caller then launches them one by one).
 DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0, int lda0, int ldb0, int ldc0,
-                                 float* p0, float* buf0, void* sh0, const void* A1, const void* B1, int M1, int N1,
-                                 int lda1, int ldb1, int ldc1, float* p1, float* buf1, void* sh1, int K,
-                                 const float* lr, float mom, float wd, hipStream_t stream) {
+                                 float* p0, float* buf0, void* sh0, void* q80, void* s80, const void* A1,
+                                 const void* B1, int M1, int N1, int lda1, int ldb1, int ldc1, float* p1, float* buf1,
+                                 void* sh1, void* q81, void* s81, int K, const float* lr, float mom, float wd,
+                                 hipStream_t stream) {
+  // q8_i / s8_i (optional): MX-FP8 codes + E8M0 scales of the updated W_i, written by the stream waves
   auto make = [&](const void* A, const void* B, int M, int N, int lda, int ldb, int ldc, float* pp, float* buf,
-                  void* sh) {
+                  void* sh, void* q8, void* s8) {
     const size_t a_bytes = ((size_t)(K - 1) * lda + M) * 2, b_bytes = ((size_t)(K - 1) * ldb + N) * 2;
     return pipe::Params{(const unsigned short*)A, (const unsigned short*)B, pp, nullptr, nullptr, nullptr,
                         M, N, K, lda, ldb, ldc, 0, pipe::EPI_SGD, 0, 1.f, (unsigned)a_bytes, (unsigned)b_bytes,
-                        SgdArgs{pp, buf, (unsigned short*)sh, lr, mom, wd}, pipe::make_geom(0, 0, 0, 0), 0, 0, 0,
-                        nullptr, 0u, nullptr, nullptr, 0, nullptr};
+                        SgdArgs{pp, buf, (unsigned short*)sh, lr, mom, wd, (unsigned char*)q8, (unsigned char*)s8},
+                        pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr, nullptr, 0, nullptr};
   };
   if (K <= 0 || lda0 % 8 || ldb0 % 8 || lda1 % 8 || ldb1 % 8 || M0 % 8 || N0 % 8 || M1 % 8 || N1 % 8) return -20;
   if (((uintptr_t)A0 | (uintptr_t)B0 | (uintptr_t)A1 | (uintptr_t)B1) & 15) return -20;
-  const pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0);
-  const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1);
+  const pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80);
+  const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81);
   if ((size_t)q0.a_bytes != ((size_t)(K - 1) * lda0 + M0) * 2 || (size_t)q1.b_bytes != ((size_t)(K - 1) * ldb1 + N1) * 2)
     return -20;  // 32-bit buffer offsets
   if (!wsgd::eligible(q0, false, false) || !wsgd::eligible(q1, false, false) || !wsgd::pair_compatible(q0, q1))

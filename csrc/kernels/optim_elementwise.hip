@@ -9,6 +9,7 @@
 // p, momentum and the bf16 shadow are written once.  16-B vector accesses,
 // grid-stride, sized for 256 CUs.
 #include "ddpx_common.h"
+#include "ddpx_mx.h"
 
 namespace ddpx {
 
@@ -26,7 +27,8 @@ template <bool GBF16>
 __global__ void __launch_bounds__(256)
 sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __restrict__ g,
                 unsigned short* __restrict__ shadow, int64_t n, const float* __restrict__ lr_ptr,
-                float lr_host, float mom, float wd, float gscale, int nesterov, int first) {
+                float lr_host, float mom, float wd, float gscale, int nesterov, int first,
+                unsigned char* __restrict__ q8, unsigned char* __restrict__ s8) {
   const float lr = lr_ptr ? *lr_ptr : lr_host;
   const int64_t nv = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -63,6 +65,12 @@ sgd_flat_kernel(float* __restrict__ p, float* __restrict__ buf, const void* __re
     if (shadow) {
       u32x2 sh = {pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
       reinterpret_cast<u32x2*>(shadow)[i] = sh;
+    }
+    if (q8) {  // MX-FP8 copy: vectors 8k..8k+7 (8 neighbouring lanes, all active: n % 32 == 0) = block k
+      unsigned e8;
+      const unsigned q = mx::e4m3_group8(po, &e8);
+      reinterpret_cast<unsigned*>(q8)[i] = q;
+      if ((i & 7) == 0) s8[i >> 3] = (unsigned char)e8;
     }
   };
   // two vectors per thread per iteration, all six loads issued before either update: twice the
@@ -157,8 +165,9 @@ using namespace ddpx;
 
 DDPX_API int ddpx_sgd_flat(float* p, float* buf, const void* g, int g_bf16, void* shadow, int64_t n,
                            const float* lr_dev, float lr_host, float momentum, float weight_decay,
-                           float grad_scale, int nesterov, int first, hipStream_t s) {
+                           float grad_scale, int nesterov, int first, void* q8, void* s8, hipStream_t s) {
   if (n <= 0) return 0;
+  if (q8 && (n % 32 || !s8 || (reinterpret_cast<uintptr_t>(q8) & 3))) return -1;
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(buf)) & 15) return -1;
   if (reinterpret_cast<uintptr_t>(g) & (g_bf16 ? 7 : 15)) return -1;
   if (reinterpret_cast<uintptr_t>(shadow) & 7) return -1;
@@ -166,11 +175,11 @@ DDPX_API int ddpx_sgd_flat(float* p, float* buf, const void* g, int g_bf16, void
   if (g_bf16)
     hipLaunchKernelGGL(sgd_flat_kernel<true>, dim3(grid), dim3(256), 0, s, p, buf, g,
                        (unsigned short*)shadow, n, lr_dev, lr_host, momentum, weight_decay, grad_scale,
-                       nesterov, first);
+                       nesterov, first, (unsigned char*)q8, (unsigned char*)s8);
   else
     hipLaunchKernelGGL(sgd_flat_kernel<false>, dim3(grid), dim3(256), 0, s, p, buf, g,
                        (unsigned short*)shadow, n, lr_dev, lr_host, momentum, weight_decay, grad_scale,
-                       nesterov, first);
+                       nesterov, first, (unsigned char*)q8, (unsigned char*)s8);
   return (int)hipGetLastError();
 }
 

@@ -105,8 +105,11 @@ class MLP(nn.Module):
             from ..runtime import native
             native.kernels()  # fail loudly if the extension is missing on a GPU
             # weights are read by the kernels only through the bf16 shadow; biases in fp32
+            # fp8: 128-element offsets, so every weight's MX copy (codes at the element offset, E8M0 scales at
+            # offset / 32) is 16-B / 4-B aligned for the MX GEMM's operand loads
             return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters()),
-                    "shadow_only_params": [m.weight for m in self.modules() if isinstance(m, nn.Linear)]}
+                    "shadow_only_params": [m.weight for m in self.modules() if isinstance(m, nn.Linear)],
+                    "align": 128 if getattr(self, "fp8", False) else 64}
         return {}
 
     def input_layout(self, device) -> str:

@@ -64,8 +64,10 @@ def conv_dgrad(dy, wd, N, H, W, C, Co, tile=-1):
     return dx
 
 
-def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None, tile=-1):
-    """Weight gradient in torch layout [Co,Cr,3,3] (written to ``out`` or applied through ``sgd``)."""
+def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None, tile=-1, prepared=None):
+    """Weight gradient in torch layout [Co,Cr,3,3] (written to ``out`` or applied through ``sgd``).
+    ``prepared`` = (wf, wd) with ``sgd``: the update also rewrites the bf16 GEMM layouts ``weight_prep`` makes
+    (whose zero channel padding it keeps), so the next forward needs no weight_prep pass."""
     N, H, W, C = x.shape
     _nhwc(x, "x")
     _nhwc(dy, "dy", Co)
@@ -78,9 +80,15 @@ def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None, tile=-1):
                  "ddpx_conv_wgrad")
     if sgd is None:
         _req(out is not None and out.numel() == Co * Cr * 9 and out.is_contiguous(), "conv_wgrad: bad out")
+        _req(prepared is None, "conv_wgrad: prepared layouts are written by the fused SGD only")
+    wf, wd = prepared if prepared is not None else (None, None)
+    if prepared is not None:
+        _req(wf.numel() == Co * 9 * C and wd.numel() == Co * 9 * C and wf.dtype == wd.dtype == torch.bfloat16,
+             "conv_wgrad: bad prepared-weight buffers")
     native.check(lib.ddpx_conv_wgrad_reduce(part.data_ptr(), S, Co, Cr, C, native.ptr(out),
                                             int(out is not None and out.dtype == torch.bfloat16), int(accumulate),
-                                            *native.sgd_args(sgd), s), "ddpx_conv_wgrad_reduce")
+                                            *native.sgd_args(sgd), native.ptr(wf), native.ptr(wd), s),
+                 "ddpx_conv_wgrad_reduce")
 
 
 def bn_finalize(stats, T, BM, M, bn_mod, training, a, b, mean, rstd):

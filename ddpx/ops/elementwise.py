@@ -52,10 +52,12 @@ def colsum_bf16(x: torch.Tensor, out: torch.Tensor, scale: float = 1.0, accumula
 
 def sgd_flat_(param: torch.Tensor, momentum_buf: torch.Tensor, grad: torch.Tensor, shadow: torch.Tensor | None,
               lr: float | torch.Tensor, momentum: float, weight_decay: float, grad_scale: float = 1.0,
-              nesterov: bool = False, first: bool = False):
+              nesterov: bool = False, first: bool = False, mx8=None):
     """One fused SGD step over flat contiguous buffers (torch.optim.SGD semantics, dampening=0).
 
     ``lr`` may be a Python float or a 0-d fp32 device tensor (graph-capturable path).
+    ``mx8`` = (codes uint8 [n], E8M0 scales uint8 [n / 32]), n % 32 == 0: also write the updated parameters as
+    MX-FP8 e4m3 blocks of 32 consecutive elements (the fp8 forward's weight operand; GPU only).
     """
     n = param.numel()
     if momentum_buf.numel() != n or grad.numel() != n or (shadow is not None and shadow.numel() != n):
@@ -81,6 +83,7 @@ def sgd_flat_(param: torch.Tensor, momentum_buf: torch.Tensor, grad: torch.Tenso
     rc = lib.ddpx_sgd_flat(param.data_ptr(), momentum_buf.data_ptr(), grad.data_ptr(),
                            int(grad.dtype == torch.bfloat16), native.ptr(shadow), n, lr_dev, lr_host,
                            float(momentum), float(weight_decay), float(grad_scale), int(nesterov), int(first),
+                           native.ptr(mx8[0] if mx8 else None), native.ptr(mx8[1] if mx8 else None),
                            native.stream_handle())
     native.check(rc, "ddpx_sgd_flat")
     return param

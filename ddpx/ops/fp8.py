@@ -39,17 +39,23 @@ class MX:
         return v * torch.exp2(e).repeat_interleave(32, dim=1)
 
 
-def quant(x: torch.Tensor, fmt: int = E4M3, rows: bool = True, cols: bool = False):
+def quant(x: torch.Tensor, fmt: int = E4M3, rows: bool = True, cols: bool = False, out=None):
     """MX-quantise bf16 ``x`` [R, C]: row blocks (for x as a K-contig operand, K = C) and/or the
-    transposed operand xᵀ [C, R] with blocks along R.  Returns MX, or (MX, MX_T) if both."""
+    transposed operand xᵀ [C, R] with blocks along R.  Returns MX, or (MX, MX_T) if both.
+    ``out`` = (codes uint8 [R, C], scales uint8 [R, C / 32]) contiguous: write the row quantisation there."""
     _req(x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1, "x must be 2-D bf16 (GPU)")
     R, C = x.shape
     _req(x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0, "x must be 16-B aligned with ld % 8 == 0")
     q = s = qt = st = None
     if rows:
         _req(C % 32 == 0, "row quantisation needs C % 32 == 0")
-        q = torch.empty((R, C), dtype=torch.uint8, device=x.device)
-        s = torch.empty((R, C // 32), dtype=torch.uint8, device=x.device)
+        if out is not None:
+            q, s = out
+            _req(q.dtype == torch.uint8 and q.shape == (R, C) and q.is_contiguous() and s.dtype == torch.uint8
+                 and s.shape == (R, C // 32) and s.is_contiguous(), "quant out: uint8 [R, C] + [R, C/32]")
+        else:
+            q = torch.empty((R, C), dtype=torch.uint8, device=x.device)
+            s = torch.empty((R, C // 32), dtype=torch.uint8, device=x.device)
     if cols:
         _req(R % 32 == 0 and R % 16 == 0, "transposed quantisation needs R % 32 == 0")
         qt = torch.empty((C, R), dtype=torch.uint8, device=x.device)

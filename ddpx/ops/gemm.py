@@ -248,14 +248,16 @@ def matmul(a, b, a_kcontig=True, b_kcontig=True, out_dtype=torch.float32, tile=-
 
 
 native.register_kernel_sig("ddpx_wgrad_sgd_pair", native.c_int, *([native.c_void_p, native.c_void_p] + [native.c_int] * 5
-                                                                  + [native.c_void_p] * 3) * 2,
+                                                                  + [native.c_void_p] * 5) * 2,
                            native.c_int, native.c_void_p, native.c_float, native.c_float, native.c_void_p)
 
 
-def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1) -> bool:
+def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
     """Both fused weight-gradient + SGD updates (dW_i = dy_iᵀ x_i applied to sgd_i's parameter) in ONE
     warp-specialised launch.  False (nothing launched) when the pair is not eligible; the caller then
-    issues them one by one with :func:`linear_wgrad`."""
+    issues them one by one with :func:`linear_wgrad`.  ``mx_i`` = (codes uint8 [M_i, N_i], E8M0 scales uint8
+    [M_i, N_i / 32]): the stream waves also write the updated W_i as MX-FP8 e4m3 (the next forward's
+    operand, ``ddpx.ops.fp8``), bitwise what ``fp8.quant`` of the bf16 copy would give."""
     for t, n in ((dy0, "dy0"), (x0, "x0"), (dy1, "dy1"), (x1, "x1")):
         _check_bf16_2d(t, n)
     if dy0.shape[0] != dy1.shape[0] or x0.shape[0] != dy0.shape[0] or x1.shape[0] != dy1.shape[0]:
@@ -264,11 +266,16 @@ def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1) -> bool:
         return False  # lr tensor, momentum, weight decay must be shared
     K = dy0.shape[0]
     args = []
-    for dy, x, sg in ((dy0, x0, sgd0), (dy1, x1, sgd1)):
+    for dy, x, sg, mx in ((dy0, x0, sgd0, mx0), (dy1, x1, sgd1, mx1)):
         M, N = dy.shape[1], x.shape[1]
         _req(sg[0].numel() == M * N, "sgd target size mismatch")
+        if mx is not None:
+            _req(mx[0].dtype == torch.uint8 and mx[0].numel() == M * N and mx[0].is_contiguous()
+                 and mx[1].dtype == torch.uint8 and mx[1].numel() == M * N // 32 and N % 32 == 0,
+                 "fp8 copy must be uint8 [M, N] codes + [M, N/32] scales")
         args += [dy.data_ptr(), x.data_ptr(), M, N, dy.stride(0), x.stride(0), N, sg[0].data_ptr(),
-                 native.ptr(sg[1]), native.ptr(sg[2])]
+                 native.ptr(sg[1]), native.ptr(sg[2]), native.ptr(mx[0] if mx else None),
+                 native.ptr(mx[1] if mx else None)]
     lr = sg[3]
     rc = native.kernels().ddpx_wgrad_sgd_pair(*args, K, lr.data_ptr(), float(sgd0[4]), float(sgd0[5]),
                                               native.stream_handle())

@@ -85,7 +85,10 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
                 saved8.append(hqt)
             else:
                 hq = F8.quant(hs[-1], F8.E4M3)
-            wq = F8.quant(flat.shadow_of(w), F8.E4M3)
+            if flat.shadow8 is None:
+                flat.enable_fp8_shadow()
+            # the e4m3 weight copy the optimizer stream wrote last step (re-quantised only when stale)
+            wq = flat.mx8_weight(w)
             hs.append(F8.gemm(hq, wq, epi=G.EPI_BIAS_RELU_BF16, bias=b))
         else:
             hs.append(G.linear_fwd(hs[-1], flat.shadow_of(w), b, relu=True))
@@ -140,10 +143,16 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             elif l == 0 and deferred is not None:
                 d1, h1, s1, w1 = deferred
                 s0 = flat.fused_spec(w)
-                if not G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0):
+                # fp8 model: the stream waves also emit both weights' MX-FP8 copies for the next forward
+                mx1, mx0 = (flat.mx8_views(w1), flat.mx8_views(w)) if flat.shadow8 is not None else (None, None)
+                paired = G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0, mx1, mx0)
+                if not paired:
                     G.linear_wgrad(d1, h1, None, sgd=s1)
                     _wgrad(saved8, 0, dpre, hs[0], None, sgd=s0)
-                flat.mark_updated(w1)
+                flat.mark_updated(w1, fp8_written=paired and mx1 is not None)
+                flat.mark_updated(w, fp8_written=paired and mx0 is not None)
+                dpre = dnext
+                continue
             else:
                 _wgrad(saved8, l, dpre, hs[l], None, sgd=flat.fused_spec(w))
             flat.mark_updated(w)

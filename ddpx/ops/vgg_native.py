@@ -47,11 +47,15 @@ class _Plan:
             self.blocks.append((conv, bn, pool))
         dev = model.classifier.weight.device
         self.wf, self.wd = [], []
+        # FlatParams version of each conv weight the prepared layouts were made from (None: never): the fused
+        # single-process update rewrites them in its reduce kernel, any other update makes them stale
+        self.wver = [None] * 0
         for conv, _, _ in self.blocks:
             Co, Ci = conv.weight.shape[:2]
             n = Co * 9 * K.padded_channels(Ci)
             self.wf.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
             self.wd.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
+        self.wver = [None] * len(self.blocks)
 
 
 def _sync_comm(model, training):
@@ -78,7 +82,10 @@ def _forward(model, x, targets, want_logits, want_grad, training):
     saved = []
     for bi, (conv, bn, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
-        K.weight_prep(conv.weight, plan.wf[bi], plan.wd[bi])
+        ver = flat.version_of(conv.weight)
+        if plan.wver[bi] != ver:
+            K.weight_prep(conv.weight, plan.wf[bi], plan.wd[bi])
+            plan.wver[bi] = ver
         y, st, T, BM = K.conv_fwd(x, plan.wf[bi], Co, stats=training)
         dev = x.device
         a = torch.empty(Co, dtype=torch.float32, device=dev)
@@ -148,8 +155,16 @@ def _backward(model, saved, last, dl, grad_out):
         Cr = conv.weight.shape[1]
         sw = flat.fused_spec(conv.weight)
         if sw is not None:
-            K.conv_wgrad(dy, x, Co, Cr, sgd=sw)
+            # prepared layouts current before this update (the forward made or kept them): the reduce rewrites
+            # them with the updated weight, after this block's dgrad below has read wd (stream order)
+            prep = plan.wver[bi] == flat.version_of(conv.weight)
+            if prep and bi > 0:
+                g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            K.conv_wgrad(dy, x, Co, Cr, sgd=sw, prepared=(plan.wf[bi], plan.wd[bi]) if prep else None)
             flat.mark_updated(conv.weight)
+            if prep:
+                plan.wver[bi] = flat.version_of(conv.weight)
+                continue
         else:
             dw, accw = flat.grad_target(conv.weight)
             K.conv_wgrad(dy, x, Co, Cr, out=dw, accumulate=accw)

@@ -162,12 +162,15 @@ class SGD(Optimizer):
         self._flush_lr()
         return self._lr_dev if self._lr_dev is not None else float(self.param_groups[0]["lr"])
 
-    def _update(self, start, end, g):
+    def _update(self, start, end, g, fp8=True):
         f = self.flat
         buf = self.momentum_buffer[start:end] if self.momentum_buffer is not None else f.master[start:end]
         sh = f.shadow[start:end] if f.shadow is not None else None
+        # a store that keeps an MX-FP8 weight copy gets it written in the same pass (fp8 forward GEMMs)
+        mx8 = f.mx8_range(start, end) if (fp8 and f.master.is_cuda) else None
         sgd_flat_(f.master[start:end], buf, f.grad[start:end], sh, self._lr_arg(), g["momentum"],
-                  g["weight_decay"], nesterov=g["nesterov"])
+                  g["weight_decay"], nesterov=g["nesterov"], mx8=mx8)
+        f.fp8_mark(start, end, mx8 is not None)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -187,7 +190,7 @@ class SGD(Optimizer):
                 for b in src.bucket_order():
                     src.wait_bucket(b)
                     for (start, end) in src.update_ranges(b):
-                        self._update(start, end, g)
+                        self._update(start, end, g, fp8=False)
                     src.gather_bucket(b)
             else:
                 # shard updates on the communicator stream, in stream order behind each bucket's
@@ -201,12 +204,14 @@ class SGD(Optimizer):
                     for b in src.bucket_order():
                         src.claim_bucket_on_comm_stream(b)
                         for (start, end) in src.update_ranges(b):
-                            self._update(start, end, g)
+                            self._update(start, end, g, fp8=False)
                         src.gather_bucket(b)
                 done = torch.cuda.Event()
                 done.record(side)
                 cur.wait_event(done)
             src.optimizer_done()
+            # the all-gathers refreshed master / bf16 copies of every shard, not the fp8 copy
+            self.flat.fp8_mark(0, self.flat.total, False)
         elif any(self.flat.updated):
             # fused-backward parameters are already stepped; update the rest range by range
             f = self.flat

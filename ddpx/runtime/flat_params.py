@@ -51,6 +51,7 @@ class FlatParams:
             if p.dtype != torch.float32:
                 raise ValueError("FlatParams expects fp32 master parameters")
         self.device = device
+        self.align = max(ALIGN, int(align))  # element alignment of every parameter offset (and of relayout groups)
         self.params = list(reversed(params))  # gradient-ready order
         self.names = {}
         for name, p in module.named_parameters():
@@ -63,6 +64,9 @@ class FlatParams:
             self.numels.append(p.numel())
             off = _round_up(off + p.numel(), align)
         self.total = off
+        # per-parameter update counter: consumers that keep a derived copy of a weight (the VGG path's permuted
+        # bf16 conv layouts) re-derive it when the counter moved since they last did
+        self.version = [0] * len(self.params)
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=grad_dtype, device=device)
         self.shadow = torch.zeros(self.total, dtype=shadow_dtype, device=device) if shadow_dtype else None
@@ -96,6 +100,12 @@ class FlatParams:
         self.chunk_rows = {}
         self._chunks_done = {}
         self._warned_unused = False
+        # optional MX-FP8 (e4m3) copy of every parameter (enable_fp8_shadow): codes [total] + E8M0 scales of
+        # each 32-element run [total / 32] (offsets are 64-aligned, so every parameter starts a block);
+        # fp8_fresh[i]: the copy of parameter i matches its master (an optimizer stream wrote it)
+        self.shadow8 = None
+        self.scale8 = None
+        self.fp8_fresh = [False] * len(self.params)
         self._hooks = []
         for p in self.params:
             if id(p) not in self.native:
@@ -115,7 +125,58 @@ class FlatParams:
     def shadow_of(self, p):
         return getattr(p, "_ddpx_shadow", None)
 
+    def enable_fp8_shadow(self):
+        """Keep an MX-FP8 copy of the parameters for fp8 forward GEMMs: the optimizer kernels that can write it
+        next to the bf16 copy do (flat SGD, fused weight-gradient + SGD pair), anything else marks it stale and
+        the next reader re-quantises (``mx8_weight``)."""
+        if self.shadow8 is None:
+            self.shadow8 = torch.zeros(self.total, dtype=torch.uint8, device=self.device)
+            self.scale8 = torch.zeros(self.total // 32, dtype=torch.uint8, device=self.device)
+        self.fp8_fresh = [False] * len(self.params)
+
+    def mx8_views(self, p):
+        """(codes [rows, cols], scales [rows, cols / 32]) views of p's fp8 copy, or None without one."""
+        if self.shadow8 is None or p.dim() != 2 or p.shape[1] % 32:
+            return None
+        i = self.index[id(p)]
+        o, n = self.offsets[i], self.numels[i]
+        if o % 128:
+            return None  # the MX GEMM needs 16-B code / 4-B scale alignment (a 128-aligned store: align=128)
+        return (self.shadow8[o:o + n].view(p.shape),
+                self.scale8[o // 32:(o + n) // 32].view(p.shape[0], p.shape[1] // 32))
+
+    def mx8_weight(self, p):
+        """p's MX-FP8 operand (ddpx.ops.fp8.MX): the optimizer-written copy when current, else the bf16 copy
+        quantised now (into the store when it keeps one, so later readers of this step reuse it)."""
+        from ..ops import fp8 as F8
+        v = self.mx8_views(p)
+        if v is None:
+            return F8.quant(self.shadow_of(p), F8.E4M3)
+        i = self.index[id(p)]
+        if not self.fp8_fresh[i]:
+            F8.quant(self.shadow_of(p), F8.E4M3, out=v)
+            self.fp8_fresh[i] = True
+        return F8.MX(v[0], v[1], F8.E4M3)
+
+    def fp8_mark(self, start, end, written):
+        """Parameters overlapping the flat range [start, end) were updated; ``written``: the update also wrote
+        the fp8 copy of the range (only parameters entirely inside it count as current)."""
+        for i, (o, n) in enumerate(zip(self.offsets, self.numels)):
+            if o < end and o + n > start:
+                self.version[i] += 1
+                if self.shadow8 is not None:
+                    self.fp8_fresh[i] = bool(written and o >= start and o + n <= end)
+
+    def mx8_range(self, start, end):
+        """(codes, scales) slices of the fp8 copy for a flat update of [start, end), or None."""
+        if self.shadow8 is None or start % 32 or (end - start) % 32:
+            return None
+        return self.shadow8[start:end], self.scale8[start // 32:end // 32]
+
     def refresh_shadow(self):
+        self.fp8_fresh = [False] * len(self.params)
+        # every parameter moves past any version a consumer may hold (also across a relayout's re-indexing)
+        self.version = [max(self.version, default=0) + 1] * len(self.params)
         if self.shadow is None:
             return
         from ..ops.elementwise import cast_bf16_
@@ -138,14 +199,15 @@ class FlatParams:
         old_params = list(self.params)
         offsets, spans, off, k = [], [], 0, 0
         for g in groups:
-            start = off
+            start = off = _round_up(off, self.align)
             for _ in g:
                 p = new_params[k]
                 offsets.append(off)
-                off = _round_up(off + p.numel(), ALIGN)
+                off = _round_up(off + p.numel(), self.align)
                 k += 1
             off = start + _round_up(max(off - start, pad_to), pad_to)
             spans.append((start, off))
+        off = _round_up(off, self.align)
         total = off
         dev = self.device
         master = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -170,6 +232,9 @@ class FlatParams:
         self.numels = [p.numel() for p in self.params]
         self.total = total
         self.master, self.grad, self.shadow = master, grad, shadow
+        if self.shadow8 is not None:
+            self.shadow8 = torch.zeros(total, dtype=torch.uint8, device=dev)
+            self.scale8 = torch.zeros(total // 32, dtype=torch.uint8, device=dev)
         self.state_tensors = states
         self.refresh_shadow()
         self.written = [False] * len(self.params)
@@ -223,10 +288,15 @@ class FlatParams:
         o._flush_lr()  # an LR advance no head forward took must land before this epilogue reads lr
         return (self.master[sl], buf, sh, o.lr_dev, g["momentum"], g["weight_decay"])
 
-    def mark_updated(self, p):
+    def version_of(self, p) -> int:
+        return self.version[self.index[id(p)]]
+
+    def mark_updated(self, p, fp8_written: bool = False):
         i = self.index[id(p)]
         self.updated[i] = True
         self.written[i] = True
+        self.version[i] += 1
+        self.fp8_fresh[i] = bool(fp8_written and self.shadow8 is not None)
 
     def grad_done(self, p, chunk=None):
         i = self.index[id(p)]

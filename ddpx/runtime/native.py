@@ -45,7 +45,7 @@ def _sig(lib, name, restype, *argtypes):
 
 def _declare_kernels(lib):
     P, I, I64, F = c_void_p, c_int, c_int64, c_float
-    _sig(lib, "ddpx_sgd_flat", I, P, P, P, I, P, I64, P, F, F, F, F, I, I, P)
+    _sig(lib, "ddpx_sgd_flat", I, P, P, P, I, P, I64, P, F, F, F, F, I, I, P, P, P)
     _sig(lib, "ddpx_cast_f32_bf16", I, P, P, I64, P)
     _sig(lib, "ddpx_colsum_bf16", I, P, P, I, I, I, F, I, P)
     _sig(lib, "ddpx_scale_f32", I, P, I64, F, P)
@@ -74,7 +74,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I, I)
     _sig(lib, "ddpx_conv_wgrad", I, P, P, P, I, I, I, I, I, I, I, P)
-    _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P, P, P)
     _sig(lib, "ddpx_bn_finalize", I, P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P)
     _sig(lib, "ddpx_bn_apply", I, P, P, P, I, I, I, I, I, I, P, P)
     _sig(lib, "ddpx_bn_local_stats", I, P, I, I, I, I, P, P)

@@ -16,6 +16,6 @@ def prepare_model(model: nn.Module, device, grad_dtype=torch.float32) -> FlatPar
         return f
     spec = model.ddpx_spec(device) if hasattr(model, "ddpx_spec") else {}
     f = FlatParams(model, grad_dtype=grad_dtype, shadow_dtype=spec.get("shadow_dtype"),
-                   native_params=spec.get("native_params", ()))
+                   native_params=spec.get("native_params", ()), align=spec.get("align", 64))
     f.shadow_only = {id(p) for p in spec.get("shadow_only_params", ())}
     return f

@@ -121,3 +121,99 @@ def test_mlp_fp8_step_tracks_bf16(gpu, wgrad8, monkeypatch):
         assert cos > 0.97 and _rel(p.main_grad, q.main_grad) < 0.3, (n, cos)
     with torch.no_grad():
         assert _rel(a(x), b(x)) < 0.06
+
+
+def test_sgd_flat_emits_mx8_copy(gpu):
+    """The flat SGD's MX-FP8 output (codes + E8M0 scales of every 32-element run) == the separate quantiser
+    applied to the bf16 copy it wrote, byte for byte."""
+    from ddpx.ops import fp8 as F8
+    from ddpx.ops.elementwise import sgd_flat_
+    torch.manual_seed(12)
+    n = 32 * 4099  # not a multiple of the grid stride: partial last iteration
+    p = torch.randn(n, device=gpu) * 0.05
+    p[:32] = 0.0  # an all-zero block (scale byte 0)
+    buf = torch.randn(n, device=gpu) * 0.01
+    g = torch.randn(n, device=gpu) * 0.1
+    sh = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    q = torch.empty(n, dtype=torch.uint8, device=gpu)
+    s = torch.empty(n // 32, dtype=torch.uint8, device=gpu)
+    lr = torch.full((), 0.05, device=gpu)
+    sgd_flat_(p, buf, g, sh, lr, 0.9, 5e-4, mx8=(q, s))
+    ref = F8.quant(sh.view(-1, 32), F8.E4M3)
+    torch.cuda.synchronize()
+    assert torch.equal(q.view(-1, 32), ref.q)
+    assert torch.equal(s.view(-1, 1), ref.s)
+
+
+@pytest.mark.parametrize("mom", [0.9, 0.0])
+def test_wgrad_sgd_pair_emits_mx8_copy(gpu, mom):
+    """The warp-specialised weight-gradient + SGD pair's stream waves write both weights' MX-FP8 copies:
+    equal to the quantiser run on the bf16 copies, and master / momentum / bf16 unchanged by the extra output."""
+    from ddpx.ops import fp8 as F8
+    from ddpx.ops import gemm as G
+    torch.manual_seed(13)
+    K = 512
+    shapes = [(256, 512), (128, 384)]
+    dys = [((torch.rand(K, m, device=gpu) * 2 - 1) * 0.1).to(torch.bfloat16) for m, _ in shapes]
+    xs = [((torch.rand(K, n, device=gpu) * 2 - 1)).to(torch.bfloat16) for _, n in shapes]
+    lr = torch.full((), 0.05, device=gpu)
+    init = [(torch.randn(m * n, device=gpu) * 0.02, torch.randn(m * n, device=gpu) * 0.01) for m, n in shapes]
+
+    def state():
+        return [(p.clone(), b.clone(), torch.empty(p.numel(), dtype=torch.bfloat16, device=gpu)) for p, b in init]
+
+    sa, sb = state(), state()
+    mxs = [(torch.empty(m, n, dtype=torch.uint8, device=gpu), torch.empty(m, n // 32, dtype=torch.uint8, device=gpu))
+           for m, n in shapes]
+    spec = lambda st: [(p, b if mom else None, s, lr, mom, 5e-4) for p, b, s in st]  # noqa: E731
+    a, b = spec(sa), spec(sb)
+    assert G.wgrad_sgd_pair(dys[0], xs[0], a[0], dys[1], xs[1], a[1], mxs[0], mxs[1])
+    assert G.wgrad_sgd_pair(dys[0], xs[0], b[0], dys[1], xs[1], b[1])
+    torch.cuda.synchronize()
+    for (m, n), (pa, ba, sha), (pb, bb, shb), (q, s) in zip(shapes, sa, sb, mxs):
+        assert torch.equal(pa, pb) and torch.equal(sha, shb)
+        if mom:
+            assert torch.equal(ba, bb)
+        ref = F8.quant(sha.view(m, n), F8.E4M3)
+        assert torch.equal(q, ref.q)
+        assert torch.equal(s, ref.s)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused):
+    """fp8 MLP training: after each step the hidden weights' fp8 copy is current (written by the fused pair
+    or the flat SGD, not re-quantised by the forward) and equals the quantiser's output for the bf16 copy."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.ops import fp8 as F8
+    from ddpx.optim.sgd import SGD
+    torch.manual_seed(5)
+    m = MLP(hidden=512)
+    m.fp8 = True
+    ddpx.prepare_model(m, gpu)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True, fused_backward=fused)
+    x = torch.rand(512, 3072, device=gpu).to(torch.bfloat16)
+    t = torch.randint(0, 10, (512,), device=gpu)
+    flat = m.fc0.weight._ddpx_flat
+    calls = []
+    orig = F8.quant
+    for step in range(3):
+        opt.zero_grad()
+        F8.quant = lambda *a, **k: (calls.append(k.get("out") is not None), orig(*a, **k))[1]
+        try:
+            loss, _ = m.forward_loss(x, t)
+        finally:
+            F8.quant = orig
+        loss.backward()
+        opt.step()
+        # step 0 quantises the initial weights into the store; later forwards reuse the optimizer's copy
+        assert sum(calls) == (2 if step == 0 else 0), (step, calls)
+        calls.clear()
+        for lin in m.linears()[:-1]:
+            w = lin.weight
+            assert flat.fp8_fresh[flat.index[id(w)]]
+            q, s = flat.mx8_views(w)
+            ref = F8.quant(flat.shadow_of(w), F8.E4M3)
+            torch.cuda.synchronize()
+            assert torch.equal(q, ref.q) and torch.equal(s, ref.s), (step, lin)
+    assert torch.isfinite(loss).item()
