@@ -561,10 +561,24 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     sync()
+    trace = os.environ.get("DDPX_STEP_TRACE") == "1" and not cpu
+    evs = []
     t0 = time.perf_counter()
-    loss = run(args.warmup, args.steps)
+    if trace:
+        # diagnostics only: one event per step (no host sync inside the window) -> per-step GPU time on stderr
+        evs.append(torch.cuda.Event(enable_timing=True))
+        evs[-1].record()
+        for i in range(args.steps):
+            loss = run(args.warmup + i, 1)
+            evs.append(torch.cuda.Event(enable_timing=True))
+            evs[-1].record()
+    else:
+        loss = run(args.warmup, args.steps)
     sync()
     t1 = time.perf_counter()
+    if trace:
+        print(json.dumps({"step_ms": [round(a.elapsed_time(b), 4) for a, b in zip(evs, evs[1:])],
+                          "host_ms": round((t1 - t0) * 1000, 3)}), file=sys.stderr)
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0

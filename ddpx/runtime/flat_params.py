@@ -27,6 +27,7 @@ first writer of an iteration overwrites instead of accumulating
 """
 from __future__ import annotations
 
+import os
 import warnings
 
 import torch
@@ -106,6 +107,10 @@ class FlatParams:
         self.shadow8 = None
         self.scale8 = None
         self.fp8_fresh = [False] * len(self.params)
+        # the optimizer kernels write the fp8 copy next to the bf16 one (DDPX_FP8_COPY=1); default off: on the
+        # wide MLP the extra stream output costs the fused wgrad+SGD pair ~200 us, more than the separate
+        # quantisation of both weights (~174 us) it replaces (profiles/r3_fp8)
+        self.fp8_from_optimizer = os.environ.get("DDPX_FP8_COPY", "0") == "1"
         self._hooks = []
         for p in self.params:
             if id(p) not in self.native:
@@ -169,7 +174,7 @@ class FlatParams:
 
     def mx8_range(self, start, end):
         """(codes, scales) slices of the fp8 copy for a flat update of [start, end), or None."""
-        if self.shadow8 is None or start % 32 or (end - start) % 32:
+        if self.shadow8 is None or not self.fp8_from_optimizer or start % 32 or (end - start) % 32:
             return None
         return self.shadow8[start:end], self.scale8[start // 32:end // 32]
 

@@ -180,9 +180,11 @@ def test_wgrad_sgd_pair_emits_mx8_copy(gpu, mom):
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused):
-    """fp8 MLP training: after each step the hidden weights' fp8 copy is current (written by the fused pair
-    or the flat SGD, not re-quantised by the forward) and equals the quantiser's output for the bf16 copy."""
+@pytest.mark.parametrize("from_opt", [True, False])
+def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused, from_opt):
+    """fp8 MLP training: the hidden weights' fp8 copy used by each forward equals the quantiser's output for
+    the bf16 copy.  With the optimizer writing it (DDPX_FP8_COPY=1: the fused pair or the flat SGD) the forward
+    never re-quantises after the first step; by default it re-quantises both weights every step."""
     import ddpx
     from ddpx.models import MLP
     from ddpx.ops import fp8 as F8
@@ -195,6 +197,7 @@ def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused):
     x = torch.rand(512, 3072, device=gpu).to(torch.bfloat16)
     t = torch.randint(0, 10, (512,), device=gpu)
     flat = m.fc0.weight._ddpx_flat
+    flat.fp8_from_optimizer = from_opt
     calls = []
     orig = F8.quant
     for step in range(3):
@@ -207,13 +210,14 @@ def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused):
         loss.backward()
         opt.step()
         # step 0 quantises the initial weights into the store; later forwards reuse the optimizer's copy
-        assert sum(calls) == (2 if step == 0 else 0), (step, calls)
+        assert sum(calls) == (2 if (step == 0 or not from_opt) else 0), (step, calls)
         calls.clear()
         for lin in m.linears()[:-1]:
             w = lin.weight
-            assert flat.fp8_fresh[flat.index[id(w)]]
-            q, s = flat.mx8_views(w)
-            ref = F8.quant(flat.shadow_of(w), F8.E4M3)
-            torch.cuda.synchronize()
-            assert torch.equal(q, ref.q) and torch.equal(s, ref.s), (step, lin)
+            assert flat.fp8_fresh[flat.index[id(w)]] == from_opt
+            if from_opt:
+                q, s = flat.mx8_views(w)
+                ref = F8.quant(flat.shadow_of(w), F8.E4M3)
+                torch.cuda.synchronize()
+                assert torch.equal(q, ref.q) and torch.equal(s, ref.s), (step, lin)
     assert torch.isfinite(loss).item()
