@@ -68,6 +68,12 @@ def parse(argv=None):
     p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
                    help="ddpx engine ops: auto = hand-written kernels except VGG at fp32 (MIOpen convolutions)")
     p.add_argument("--no_graph", action="store_true")
+    p.add_argument("--prefetch_batch", type=int, default=0,
+                   help="1 (N = 1, graphs): step k's kernels read a batch augmented during step k-1 on a side stream "
+                        "(double-buffered input), so the augment kernel overlaps the previous step instead of "
+                        "opening each step; same batches, same seeds, one augment per step.  Default 0: the "
+                        "side-stream fork/join inside the graph costs more than the 8 us augment "
+                        "(0.2753-0.2782 vs 0.2521-0.2531 ms/step, profiles/r3_val/NOTES.md)")
     p.add_argument("--graph_steps", type=int, default=1,
                    help="training steps per captured HIP graph (the launch gap between replays is paid once "
                         "per graph); the timed region still runs exactly --steps steps")
@@ -107,6 +113,9 @@ def parse(argv=None):
                    help="1: also time the stock PyTorch recipe (torch.nn + torch DDP over RCCL at N > 1) in this "
                         "job, after the ddpx timing, on the same data (default 1)")
     p.add_argument("--stock_steps", type=int, default=30)
+    p.add_argument("--digest", type=int, default=0,
+                   help="1: report a SHA-256 of this rank's fp32 master weights + optimizer state after the timed "
+                        "steps (``master_digest``; tests compare schedules for bitwise-identical training)")
     p.add_argument("--stock_first", type=int, default=None,
                    help="1: time the stock recipe BEFORE the ddpx warm-up instead of after the ddpx timing "
                         "(default 0)")
@@ -413,10 +422,10 @@ def measure_stock_same_run(args, device, world, rank, idx_all, full):
             "recipe": recipe, "steps": args.stock_steps}
 
 
-def replica_digest(net):
+def replica_digest(net, flat=None):
     """SHA-256 of this rank's fp32 master weights and optimizer state, byte for byte (after consolidate)."""
     import hashlib
-    f = net.flat
+    f = flat if flat is not None else net.flat
     h = hashlib.sha256()
     for t in [f.master] + [f.state_tensors[k] for k in sorted(f.state_tensors)]:
         h.update(t.detach().cpu().contiguous().numpy().tobytes())
@@ -487,6 +496,44 @@ def main(argv=None):
 
         use_graph = not args.no_graph
         S = max(1, args.graph_steps) if use_graph else 1
+        prefetch = bool(args.prefetch_batch and use_graph and world == 1 and S == 1)
+        args.prefetch_batch = int(prefetch)
+        if prefetch:
+            # double-buffered batches: step k reads bufs[k % 2], filled during step k-1 by the augment kernel on a
+            # side stream (forked at the step's start, joined at its end), which draws batch k + 1 into the other
+            # buffer from its own device cursor (batch index = augments issued so far)
+            bufs = [(static_x, static_y), (torch.empty_like(static_x), torch.empty_like(static_y))]
+            side = torch.cuda.Stream(device)
+            data_ctr = counter.clone()
+            loader.cursor_batch(idx_dev, nfull, *bufs[0], counter=data_ctr)  # batch of the first step
+            data_ctr.add_(1)
+            pstate = {"k": 0}
+
+            def pf_body(par):
+                x, y = bufs[par]
+                nx, ny = bufs[1 - par]
+                cur = torch.cuda.current_stream()
+                fork = torch.cuda.Event()
+                fork.record(cur)
+                side.wait_event(fork)
+                with torch.cuda.stream(side):
+                    loader.cursor_batch(idx_dev, nfull, nx, ny, counter=data_ctr)
+                    data_ctr.add_(1)
+                ready = torch.cuda.Event()
+                ready.record(side)
+                opt.device_lr_step()
+                opt.zero_grad()
+                loss, _ = net.forward_loss(x, y) if hasattr(model, "forward_loss") else (
+                    torch.nn.functional.cross_entropy(net(x), y), None)
+                loss.backward(one)
+                opt.step()
+                cur.wait_event(ready)
+                return loss
+
+            def pf_eager():
+                loss = pf_body(pstate["k"] % 2)
+                pstate["k"] += 1
+                return loss
 
         def multi_body(x, y):
             loss = None
@@ -501,6 +548,15 @@ def main(argv=None):
             # host-side step state a failed capture could leave half-done (restored by the fallback)
             snap["ddp"] = net.iteration_state() if hasattr(net, "iteration_state") else None
             snap["step_count"] = opt.step_count
+            if prefetch:
+                gp = [CapturedStep(lambda x, y, par=par: pf_body(par), static_x, static_y, use_inputs_as_static=True,
+                                   comm=comm_obj) for par in (0, 1)]
+
+                def replay_pf():
+                    loss = gp[pstate["k"] % 2]()
+                    pstate["k"] += 1
+                    return loss
+                return {1: replay_pf}
             g = {1: CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)}
             if S > 1:
                 g[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)
@@ -522,7 +578,8 @@ def main(argv=None):
             dist.all_reduce(t, op=dist.ReduceOp.MIN)  # gloo group: CPU tensors
             return bool(t.item())
 
-        runner = GraphedSteps(lambda: step_body(static_x, static_y), make_graphs, steps_per_graph=S,
+        runner = GraphedSteps(pf_eager if prefetch else (lambda: step_body(static_x, static_y)), make_graphs,
+                              steps_per_graph=S,
                               use_graph=use_graph, agree=agree, on_fallback=fallback,
                               after=lambda m: [sched.step() for _ in range(m)])
 
@@ -601,6 +658,10 @@ def main(argv=None):
         consistent = all(c == allck[0] for c in allck)
         esz = net.flat.grad.element_size()
         buckets_mb = [round((e - s) * esz / 2 ** 20, 3) for s, e in net.bucket_ranges]
+    digest = None
+    if args.digest and args.impl == "ddpx":
+        from ddpx.runtime.flat_params import flat_of
+        digest = allck[rank] if ddpx_ddp else replica_digest(None, flat=flat_of(model))
     if args.stock_ref and not args.stock_first:
         stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
     value = world * bs * args.steps / elapsed
@@ -635,6 +696,7 @@ def main(argv=None):
                    "comm": (args.comm if ddpx_ddp else None),
                    "graph": bool(runner is not None and runner.use_graph),
                    "graph_steps": (args.graph_steps if (runner is not None and runner.use_graph) else None),
+                   "prefetch_batch": bool(getattr(args, "prefetch_batch", 0)),
                    "graph_error": (runner.graph_error if runner is not None else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
                        " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer
@@ -652,6 +714,7 @@ def main(argv=None):
                    "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
                    "final_loss": round(final_loss, 4), "ddp": bool(multi),
                    "replicas_consistent": consistent,
+                   "master_digest": digest,
                    "comm_ms_per_step": round(comm["comm_ms"], 4) if comm else None,
                    "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None,
                    "stock_same_run": stock,

@@ -20,6 +20,8 @@
 //     sum(g*xhat) per channel (per-block partials, fixed-order merge); pass 2
 //     writes dy = a*(g - mean(g) - xhat*mean(g*xhat)) in bf16 for the conv
 //     dgrad/wgrad GEMMs.
+#include <cstdlib>
+
 #include "ddpx_common.h"
 
 namespace ddpx {
@@ -111,6 +113,225 @@ finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, co
   b_out[c] = beta[c] - mean * a;
   mean_out[c] = mean;
   rstd_out[c] = rstd;
+}
+
+// ---------------------------------------------------------------- two-level, channel-coalesced merges
+// The per-channel kernels above read one channel of a [T][2][C] partial array per wave: every lane touches a
+// different row, so a 64-channel line is fetched by up to 64 waves (VGG's 32x32 layers: T = 2048, 22 us for a
+// 1 MB merge).  Here a lane is a channel (a wave reads 256 contiguous bytes of one tile row), the tiles are split
+// over S workgroups per 64-channel group, and the LAST workgroup of a group to finish (agent-scope ticket)
+// merges the S partials in split order: deterministic, and the hand-off is MI355X_MICROARCH "Valid forms" row 1
+// (sc1 stores drained by vmcnt(0) before the ticket, sc1 loads after it).  Tickets reset by their last arriver.
+constexpr int kMergeMaxC = 1024, kFinMaxS = 32, kBwdMaxS = 32;
+// DDPX_BN_MERGE=legacy (or ddpx_bn_set_merge(1)): the per-channel merge kernels above (A/B measurements)
+static int g_merge_mode = -1;
+static inline bool merge_legacy() {
+  if (g_merge_mode < 0) {
+    const char* e = getenv("DDPX_BN_MERGE");
+    g_merge_mode = (e && e[0] == 'l') ? 1 : 0;
+  }
+  return g_merge_mode == 1;
+}
+__device__ int g_merge_tickets[2][kMergeMaxC / 64];
+__device__ float g_fin_scratch[kFinMaxS * 3 * kMergeMaxC];
+__device__ float g_bwd_scratch[kBwdMaxS * 2 * kMergeMaxC];
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* base, unsigned bytes, unsigned off_bytes) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 16));
+}
+// lane 0 of wave 0 takes the ticket after every wave's sc1 stores drained (vmcnt(0) + barrier)
+__device__ __forceinline__ bool take_last(int* ticket, int S, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  __syncthreads();
+  return *flag != 0;
+}
+
+static inline int fin_splits(int T) {
+  int S = (T + 63) / 64;  // <= 16 tiles per lane
+  return S < 1 ? 1 : (S > kFinMaxS ? kFinMaxS : S);
+}
+static inline int bwd_splits(int B) {
+  int S = (B + 31) / 32;
+  return S < 1 ? 1 : (S > kBwdMaxS ? kBwdMaxS : S);
+}
+
+// Training statistics: tiles t = 4 s + w (+ 4 S j) merged per lane, waves merged in order, then the split
+// partials in split order by the last workgroup, which also runs finalize_kernel's epilogue.
+__global__ void __launch_bounds__(256)
+finalize_split_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, int S,
+                      const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
+                      float* __restrict__ rvar, int64_t* __restrict__ nbt, float momentum, float eps,
+                      float* __restrict__ a_out, float* __restrict__ b_out, float* __restrict__ mean_out,
+                      float* __restrict__ rstd_out, float* __restrict__ merged_out) {
+  __shared__ float wres[4][3][64];
+  __shared__ int flag;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cg = blockIdx.x, sp = blockIdx.y;
+  const int c = cg * 64 + lane;
+  const bool cok = c < C;
+  const int cc = cok ? c : 0;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  const int step = 4 * S;
+  int t = 4 * sp + w;
+  for (; t + 3 * step < T; t += 4 * step) {
+    float tm[4], tq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      tm[u] = stats[((size_t)(t + u * step) * 2) * C + cc];
+      tq[u] = stats[((size_t)(t + u * step) * 2 + 1) * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) chan_merge(n, mu, m2, (float)min(BM, M - (t + u * step) * BM), tm[u], tq[u]);
+  }
+  for (; t < T; t += step)
+    chan_merge(n, mu, m2, (float)min(BM, M - t * BM), stats[((size_t)t * 2) * C + cc], stats[((size_t)t * 2 + 1) * C + cc]);
+  wres[w][0][lane] = n;
+  wres[w][1][lane] = mu;
+  wres[w][2][lane] = m2;
+  __syncthreads();
+  float* part = g_fin_scratch;
+  if (w == 0) {
+    for (int q = 1; q < 4; ++q) chan_merge(n, mu, m2, wres[q][0][lane], wres[q][1][lane], wres[q][2][lane]);
+    if (cok) {
+      st_sc1(part + ((size_t)sp * 3 + 0) * C + c, n);
+      st_sc1(part + ((size_t)sp * 3 + 1) * C + c, mu);
+      st_sc1(part + ((size_t)sp * 3 + 2) * C + c, m2);
+    }
+  }
+  if (!take_last(&g_merge_tickets[0][cg], S, &flag)) return;
+  if (threadIdx.x == 0) __hip_atomic_store(&g_merge_tickets[0][cg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // all 4 waves: wave w merges partials w, w + 4, ... with every load issued first (one round trip), then the
+  // waves' states merge in wave order through LDS (a fixed tree: deterministic)
+  {
+    const unsigned bytes = (unsigned)((size_t)S * 3 * C * 4);
+    constexpr int PW = kFinMaxS / 4;
+    float v[PW][3];
+#pragma unroll
+    for (int u = 0; u < PW; ++u)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int sp2 = w + 4 * u;
+        v[u][k] = (cok && sp2 < S) ? ld_sc1(part, bytes, (unsigned)((((size_t)sp2 * 3 + k) * C + c) * 4)) : 0.f;
+      }
+    n = mu = m2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < PW; ++u) chan_merge(n, mu, m2, v[u][0], v[u][1], v[u][2]);
+    __syncthreads();  // wres reuse
+    wres[w][0][lane] = n;
+    wres[w][1][lane] = mu;
+    wres[w][2][lane] = m2;
+    __syncthreads();
+  }
+  if (w != 0 || !cok) return;
+  n = wres[0][0][lane];
+  mu = wres[0][1][lane];
+  m2 = wres[0][2][lane];
+  for (int q = 1; q < 4; ++q) chan_merge(n, mu, m2, wres[q][0][lane], wres[q][1][lane], wres[q][2][lane]);
+  if (merged_out) {
+    merged_out[c] = mu;
+    merged_out[C + c] = m2;
+    return;
+  }
+  const float var = m2 / (float)M;
+  const float unbiased = M > 1 ? m2 / (float)(M - 1) : m2;
+  rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+  rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+  if (c == 0 && nbt) nbt[0] += 1;
+  const float rstd = rsqrtf(var + eps);
+  const float a = gamma[c] * rstd;
+  a_out[c] = a;
+  b_out[c] = beta[c] - mu * a;
+  mean_out[c] = mu;
+  rstd_out[c] = rstd;
+}
+
+// Backward sums: part[B][2][C] (sum gz, sum gz*xhat per reduce block) -> c1 = sum/M, c2, and dgamma / dbeta
+// stored or applied (bwd_finalize_kernel's epilogue), blocks split over S workgroups per channel group.
+__global__ void __launch_bounds__(256)
+bwd_finalize_split_kernel(const float* __restrict__ part, int B, int C, int M, int S, float* __restrict__ c1,
+                          float* __restrict__ c2, void* __restrict__ dgamma, void* __restrict__ dbeta, int out_bf16,
+                          int accumulate, SgdArgs sg, SgdArgs sb) {
+  __shared__ float wres[4][2][64];
+  __shared__ int flag;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cg = blockIdx.x, sp = blockIdx.y;
+  const int c = cg * 64 + lane;
+  const bool cok = c < C;
+  const int cc = cok ? c : 0;
+  float s1 = 0.f, s2 = 0.f;
+  const int step = 4 * S;
+  int k = 4 * sp + w;
+  for (; k + 3 * step < B; k += 4 * step) {
+    float a[4], q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = part[((size_t)(k + u * step) * 2) * C + cc];
+      q[u] = part[((size_t)(k + u * step) * 2 + 1) * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += q[u]; }
+  }
+  for (; k < B; k += step) {
+    s1 += part[((size_t)k * 2) * C + cc];
+    s2 += part[((size_t)k * 2 + 1) * C + cc];
+  }
+  wres[w][0][lane] = s1;
+  wres[w][1][lane] = s2;
+  __syncthreads();
+  float* sc = g_bwd_scratch;
+  if (w == 0) {
+    s1 = ((wres[0][0][lane] + wres[1][0][lane]) + wres[2][0][lane]) + wres[3][0][lane];
+    s2 = ((wres[0][1][lane] + wres[1][1][lane]) + wres[2][1][lane]) + wres[3][1][lane];
+    if (cok) {
+      st_sc1(sc + ((size_t)sp * 2) * C + c, s1);
+      st_sc1(sc + ((size_t)sp * 2 + 1) * C + c, s2);
+    }
+  }
+  if (!take_last(&g_merge_tickets[1][cg], S, &flag)) return;
+  if (threadIdx.x == 0) __hip_atomic_store(&g_merge_tickets[1][cg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    const unsigned bytes = (unsigned)((size_t)S * 2 * C * 4);
+    constexpr int PW = kBwdMaxS / 4;
+    float v[PW][2];
+#pragma unroll
+    for (int u = 0; u < PW; ++u)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int sp2 = w + 4 * u;
+        v[u][j] = (cok && sp2 < S) ? ld_sc1(sc, bytes, (unsigned)((((size_t)sp2 * 2 + j) * C + c) * 4)) : 0.f;
+      }
+    s1 = s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < PW; ++u) { s1 += v[u][0]; s2 += v[u][1]; }
+    __syncthreads();
+    wres[w][0][lane] = s1;
+    wres[w][1][lane] = s2;
+    __syncthreads();
+  }
+  if (w != 0 || !cok) return;
+  s1 = ((wres[0][0][lane] + wres[1][0][lane]) + wres[2][0][lane]) + wres[3][0][lane];
+  s2 = ((wres[0][1][lane] + wres[1][1][lane]) + wres[2][1][lane]) + wres[3][1][lane];
+  c1[c] = s1 / (float)M;
+  c2[c] = s2 / (float)M;
+  auto put = [&](const SgdArgs& sgd, void* out, float v) {
+    if (sgd.p) {
+      sgd_apply(sgd, c, v, *sgd.lr);
+    } else if (out_bf16) {
+      unsigned short* d = reinterpret_cast<unsigned short*>(out) + c;
+      *d = f2bf(accumulate ? v + bf2f(*d) : v);
+    } else if (out) {
+      float* d = reinterpret_cast<float*>(out) + c;
+      *d = accumulate ? v + *d : v;
+    }
+  };
+  put(sg, dgamma, s2);
+  put(sb, dbeta, s1);
 }
 
 // ---------------------------------------------------------------- apply
@@ -449,9 +670,17 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const unsigned short* 
 
 using namespace ddpx;
 
+DDPX_API void ddpx_bn_set_merge(int legacy) { bn::g_merge_mode = legacy ? 1 : 0; }
+
 DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
                               float* a, float* b, float* mean, float* rstd, hipStream_t s) {
+  if (training && C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+    const int S = bn::fin_splits(T);
+    hipLaunchKernelGGL(bn::finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, stats, T, BM, M, C, S,
+                       gamma, beta, rmean, rvar, nbt, momentum, eps, a, b, mean, rstd, (float*)nullptr);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn::finalize_kernel, dim3(C), dim3(256), 0, s, stats, T, BM, M, C, gamma, beta, rmean,
                      rvar, nbt, momentum, eps, training, a, b, mean, rstd, (float*)nullptr);
   return (int)hipGetLastError();
@@ -462,6 +691,14 @@ DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, c
 // [ws][2][C] and ddpx_bn_finalize(gathered, T = ws, BM = M, M = ws * M) merges them in rank order — the
 // same Chan merge on every rank, so every rank normalises with bitwise-identical statistics.
 DDPX_API int ddpx_bn_local_stats(const float* stats, int T, int BM, int M, int C, float* out, hipStream_t s) {
+  if (C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+    const int S = bn::fin_splits(T);
+    hipLaunchKernelGGL(bn::finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, stats, T, BM, M, C, S,
+                       (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (int64_t*)nullptr, 0.f, 0.f, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, out);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn::finalize_kernel, dim3(C), dim3(256), 0, s, stats, T, BM, M, C, (const float*)nullptr,
                      (const float*)nullptr, (float*)nullptr, (float*)nullptr, (int64_t*)nullptr, 0.f, 0.f, 1,
                      (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, out);
@@ -476,6 +713,21 @@ DDPX_API int ddpx_bn_apply(const void* y, const float* a, const float* b, int N,
                      W, C, relu, pool, (unsigned short*)out);
   return (int)hipGetLastError();
 }
+
+namespace {
+hipError_t launch_bwd_finalize(const float* part, int B, int C, int M, float* c1, float* c2, void* dgamma, void* dbeta,
+                               int out_bf16, int accumulate, SgdArgs sg, SgdArgs sb, hipStream_t s) {
+  if (C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+    const int S = bn::bwd_splits(B);
+    hipLaunchKernelGGL(bn::bwd_finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, part, B, C, M, S, c1,
+                       c2, dgamma, dbeta, out_bf16, accumulate, sg, sb);
+  } else {
+    hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, M, c1, c2, dgamma,
+                       dbeta, out_bf16, accumulate, sg, sb);
+  }
+  return hipGetLastError();
+}
+}  // namespace
 
 DDPX_API int ddpx_bn_bwd_blocks(int N, int H, int W, int C) {
   const int lanes = 256 / (C / 8);
@@ -494,9 +746,8 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
-                     dgamma, dbeta, out_bf16, accumulate, SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd},
-                     SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd});
+  launch_bwd_finalize(part, B, C, N * H * W, c1, c2, dgamma, dbeta, out_bf16, accumulate,
+                      SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd}, SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd}, s);
   const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
   hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu, 1,
@@ -518,9 +769,9 @@ DDPX_API int ddpx_bn_bwd_sums(const void* gout, const void* y, const float* a, c
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, 1, sums, sums + C,
-                     dgamma, dbeta, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
-                     SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+  launch_bwd_finalize(part, B, C, 1, sums, sums + C, dgamma, dbeta, out_bf16, accumulate,
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, s);
   return (int)hipGetLastError();
 }
 
@@ -543,9 +794,9 @@ DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bia
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
-  hipLaunchKernelGGL(bn::bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, B, C, N * H * W, c1, c2,
-                     nullptr, dbias, out_bf16, accumulate, SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
-                     SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f});
+  launch_bwd_finalize(part, B, C, N * H * W, c1, c2, nullptr, dbias, out_bf16, accumulate,
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, s);
   const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
   hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
                      (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,

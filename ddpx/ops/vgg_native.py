@@ -22,12 +22,19 @@ the fp32 masters once per forward; dgrad reads them, so the fused update of W ne
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
 from . import conv as K
 from ..optim.sgd import take_lr_advance
 from .head import head_backward, head_forward
+
+
+# DDPX_CONV_PREP_FROM_UPDATE=0: re-derive the bf16 conv layouts every forward (weight_prep) even when the fused
+# update already wrote them (A/B checks)
+_PREP_FROM_UPDATE = os.environ.get("DDPX_CONV_PREP_FROM_UPDATE", "1") != "0"
 
 
 class _Plan:
@@ -157,7 +164,7 @@ def _backward(model, saved, last, dl, grad_out):
         if sw is not None:
             # prepared layouts current before this update (the forward made or kept them): the reduce rewrites
             # them with the updated weight, after this block's dgrad below has read wd (stream order)
-            prep = plan.wver[bi] == flat.version_of(conv.weight)
+            prep = _PREP_FROM_UPDATE and plan.wver[bi] == flat.version_of(conv.weight)
             if prep and bi > 0:
                 g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
             K.conv_wgrad(dy, x, Co, Cr, sgd=sw, prepared=(plan.wf[bi], plan.wd[bi]) if prep else None)

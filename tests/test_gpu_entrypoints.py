@@ -86,3 +86,20 @@ def test_bench_contract_one_gpu(gpu, tmp_path):
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 1 and rec["steps"] == 10 and rec["value"] > 0 and rec["dtype"] == "bf16"
+
+
+@pytest.mark.parametrize("model", ["mlp", "vgg"])
+def test_bench_batch_prefetch_trains_identically(gpu, tmp_path, model):
+    """The double-buffered batch prefetch (augment of step k+1 on a side stream during step k) trains on the
+    same batches in the same order: final loss and fp32 master + momentum bytes equal the in-step augment's,
+    over an odd number of graph replays (both buffer parities, eager warm-up steps included)."""
+    recs = []
+    for pf in (1, 0):
+        out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--model", model, "--steps", "7", "--warmup", "4",
+                    "--stock_ref", "0", "--digest", "1", "--prefetch_batch", str(pf)], tmp_path)
+        recs.append(json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1]))
+    a, b = recs
+    assert a["config"]["prefetch_batch"] is True and b["config"]["prefetch_batch"] is False
+    assert a["config"]["graph"] and b["config"]["graph"]
+    assert a["config"]["final_loss"] == b["config"]["final_loss"]
+    assert a["config"]["master_digest"] == b["config"]["master_digest"] is not None

@@ -205,3 +205,48 @@ def test_native_sync_batchnorm_kernels_match_local_bn(gpu):
     bad = [(n, _rel(q.main_grad, p.main_grad)) for (n, p), q in zip(a.named_parameters(), b.parameters())
            if _rel(q.main_grad, p.main_grad) > 2e-2]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("N,H,Ci,Co", [(512, 32, 8, 64), (512, 8, 256, 256), (64, 4, 512, 512), (5, 6, 16, 24)])
+def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
+    """BatchNorm statistics from the conv epilogue's tile partials: the two-level channel-coalesced merges
+    (default) and the per-channel ones (DDPX_BN_MERGE=legacy) both match an fp64 reduction of the stored bf16
+    outputs (batch mean / biased variance / running stats), and so do the backward sums (c1, c2, dgamma, dbeta)."""
+    from ddpx.ops import conv as K
+    from ddpx.runtime import native
+    torch.manual_seed(3)
+    lib = native.kernels()
+    xn = torch.randn(N, H, H, Ci, device=gpu).to(torch.bfloat16).contiguous()
+    wf = (torch.randn(Co * 9 * Ci, device=gpu) * (1.0 / (Ci * 9) ** 0.5)).to(torch.bfloat16)
+    y, st, T, BM = K.conv_fwd(xn, wf, Co)
+    P = N * H * H
+    y64 = y.double()
+    mean64 = y64.mean(0)
+    var64 = y64.var(0, unbiased=False)
+    g = torch.randn(P, Co, device=gpu).to(torch.bfloat16).contiguous()
+    outs = {}
+    try:
+        for legacy in (0, 1):
+            lib.ddpx_bn_set_merge(legacy)
+            bn = torch.nn.BatchNorm2d(Co).to(gpu)
+            a, b, mean, rstd = (torch.empty(Co, device=gpu) for _ in range(4))
+            K.bn_finalize(st, T, BM, P, bn, True, a, b, mean, rstd)
+            dgam, dbet = torch.zeros(Co, device=gpu), torch.zeros(Co, device=gpu)
+            dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, H, Co, False, dgamma=dgam, dbeta=dbet)
+            torch.cuda.synchronize()
+            outs[legacy] = (mean.clone(), rstd.clone(), bn.running_var.clone(), dgam, dbet, dy.float())
+    finally:
+        lib.ddpx_bn_set_merge(0)
+    rstd64 = (var64 + 1e-5).rsqrt()
+    xhat64 = (y64 - mean64) * rstd64
+    gz64 = xhat64.gt(0).double() * g.double()  # gamma 1, beta 0: ReLU mask of xhat (a rare fp32 flip at 0 is
+    # one |g| ~ 1 term of a sum over P elements: atol 4)
+    for legacy, (mean, rstd, rvar, dgam, dbet, dy) in outs.items():
+        assert torch.allclose(mean.double(), mean64, rtol=1e-5, atol=1e-5), legacy
+        assert torch.allclose(rstd.double(), rstd64, rtol=1e-4, atol=1e-5), legacy
+        assert torch.allclose(rvar.double(), 0.9 + 0.1 * y64.var(0, unbiased=True), rtol=1e-4, atol=1e-5), legacy
+        assert torch.allclose(dbet.double(), gz64.sum(0), rtol=1e-3, atol=4.0), legacy
+        assert torch.allclose(dgam.double(), (gz64 * xhat64).sum(0), rtol=1e-3, atol=4.0), legacy
+    # the two merges differ only by fp32 rounding of the merge order
+    assert _rel(outs[0][0], outs[1][0]) < 1e-5 and _rel(outs[0][1], outs[1][1]) < 1e-5
+    assert _rel(outs[0][5], outs[1][5]) < 1e-2
