@@ -46,7 +46,7 @@ struct Cfg {
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
-template <int STAGES>
+template <int STAGES, bool FP8>
 __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
@@ -155,82 +155,114 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     // optimizer's 18 B per weight at 6.2 TB/s with 4 vectors in flight per thread, against 3.5 TB/s holding a
     // whole tile (8 vectors, 128 VGPRs of state) ahead, which also pushed this kernel into register spills.
     constexpr int DIST = 4;
-    static_assert(VPT % DIST == 0, "ring");
+    static_assert(VPT % DIST == 0 && VPT == 2 * DIST, "ring");
+    // Every update issues the same memory operations — 3 stores (master, momentum, bf16; + the fp8 copy when
+    // FP8) then 2 refill loads, never skipped (no momentum: the momentum stream aliases the master and the
+    // "momentum" store rewrites the same value; past the last tile the refill reloads the current vector) —
+    // so the compiler can count the ring: a vector's loads are waited for with vmcnt(3 x ops per update),
+    // not vmcnt(0).  A data-dependent branch around a refill made hipcc drain the whole ring (and, as gfx950
+    // counts stores in vmcnt, the previous updates' stores) at every K-step.
     const int st = tid - 256;
     const int row0 = st >> 5, col = 4 * (st & 31);
     const float lr = *p.sgd.lr;
     const float mom = p.sgd.mom, wd = p.sgd.wd;
     const bool has_mom = mom != 0.f;
     f32x4 rp0, rp1, rp2, rp3, rm0, rm1, rm2, rm3;  // the ring (statically indexed)
+    // per-GEMM pointers selected as scalars (a reference to p0.sgd / p1.sgd picked at run time put the structs
+    // on the stack: scratch loads, which also count in vmcnt)
+    float* const P0 = p0.sgd.p;
+    float* const P1 = p1.sgd.p;
+    float* const M0 = has_mom ? p0.sgd.buf : p0.sgd.p;
+    float* const M1 = has_mom ? p1.sgd.buf : p1.sgd.p;
+    unsigned short* const S0 = p0.sgd.shadow;
+    unsigned short* const S1 = p1.sgd.shadow;
+    unsigned char* const Q0 = p0.sgd.q8;
+    unsigned char* const Q1 = p1.sgd.q8;
+    unsigned char* const E0 = p0.sgd.s8;
+    unsigned char* const E1 = p1.sgd.s8;
+    const int ldc0 = p0.ldc, ldc1 = p1.ldc;
+    auto vec_off = [&](int j, int v, int& sel) -> size_t {
+      int m0, n0;
+      sel = tile_origin(j, m0, n0);
+      return (size_t)(m0 + row0 + 8 * v) * (sel ? ldc1 : ldc0) + n0 + col;
+    };
     // load vector v of tile j into a ring slot
     auto load_vec = [&](int j, int v, f32x4& pv, f32x4& mv) {
-      int m0, n0;
-      const int sel = tile_origin(j, m0, n0);
-      const SgdArgs& sg = sel ? p1.sgd : p0.sgd;
-      const size_t off = (size_t)(m0 + row0 + 8 * v) * (sel ? p1.ldc : p0.ldc) + n0 + col;
-      pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.p + off));
-      mv = has_mom ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sg.buf + off))
-                   : (f32x4){0.f, 0.f, 0.f, 0.f};
+      int sel;
+      const size_t off = vec_off(j, v, sel);
+      pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? P1 : P0) + off));
+      mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? M1 : M0) + off));
     };
     // update vector v of tile j from the gradient tile T, then refill the slot with the vector DIST ahead
     auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
-      int m0, n0;
-      const int sel = tile_origin(j, m0, n0);
+      int sel;
+      const size_t off = vec_off(j, v, sel);
       const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + 8 * v) * ALD + col);
       f32x4 po, bo;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
         float d = fmaf(wd, pv[q], g[q]);
-        if (has_mom) {
-          d = fmaf(mom, mv[q], d);
-          bo[q] = d;
-        }
+        if (has_mom) d = fmaf(mom, mv[q], d);
         po[q] = fmaf(-lr, d, pv[q]);
+        bo[q] = has_mom ? d : po[q];
       }
-      const SgdArgs& sg = sel ? p1.sgd : p0.sgd;
-      const size_t off = (size_t)(m0 + row0 + 8 * v) * (sel ? p1.ldc : p0.ldc) + n0 + col;
-      __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(sg.p + off));
-      if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sg.buf + off));
-      if (sg.shadow)
-        *reinterpret_cast<u32x2*>(sg.shadow + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
-      if (sg.q8) {  // MX-FP8 weight copy for the next forward: 8 lanes = one 32-column block (uniform branch)
+      __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>((sel ? P1 : P0) + off));
+      __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>((sel ? M1 : M0) + off));
+      *reinterpret_cast<u32x2*>((sel ? S1 : S0) + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      if constexpr (FP8) {  // MX-FP8 weight copy for the next forward: 8 lanes = one 32-column block
         unsigned e8;
         const unsigned q = mx::e4m3_group8(po, &e8);
-        *reinterpret_cast<unsigned*>(sg.q8 + off) = q;
+        *reinterpret_cast<unsigned*>((sel ? Q1 : Q0) + off) = q;
         // the row's 4 block scales (lanes 0/8/16/24 of each half-wave) as ONE dword store by the half-wave's
         // first lane: byte stores scattered over the tile's rows cost more than the codes themselves
         const unsigned e1 = __shfl_down(e8, 8, 64), e2 = __shfl_down(e8, 16, 64), e3 = __shfl_down(e8, 24, 64);
         if ((lane & 31) == 0)
-          *reinterpret_cast<unsigned*>(sg.s8 + (off >> 5)) = e8 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+          *reinterpret_cast<unsigned*>((sel ? E1 : E0) + (off >> 5)) = e8 | (e1 << 8) | (e2 << 16) | (e3 << 24);
       }
-      // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1
+      // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1, or (past the last tile)
+      // vector v of tile j again — a harmless reload that keeps the per-update operation count fixed
       const int vn = v + DIST;
-      if (vn < VPT) load_vec(j, vn, pv, mv);
-      else if (j + 1 < nt) load_vec(j + 1, vn - VPT, pv, mv);
+      const bool same = vn < VPT, next = !same && j + 1 < nt;
+      load_vec(same ? j : (next ? j + 1 : j), same ? vn : (next ? vn - VPT : v), pv, mv);
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
-    if (nt > 0) {
-      load_vec(0, 0, rp0, rm0);
-      load_vec(0, 1, rp1, rm1);
-      load_vec(0, 2, rp2, rm2);
-      load_vec(0, 3, rp3, rm3);
-    }
-    for (int i = 0; i <= nt; ++i) {
+    load_vec(0, 0, rp0, rm0);
+    load_vec(0, 1, rp1, rm1);
+    load_vec(0, 2, rp2, rm2);
+    load_vec(0, 3, rp3, rm3);
+    for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
+    // trip r = 4 K-steps: iteration i = 1 + r / 2 updates tile i - 1, vectors (r & 1) * 4 .. + 3; the first trip
+    // is peeled so the loop is entered with the same memory operations in flight as on its back edge (the
+    // compiler then counts every update's ring wait as vmcnt(15) instead of the entry path's 4)
+    auto trip = [&](int r) {
+      const int i = 1 + (r >> 1), t = (r & 1) * DIST;
       const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
-      for (int t = 0; t < nk; t += DIST) {
-        // K-steps t .. t+3 of iteration i: vectors t .. t+3 of tile i-1 (nk == VPT)
-        __builtin_amdgcn_s_barrier();
-        if (i > 0) update_vec(i - 1, t, T, rp0, rm0);
-        __builtin_amdgcn_s_barrier();
-        if (i > 0) update_vec(i - 1, t + 1, T, rp1, rm1);
-        __builtin_amdgcn_s_barrier();
-        if (i > 0) update_vec(i - 1, t + 2, T, rp2, rm2);
-        __builtin_amdgcn_s_barrier();
-        if (i > 0) update_vec(i - 1, t + 3, T, rp3, rm3);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // sched_barrier: keep each update's register work (which waits for its ring slot) inside its own K-step
       __builtin_amdgcn_s_barrier();
-    }
+      __builtin_amdgcn_sched_barrier(0);
+      update_vec(i - 1, t, T, rp0, rm0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      update_vec(i - 1, t + 1, T, rp1, rm1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      update_vec(i - 1, t + 2, T, rp2, rm2);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      update_vec(i - 1, t + 3, T, rp3, rm3);
+      __builtin_amdgcn_sched_barrier(0);
+      if (r & 1) {  // end of iteration i: the buffer hand-off barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    };
+    trip(0);
+#pragma unroll 1
+    for (int r = 1; r < 2 * nt; ++r) trip(r);
   }
 }
 
@@ -239,7 +271,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
 // are nk + 1 per iteration), ldc % 4 == 0.
 static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
   return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K == 64 * VPT && (p.ldc & 3) == 0 && p.sgd.p &&
-         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3)));
+         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && p.sgd.shadow && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3)));
 }
 
 // Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:
@@ -267,8 +299,14 @@ static inline int spread() {
 static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  if (stages(ntiles, num_cus) == 4) hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p, p, 0, spread());
-  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+  const bool fp8 = p.sgd.q8 != nullptr;
+  if (stages(ntiles, num_cus) == 4) {
+    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, true>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+  } else {
+    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, true>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+  }
   return hipGetLastError();
 }
 
@@ -282,9 +320,15 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int nt1 = (p1.M / BM) * (p1.N / BN);
   const int ntiles = (p0.M / BM) * (p0.N / BN) + nt1;
   const int grid = ntiles < num_cus ? ntiles : num_cus;
-  if (stages(ntiles, num_cus) == 4)
-    hipLaunchKernelGGL(wgrad_sgd_ws_kernel<4>, dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
-  else hipLaunchKernelGGL(wgrad_sgd_ws_kernel<3>, dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+  if ((p0.sgd.q8 != nullptr) != (p1.sgd.q8 != nullptr)) return hipErrorInvalidValue;  // both or neither
+  const bool fp8 = p0.sgd.q8 != nullptr;
+  if (stages(ntiles, num_cus) == 4) {
+    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, true>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+  } else {
+    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, true>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+  }
   return hipGetLastError();
 }
 

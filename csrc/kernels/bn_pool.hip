@@ -123,15 +123,22 @@ finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, co
 // merges the S partials in split order: deterministic, and the hand-off is MI355X_MICROARCH "Valid forms" row 1
 // (sc1 stores drained by vmcnt(0) before the ticket, sc1 loads after it).  Tickets reset by their last arriver.
 constexpr int kMergeMaxC = 1024, kFinMaxS = 32, kBwdMaxS = 32;
-// DDPX_BN_MERGE=legacy (or ddpx_bn_set_merge(1)): the per-channel merge kernels above (A/B measurements)
+// Which merges use the two-level kernels: 0 both, 1 neither (the per-channel kernels above; default), 2 the
+// backward sums only.  Split, the forward statistics merge measured no faster (86.8 vs 87 us per VGG step) and
+// the backward one 83 -> 61 us; both match fp64 like the per-channel ones (tests/test_gpu_vgg.py), but the
+// changed summation order moves the deterministic bf16 VGG trajectory of tests/test_gpu_parity.py from a tail
+// loss of 0.53 (per-channel) to 0.65-0.71 against torch fp32's 0.47-0.56 (profiles/r3_bn/NOTES.md), so the
+// per-channel merges stay the default.  DDPX_BN_MERGE=split|legacy|bwd, or ddpx_bn_set_merge(mode).
 static int g_merge_mode = -1;
-static inline bool merge_legacy() {
+static inline int merge_mode() {
   if (g_merge_mode < 0) {
     const char* e = getenv("DDPX_BN_MERGE");
-    g_merge_mode = (e && e[0] == 'l') ? 1 : 0;
+    g_merge_mode = !e ? 1 : (e[0] == 's' ? 0 : (e[0] == 'b' ? 2 : 1));
   }
-  return g_merge_mode == 1;
+  return g_merge_mode;
 }
+static inline bool merge_legacy() { return merge_mode() != 0; }        // forward statistics
+static inline bool merge_legacy_bwd() { return merge_mode() == 1; }    // backward sums
 __device__ int g_merge_tickets[2][kMergeMaxC / 64];
 __device__ float g_fin_scratch[kFinMaxS * 3 * kMergeMaxC];
 __device__ float g_bwd_scratch[kBwdMaxS * 2 * kMergeMaxC];
@@ -670,7 +677,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const unsigned short* 
 
 using namespace ddpx;
 
-DDPX_API void ddpx_bn_set_merge(int legacy) { bn::g_merge_mode = legacy ? 1 : 0; }
+DDPX_API void ddpx_bn_set_merge(int mode) { bn::g_merge_mode = mode < 0 || mode > 2 ? 1 : mode; }
 
 DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
@@ -717,7 +724,7 @@ DDPX_API int ddpx_bn_apply(const void* y, const float* a, const float* b, int N,
 namespace {
 hipError_t launch_bwd_finalize(const float* part, int B, int C, int M, float* c1, float* c2, void* dgamma, void* dbeta,
                                int out_bf16, int accumulate, SgdArgs sg, SgdArgs sb, hipStream_t s) {
-  if (C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+  if (C <= bn::kMergeMaxC && !bn::merge_legacy_bwd()) {
     const int S = bn::bwd_splits(B);
     hipLaunchKernelGGL(bn::bwd_finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, part, B, C, M, S, c1,
                        c2, dgamma, dbeta, out_bf16, accumulate, sg, sb);

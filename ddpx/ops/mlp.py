@@ -87,8 +87,8 @@ def _forward(model, x, targets, want_logits, want_grad, for_backward=None):
                 hq = F8.quant(hs[-1], F8.E4M3)
             if flat.shadow8 is None:
                 flat.enable_fp8_shadow()
-            # the e4m3 weight copy in the store: re-quantised from the bf16 copy when stale (every step, unless
-            # the optimizer writes it: DDPX_FP8_COPY=1)
+            # the e4m3 weight copy in the store: the fused wgrad+SGD pair writes it (default), anything else that
+            # updated the weight leaves it stale and it is re-quantised from the bf16 copy here
             wq = flat.mx8_weight(w)
             hs.append(F8.gemm(hq, wq, epi=G.EPI_BIAS_RELU_BF16, bias=b))
         else:
@@ -144,7 +144,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             elif l == 0 and deferred is not None:
                 d1, h1, s1, w1 = deferred
                 s0 = flat.fused_spec(w)
-                # fp8 model with DDPX_FP8_COPY=1: the stream waves also emit both weights' MX-FP8 copies
+                # fp8 model (DDPX_FP8_COPY=pair|1, default pair): the stream waves also emit both weights' MX-FP8 copies
                 emit = flat.shadow8 is not None and flat.fp8_from_optimizer
                 mx1, mx0 = (flat.mx8_views(w1), flat.mx8_views(w)) if emit else (None, None)
                 paired = G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0, mx1, mx0)

@@ -107,10 +107,13 @@ class FlatParams:
         self.shadow8 = None
         self.scale8 = None
         self.fp8_fresh = [False] * len(self.params)
-        # the optimizer kernels write the fp8 copy next to the bf16 one (DDPX_FP8_COPY=1); default off: on the
-        # wide MLP the extra stream output costs the fused wgrad+SGD pair ~200 us, more than the separate
-        # quantisation of both weights (~174 us) it replaces (profiles/r3_fp8)
-        self.fp8_from_optimizer = os.environ.get("DDPX_FP8_COPY", "0") == "1"
+        # which optimizer kernels write the fp8 copy next to the bf16 one (DDPX_FP8_COPY): "pair" (default) the
+        # fused wgrad+SGD stream (+53-126 us on the wide MLP's pair vs 175 us for quantising both weights
+        # separately, profiles/r3_fp8), "1" also the flat SGD (DDP path; not measured faster), "0" none (every
+        # fp8 forward re-quantises the bf16 copy)
+        mode = os.environ.get("DDPX_FP8_COPY", "pair")
+        self.fp8_from_optimizer = mode in ("1", "pair")
+        self.fp8_from_flat_sgd = mode == "1"
         self._hooks = []
         for p in self.params:
             if id(p) not in self.native:
@@ -174,7 +177,7 @@ class FlatParams:
 
     def mx8_range(self, start, end):
         """(codes, scales) slices of the fp8 copy for a flat update of [start, end), or None."""
-        if self.shadow8 is None or not self.fp8_from_optimizer or start % 32 or (end - start) % 32:
+        if self.shadow8 is None or not self.fp8_from_flat_sgd or start % 32 or (end - start) % 32:
             return None
         return self.shadow8[start:end], self.scale8[start // 32:end // 32]
 

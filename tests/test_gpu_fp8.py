@@ -184,7 +184,7 @@ def test_wgrad_sgd_pair_emits_mx8_copy(gpu, mom):
 def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused, from_opt):
     """fp8 MLP training: the hidden weights' fp8 copy used by each forward equals the quantiser's output for
     the bf16 copy.  With the optimizer writing it (DDPX_FP8_COPY=1: the fused pair or the flat SGD) the forward
-    never re-quantises after the first step; by default it re-quantises both weights every step."""
+    never re-quantises after the first step; without (DDPX_FP8_COPY=0) it re-quantises both weights every step."""
     import ddpx
     from ddpx.models import MLP
     from ddpx.ops import fp8 as F8
@@ -197,7 +197,7 @@ def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused, from_opt):
     x = torch.rand(512, 3072, device=gpu).to(torch.bfloat16)
     t = torch.randint(0, 10, (512,), device=gpu)
     flat = m.fc0.weight._ddpx_flat
-    flat.fp8_from_optimizer = from_opt
+    flat.fp8_from_optimizer = flat.fp8_from_flat_sgd = from_opt
     calls = []
     orig = F8.quant
     for step in range(3):

@@ -75,23 +75,34 @@ def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     # one-cycle over the whole run: 20 "epochs" of steps/20 batches
     lam = OneCycleLambda(steps_per_epoch=steps // 20, num_epochs=20)
 
-    o_ref = torch.optim.SGD(ref.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
-    s_ref = torch.optim.lr_scheduler.LambdaLR(o_ref, lam)
-    l_ref = _train(ref, DeviceLoader(train, B, gpu, layout="nchw_f32", seed=0), o_ref, s_ref, steps, False)
+    # the stock fp32 reference is not bitwise reproducible on the GPU (MIOpen / hipBLASLt algorithm choice and
+    # reduction order): two runs from the same weights measured tail losses 0.47-0.56 and test accuracies
+    # 86.5-90.1 % (profiles/r3_bn/NOTES.md).  The reference band below is widened by the spread of two runs.
+    init = {k: v.clone() for k, v in ref.state_dict().items()}
+    refs = []
+    for _ in range(2):
+        ref.load_state_dict(init)
+        o_ref = torch.optim.SGD(ref.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
+        s_ref = torch.optim.lr_scheduler.LambdaLR(o_ref, lam)
+        l_ref = _train(ref, DeviceLoader(train, B, gpu, layout="nchw_f32", seed=0), o_ref, s_ref, steps, False)
+        refs.append((l_ref, _accuracy(ref, DeviceLoader(test, B, gpu, train=False, layout="nchw_f32"))))
 
     o_nat = SGD(nat.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, fused_backward=True)
     s_nat = torch.optim.lr_scheduler.LambdaLR(o_nat, lam)
     l_nat = _train(nat, DeviceLoader(train, B, gpu, layout="nhwc8_bf16", seed=0), o_nat, s_nat, steps, True)
     torch.cuda.synchronize()
 
-    assert torch.isfinite(l_nat).all() and torch.isfinite(l_ref).all()
-    tail_ref, tail_nat = l_ref[-20:].mean().item(), l_nat[-20:].mean().item()
-    acc_ref = _accuracy(ref, DeviceLoader(test, B, gpu, train=False, layout="nchw_f32"))
+    assert torch.isfinite(l_nat).all() and all(torch.isfinite(lr_).all() for lr_, _ in refs)
+    tails = [lr_[-20:].mean().item() for lr_, _ in refs]
+    accs = [a for _, a in refs]
+    tail_ref, acc_ref = sum(tails) / 2, sum(accs) / 2
+    tail_nat = l_nat[-20:].mean().item()
     acc_nat = _accuracy(nat, DeviceLoader(test, B, gpu, train=False, layout="nhwc8_bf16"))
-    print(f"\nloss first/last-20 ref {l_ref[:10].mean():.4f}/{tail_ref:.4f} native {l_nat[:10].mean():.4f}/"
-          f"{tail_nat:.4f}; test accuracy ref {acc_ref:.2f}% native {acc_nat:.2f}%")
+    print(f"\nloss last-20 ref {tails[0]:.4f} / {tails[1]:.4f} native {tail_nat:.4f}; test accuracy ref "
+          f"{accs[0]:.2f}% / {accs[1]:.2f}% native {acc_nat:.2f}%")
     # both learn the task ...
-    assert tail_ref < 0.8 * l_ref[:10].mean().item() and acc_ref > 30.0
+    for lr_, a in refs:
+        assert lr_[-20:].mean().item() < 0.8 * lr_[:10].mean().item() and a > 30.0
     # ... and end in the same place: bf16 compute vs fp32 changes the trajectory, not the outcome
-    assert abs(tail_nat - tail_ref) < max(0.05, 0.25 * tail_ref), (tail_nat, tail_ref)
-    assert abs(acc_nat - acc_ref) < 5.0, (acc_nat, acc_ref)  # measured 89.3 vs 86.5 % at step 100
+    assert abs(tail_nat - tail_ref) < max(0.05, 0.25 * tail_ref) + abs(tails[0] - tails[1]), (tail_nat, tails)
+    assert abs(acc_nat - acc_ref) < 5.0 + abs(accs[0] - accs[1]), (acc_nat, accs)

@@ -210,8 +210,8 @@ def test_native_sync_batchnorm_kernels_match_local_bn(gpu):
 @pytest.mark.parametrize("N,H,Ci,Co", [(512, 32, 8, 64), (512, 8, 256, 256), (64, 4, 512, 512), (5, 6, 16, 24)])
 def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
     """BatchNorm statistics from the conv epilogue's tile partials: the two-level channel-coalesced merges
-    (default) and the per-channel ones (DDPX_BN_MERGE=legacy) both match an fp64 reduction of the stored bf16
-    outputs (batch mean / biased variance / running stats), and so do the backward sums (c1, c2, dgamma, dbeta)."""
+    (mode 0, DDPX_BN_MERGE=split) and the per-channel ones (mode 1, the default) both match an fp64 reduction of the stored bf16 outputs (batch mean / biased variance /
+    running stats), and so do the backward sums (c1, c2, dgamma, dbeta)."""
     from ddpx.ops import conv as K
     from ddpx.runtime import native
     torch.manual_seed(3)
@@ -227,7 +227,7 @@ def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
     outs = {}
     try:
         for legacy in (0, 1):
-            lib.ddpx_bn_set_merge(legacy)
+            lib.ddpx_bn_set_merge(1 if legacy else 0)
             bn = torch.nn.BatchNorm2d(Co).to(gpu)
             a, b, mean, rstd = (torch.empty(Co, device=gpu) for _ in range(4))
             K.bn_finalize(st, T, BM, P, bn, True, a, b, mean, rstd)
@@ -236,7 +236,7 @@ def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
             torch.cuda.synchronize()
             outs[legacy] = (mean.clone(), rstd.clone(), bn.running_var.clone(), dgam, dbet, dy.float())
     finally:
-        lib.ddpx_bn_set_merge(0)
+        lib.ddpx_bn_set_merge(1)
     rstd64 = (var64 + 1e-5).rsqrt()
     xhat64 = (y64 - mean64) * rstd64
     gz64 = xhat64.gt(0).double() * g.double()  # gamma 1, beta 0: ReLU mask of xhat (a rare fp32 flip at 0 is
