@@ -46,7 +46,7 @@ struct Cfg {
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
-template <int STAGES, bool FP8>
+template <int STAGES, bool FP8, int DIST, bool NORD>
 __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
@@ -63,13 +63,22 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
   const int nt = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= ntiles)
   const int nk = p0.K / 64;
   // tile i of this workgroup: origin and which GEMM it belongs to (uniform per workgroup)
+  // NORD: the tiles running at once sweep whole rows of W (n fastest): the optimizer stream then reads and
+  // writes every row's 512-B tile segments side by side instead of 64 rows x 4 segments scattered over W
+  // (m fastest), which is what the HBM sees of 256 CUs streaming at once.
   auto tile_origin = [&](int i, int& m0, int& n0) -> int {
     int g = (int)blockIdx.x + i * (int)gridDim.x;
     const int sel = g >= nt0;
     if (sel) g -= nt0;
-    const int tm = sel ? tiles_m1 : tiles_m0;
-    m0 = (g % tm) * BM;
-    n0 = (g / tm) * BN;
+    if constexpr (NORD) {
+      const int tn = (sel ? p1.N : p0.N) / BN;
+      m0 = (g / tn) * BM;
+      n0 = (g % tn) * BN;
+    } else {
+      const int tm = sel ? tiles_m1 : tiles_m0;
+      m0 = (g % tm) * BM;
+      n0 = (g / tm) * BN;
+    }
     return sel;
   };
   const pipe::Params& p = p0;  // K, alpha, lr, momentum, wd: shared by both GEMMs
@@ -154,20 +163,16 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     // ring of DIST register slots.  Profiled on MI355X (benchmarks/stream_probe.hip): 4 waves per CU stream the
     // optimizer's 18 B per weight at 6.2 TB/s with 4 vectors in flight per thread, against 3.5 TB/s holding a
     // whole tile (8 vectors, 128 VGPRs of state) ahead, which also pushed this kernel into register spills.
-    constexpr int DIST = 4;
-    static_assert(VPT % DIST == 0 && VPT == 2 * DIST, "ring");
-    // Every update issues the same memory operations — 3 stores (master, momentum, bf16; + the fp8 copy when
-    // FP8) then 2 refill loads, never skipped (no momentum: the momentum stream aliases the master and the
-    // "momentum" store rewrites the same value; past the last tile the refill reloads the current vector) —
-    // so the compiler can count the ring: a vector's loads are waited for with vmcnt(3 x ops per update),
-    // not vmcnt(0).  A data-dependent branch around a refill made hipcc drain the whole ring (and, as gfx950
-    // counts stores in vmcnt, the previous updates' stores) at every K-step.
+    static_assert(VPT % DIST == 0, "ring");
+    // DIST vectors in flight per thread.  The stream is bound by bytes in flight (Little's law: 4 waves x
+    // DIST x 2 KiB per CU against ~2 us of loaded HBM latency): DIST = 4 streams ~4.3 TB/s, DIST = 8 (a whole
+    // tile ahead, 64 ring VGPRs) doubles what is in flight (DDPX_WSGD_DIST, profiles/r3_wsgd).
     const int st = tid - 256;
     const int row0 = st >> 5, col = 4 * (st & 31);
     const float lr = *p.sgd.lr;
     const float mom = p.sgd.mom, wd = p.sgd.wd;
     const bool has_mom = mom != 0.f;
-    f32x4 rp0, rp1, rp2, rp3, rm0, rm1, rm2, rm3;  // the ring (statically indexed)
+    f32x4 rp[DIST], rm[DIST];  // the ring (statically indexed: every loop over it is unrolled)
     // per-GEMM pointers selected as scalars (a reference to p0.sgd / p1.sgd picked at run time put the structs
     // on the stack: scratch loads, which also count in vmcnt)
     float* const P0 = p0.sgd.p;
@@ -226,43 +231,34 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
       load_vec(same ? j : (next ? j + 1 : j), same ? vn : (next ? vn - VPT : v), pv, mv);
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
-    load_vec(0, 0, rp0, rm0);
-    load_vec(0, 1, rp1, rm1);
-    load_vec(0, 2, rp2, rm2);
-    load_vec(0, 3, rp3, rm3);
+#pragma unroll
+    for (int v = 0; v < DIST; ++v) load_vec(0, v, rp[v], rm[v]);
     for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_barrier();
-    // trip r = 4 K-steps: iteration i = 1 + r / 2 updates tile i - 1, vectors (r & 1) * 4 .. + 3; the first trip
-    // is peeled so the loop is entered with the same memory operations in flight as on its back edge (the
-    // compiler then counts every update's ring wait as vmcnt(15) instead of the entry path's 4)
+    // trip r = DIST K-steps: iteration i = 1 + r / TPI updates tile i - 1, vectors (r % TPI) * DIST .. + DIST - 1;
+    // the first trip is peeled so the loop is entered with the same memory operations in flight as on its back
+    // edge (the compiler then counts every update's ring wait, e.g. vmcnt(15) at DIST = 4, instead of the
+    // entry path's smaller count)
+    constexpr int TPI = VPT / DIST;  // trips per iteration
     auto trip = [&](int r) {
-      const int i = 1 + (r >> 1), t = (r & 1) * DIST;
+      const int i = 1 + r / TPI, t = (r % TPI) * DIST;
       const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
-      // sched_barrier: keep each update's register work (which waits for its ring slot) inside its own K-step
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      update_vec(i - 1, t, T, rp0, rm0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      update_vec(i - 1, t + 1, T, rp1, rm1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      update_vec(i - 1, t + 2, T, rp2, rm2);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      update_vec(i - 1, t + 3, T, rp3, rm3);
-      __builtin_amdgcn_sched_barrier(0);
-      if (r & 1) {  // end of iteration i: the buffer hand-off barrier
+#pragma unroll
+      for (int u = 0; u < DIST; ++u) {
+        // sched_barrier: keep each update's register work (which waits for its ring slot) inside its K-step
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        update_vec(i - 1, t + u, T, rp[u], rm[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
     };
     trip(0);
 #pragma unroll 1
-    for (int r = 1; r < 2 * nt; ++r) trip(r);
+    for (int r = 1; r < TPI * nt; ++r) trip(r);
   }
 }
 
@@ -296,16 +292,45 @@ static inline int spread() {
   return v;
 }
 
+// Stream ring depth: DDPX_WSGD_DIST=4|8 (default 4: 8 measured no faster, 125.0 vs 124.7 us, profiles/r3_wsgd).
+static inline int dist() {
+  static const int v = [] {
+    const char* e = getenv("DDPX_WSGD_DIST");
+    return e && e[0] == '8' ? 8 : 4;
+  }();
+  return v;
+}
+// Tile order: DDPX_WSGD_ORDER=n (n fastest, default) | m.
+static inline bool n_order() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_WSGD_ORDER");
+    return !(e && e[0] == 'm');
+  }();
+  return v;
+}
+
+template <int STAGES, bool FP8>
+static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1) {
+  const bool no = n_order();
+  if (dist() == 8) {
+    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+  } else {
+    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, false>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+  }
+}
+
 static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t s) {
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   const bool fp8 = p.sgd.q8 != nullptr;
   if (stages(ntiles, num_cus) == 4) {
-    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, true>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+    if (fp8) launch_dist<4, true>(dim3(grid), s, p, p, 0);
+    else launch_dist<4, false>(dim3(grid), s, p, p, 0);
   } else {
-    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, true>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false>), dim3(grid), dim3(512), 0, s, p, p, 0, spread());
+    if (fp8) launch_dist<3, true>(dim3(grid), s, p, p, 0);
+    else launch_dist<3, false>(dim3(grid), s, p, p, 0);
   }
   return hipGetLastError();
 }
@@ -323,11 +348,11 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   if ((p0.sgd.q8 != nullptr) != (p1.sgd.q8 != nullptr)) return hipErrorInvalidValue;  // both or neither
   const bool fp8 = p0.sgd.q8 != nullptr;
   if (stages(ntiles, num_cus) == 4) {
-    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, true>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+    if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1);
+    else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1);
   } else {
-    if (fp8) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, true>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false>), dim3(grid), dim3(512), 0, s, p0, p1, nt1, spread());
+    if (fp8) launch_dist<3, true>(dim3(grid), s, p0, p1, nt1);
+    else launch_dist<3, false>(dim3(grid), s, p0, p1, nt1);
   }
   return hipGetLastError();
 }
