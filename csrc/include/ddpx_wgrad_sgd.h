@@ -46,8 +46,8 @@ struct Cfg {
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
-template <int STAGES, bool FP8, int DIST, bool NORD>
-__global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
+template <int STAGES, bool FP8, int NSW, bool NORD>
+__global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
@@ -163,12 +163,15 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     // ring of DIST register slots.  Profiled on MI355X (benchmarks/stream_probe.hip): 4 waves per CU stream the
     // optimizer's 18 B per weight at 6.2 TB/s with 4 vectors in flight per thread, against 3.5 TB/s holding a
     // whole tile (8 vectors, 128 VGPRs of state) ahead, which also pushed this kernel into register spills.
-    static_assert(VPT % DIST == 0, "ring");
-    // DIST vectors in flight per thread.  The stream is bound by bytes in flight (Little's law: 4 waves x
-    // DIST x 2 KiB per CU against ~2 us of loaded HBM latency): DIST = 4 streams ~4.3 TB/s, DIST = 8 (a whole
-    // tile ahead, 64 ring VGPRs) doubles what is in flight (DDPX_WSGD_DIST, profiles/r3_wsgd).
+    // NSW stream waves (4, or 8 with DDPX_WSGD_STREAM_WAVES=8): SV vectors per stream thread per tile, one
+    // update every KPU K-steps; a ring of DIST = 4 vectors in flight per thread (a ring of 8 measured no faster).
+    constexpr int DIST = 4;
+    constexpr int SV = BM * BN / 4 / (NSW * 64);  // 8 (NSW 4) or 4 (NSW 8)
+    constexpr int KPU = VPT / SV;                 // K-steps per update: 1 or 2
+    constexpr int RSTEP = NSW * 2;                // tile rows between a thread's consecutive vectors
+    static_assert(SV % DIST == 0 && VPT % SV == 0, "ring");
     const int st = tid - 256;
-    const int row0 = st >> 5, col = 4 * (st & 31);
+    const int row0 = st >> 5, col = 4 * (st & 31);  // row0 < RSTEP
     const float lr = *p.sgd.lr;
     const float mom = p.sgd.mom, wd = p.sgd.wd;
     const bool has_mom = mom != 0.f;
@@ -189,7 +192,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     auto vec_off = [&](int j, int v, int& sel) -> size_t {
       int m0, n0;
       sel = tile_origin(j, m0, n0);
-      return (size_t)(m0 + row0 + 8 * v) * (sel ? ldc1 : ldc0) + n0 + col;
+      return (size_t)(m0 + row0 + RSTEP * v) * (sel ? ldc1 : ldc0) + n0 + col;
     };
     // load vector v of tile j into a ring slot
     auto load_vec = [&](int j, int v, f32x4& pv, f32x4& mv) {
@@ -202,7 +205,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
       int sel;
       const size_t off = vec_off(j, v, sel);
-      const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + 8 * v) * ALD + col);
+      const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + RSTEP * v) * ALD + col);
       f32x4 po, bo;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
@@ -227,8 +230,8 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
       // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1, or (past the last tile)
       // vector v of tile j again — a harmless reload that keeps the per-update operation count fixed
       const int vn = v + DIST;
-      const bool same = vn < VPT, next = !same && j + 1 < nt;
-      load_vec(same ? j : (next ? j + 1 : j), same ? vn : (next ? vn - VPT : v), pv, mv);
+      const bool same = vn < SV, next = !same && j + 1 < nt;
+      load_vec(same ? j : (next ? j + 1 : j), same ? vn : (next ? vn - SV : v), pv, mv);
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
 #pragma unroll
@@ -239,7 +242,7 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
     // the first trip is peeled so the loop is entered with the same memory operations in flight as on its back
     // edge (the compiler then counts every update's ring wait, e.g. vmcnt(15) at DIST = 4, instead of the
     // entry path's smaller count)
-    constexpr int TPI = VPT / DIST;  // trips per iteration
+    constexpr int TPI = SV / DIST;  // trips per iteration
     auto trip = [&](int r) {
       const int i = 1 + r / TPI, t = (r % TPI) * DIST;
       const float* T = accb + ((i - 1) & 1) * (ACC_BYTES / 4);
@@ -250,6 +253,8 @@ __global__ void __launch_bounds__(512) wgrad_sgd_ws_kernel(pipe::Params p0, pipe
         __builtin_amdgcn_sched_barrier(0);
         update_vec(i - 1, t + u, T, rp[u], rm[u]);
         __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 1; k < KPU; ++k) __builtin_amdgcn_s_barrier();
       }
       if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -292,13 +297,16 @@ static inline int spread() {
   return v;
 }
 
-// Stream ring depth: DDPX_WSGD_DIST=4|8 (default 4: 8 measured no faster, 125.0 vs 124.7 us, profiles/r3_wsgd).
-static inline int dist() {
-  static const int v = [] {
-    const char* e = getenv("DDPX_WSGD_DIST");
-    return e && e[0] == '8' ? 8 : 4;
+// Stream waves per workgroup: DDPX_WSGD_STREAM_WAVES=4|8 forces it; by default 8 once every CU owns >= 64
+// tiles (wide MLP, ~150 tiles per CU: 2.108 vs 2.175 ms/step) and 4 below (toy MLP, 14 tiles per CU: pair
+// 115.9 vs 120.4 us; profiles/r3_wsgd).
+static inline int stream_waves(long long ntiles, int num_cus) {
+  static const int forced = [] {
+    const char* e = getenv("DDPX_WSGD_STREAM_WAVES");
+    return e && e[0] == '8' ? 8 : (e && e[0] == '4' ? 4 : 0);
   }();
-  return v;
+  if (forced) return forced;
+  return ntiles >= 64LL * num_cus ? 8 : 4;
 }
 // Tile order: DDPX_WSGD_ORDER=n (n fastest, default) | m.
 static inline bool n_order() {
@@ -310,11 +318,12 @@ static inline bool n_order() {
 }
 
 template <int STAGES, bool FP8>
-static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1) {
+static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1,
+                               int nsw) {
   const bool no = n_order();
-  if (dist() == 8) {
-    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+  if (nsw == 8) {
+    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(768), 0, s, p0, p1, nt1, 1);
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(768), 0, s, p0, p1, nt1, 1);
   } else {
     if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
     else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, false>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
@@ -325,12 +334,13 @@ static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t 
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   const bool fp8 = p.sgd.q8 != nullptr;
+  const int nsw = stream_waves(ntiles, num_cus);
   if (stages(ntiles, num_cus) == 4) {
-    if (fp8) launch_dist<4, true>(dim3(grid), s, p, p, 0);
-    else launch_dist<4, false>(dim3(grid), s, p, p, 0);
+    if (fp8) launch_dist<4, true>(dim3(grid), s, p, p, 0, nsw);
+    else launch_dist<4, false>(dim3(grid), s, p, p, 0, nsw);
   } else {
-    if (fp8) launch_dist<3, true>(dim3(grid), s, p, p, 0);
-    else launch_dist<3, false>(dim3(grid), s, p, p, 0);
+    if (fp8) launch_dist<3, true>(dim3(grid), s, p, p, 0, nsw);
+    else launch_dist<3, false>(dim3(grid), s, p, p, 0, nsw);
   }
   return hipGetLastError();
 }
@@ -347,12 +357,13 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   if ((p0.sgd.q8 != nullptr) != (p1.sgd.q8 != nullptr)) return hipErrorInvalidValue;  // both or neither
   const bool fp8 = p0.sgd.q8 != nullptr;
+  const int nsw = stream_waves(ntiles, num_cus);
   if (stages(ntiles, num_cus) == 4) {
-    if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1);
-    else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1);
+    if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1, nsw);
+    else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1, nsw);
   } else {
-    if (fp8) launch_dist<3, true>(dim3(grid), s, p0, p1, nt1);
-    else launch_dist<3, false>(dim3(grid), s, p0, p1, nt1);
+    if (fp8) launch_dist<3, true>(dim3(grid), s, p0, p1, nt1, nsw);
+    else launch_dist<3, false>(dim3(grid), s, p0, p1, nt1, nsw);
   }
   return hipGetLastError();
 }
