@@ -300,13 +300,14 @@ static inline int spread() {
 // Stream waves per workgroup: DDPX_WSGD_STREAM_WAVES=4|8 forces it; by default 8 once every CU owns >= 64
 // tiles (wide MLP, ~150 tiles per CU: 2.108 vs 2.175 ms/step) and 4 below (toy MLP, 14 tiles per CU: pair
 // 115.9 vs 120.4 us; profiles/r3_wsgd).
-static inline int stream_waves(long long ntiles, int num_cus) {
+// With the MX-FP8 copy (FP8) 4 stream waves stay faster on the wide MLP too (2.052-2.069 vs 2.072-2.082 ms).
+static inline int stream_waves(long long ntiles, int num_cus, bool fp8) {
   static const int forced = [] {
     const char* e = getenv("DDPX_WSGD_STREAM_WAVES");
     return e && e[0] == '8' ? 8 : (e && e[0] == '4' ? 4 : 0);
   }();
   if (forced) return forced;
-  return ntiles >= 64LL * num_cus ? 8 : 4;
+  return (!fp8 && ntiles >= 64LL * num_cus) ? 8 : 4;
 }
 // Tile order: DDPX_WSGD_ORDER=n (n fastest, default) | m.
 static inline bool n_order() {
@@ -334,7 +335,7 @@ static inline hipError_t launch(const pipe::Params& p, int num_cus, hipStream_t 
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   const bool fp8 = p.sgd.q8 != nullptr;
-  const int nsw = stream_waves(ntiles, num_cus);
+  const int nsw = stream_waves(ntiles, num_cus, fp8);
   if (stages(ntiles, num_cus) == 4) {
     if (fp8) launch_dist<4, true>(dim3(grid), s, p, p, 0, nsw);
     else launch_dist<4, false>(dim3(grid), s, p, p, 0, nsw);
@@ -357,7 +358,7 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   if ((p0.sgd.q8 != nullptr) != (p1.sgd.q8 != nullptr)) return hipErrorInvalidValue;  // both or neither
   const bool fp8 = p0.sgd.q8 != nullptr;
-  const int nsw = stream_waves(ntiles, num_cus);
+  const int nsw = stream_waves(ntiles, num_cus, fp8);
   if (stages(ntiles, num_cus) == 4) {
     if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1, nsw);
     else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1, nsw);
