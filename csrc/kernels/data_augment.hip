@@ -16,6 +16,15 @@ namespace ddpx {
 enum OutLayout : int { OUT_NCHW_F32 = 0, OUT_NCHW_BF16 = 1, OUT_NHWC_BF16 = 2, OUT_NHWC_F32 = 3, OUT_NHWC8_BF16 = 4,
                        OUT_NHWC4_F32 = 5 };
 
+// x mod m for a small m (the crop range 2 * pad + 1) with 32-bit operations only: x = hi * 2^32 + lo, so
+// x mod m = ((hi mod m) * (2^32 mod m) + lo mod m) mod m — exactly the 64-bit remainder the CPU twin takes.
+__device__ __forceinline__ unsigned mod64(uint64_t x, int m) {
+  const unsigned um = (unsigned)m;
+  const unsigned p32 = (0xFFFFFFFFu % um + 1u) % um;
+  const unsigned hi = (unsigned)(x >> 32) % um, lo = (unsigned)x % um;
+  return (hi * p32 + lo) % um;  // < m * m + m: no overflow for the small m used here (m < 65536)
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -52,8 +61,8 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
   int dy = pad, dx = pad, flip = 0;
   if (train) {
     const uint64_t r = splitmix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(b + 1)));
-    dy = (int)(r % (uint64_t)(2 * pad + 1));
-    dx = (int)((r >> 16) % (uint64_t)(2 * pad + 1));
+    dy = (int)mod64(r, 2 * pad + 1);
+    dx = (int)mod64(r >> 16, 2 * pad + 1);
     flip = (int)((r >> 40) & 1);
   }
   if (tgt_out && y == 0 && c == 0 && xg == 0 && xo == 0) tgt_out[b] = labels[src];
@@ -64,12 +73,29 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
   if (!nhwc) {
     const uint8_t* row = img + (size_t)c * H * W + (size_t)(row_ok ? sy : 0) * W;
     float v[8];
+    if (W == 32 && (((uintptr_t)row) & 15) == 0) {
+      // CIFAR rows: the whole 32-B source row in two 16-B loads (2 address operations per lane instead of 8
+      // byte loads), bytes picked in registers
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(row), hi = *reinterpret_cast<const u32x4*>(row + 16);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ox = xg * 8 + j;                 // output column
-      const int x = flip ? (W - 1 - ox) : ox;    // column of the cropped image
-      const int sx = x + dx - pad;
-      v[j] = (row_ok && sx >= 0 && sx < W) ? (float)row[sx] * inv : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int ox = xg * 8 + j;
+        const int x = flip ? (W - 1 - ox) : ox;
+        const int sx = x + dx - pad;
+        const int d = (sx >> 2) & 7;
+        const unsigned w = d < 4 ? (d < 2 ? (d == 0 ? lo[0] : lo[1]) : (d == 2 ? lo[2] : lo[3]))
+                                 : (d < 6 ? (d == 4 ? hi[0] : hi[1]) : (d == 6 ? hi[2] : hi[3]));
+        const unsigned byte = (w >> (8 * (sx & 3))) & 0xFFu;
+        v[j] = (row_ok && sx >= 0 && sx < W) ? (float)byte * inv : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ox = xg * 8 + j;                 // output column
+        const int x = flip ? (W - 1 - ox) : ox;    // column of the cropped image
+        const int sx = x + dx - pad;
+        v[j] = (row_ok && sx >= 0 && sx < W) ? (float)row[sx] * inv : 0.f;
+      }
     }
     const size_t o = (((size_t)b * C + c) * H + y) * W + xg * 8;
     if (layout == OUT_NCHW_BF16) {
@@ -138,6 +164,7 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
                           hipStream_t s) {
   if (B <= 0) return 0;
   if (W % 8) return -1;
+  if (pad < 0 || pad > 4096) return -4;  // mod64's 32-bit arithmetic assumes a small crop range
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
                      layout == OUT_NHWC4_F32);
   if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
@@ -154,6 +181,7 @@ DDPX_API int ddpx_augment_cursor(const void* images, const int64_t* labels, cons
                                  int64_t* tgt_out, const int* cursor, hipStream_t s) {
   if (B <= 0 || nbatch <= 0 || !cursor) return -3;
   if (W % 8) return -1;
+  if (pad < 0 || pad > 4096) return -4;  // mod64's 32-bit arithmetic assumes a small crop range
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
                      layout == OUT_NHWC4_F32);
   if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
