@@ -8,12 +8,13 @@
 // each tile's MFMA main loop: both halves serialised and the fused kernels (toy MLP fc1 / fc0: 97 / 78 us,
 // profiles/r2_head) were no faster than a stored fp32 gradient plus one flat SGD pass.
 //
-// Here every workgroup (one per CU, 8 waves) owns a list of 64x128 tiles and splits its waves by role:
+// Here every workgroup (one per CU, 4 + NSW waves) owns a list of 64x128 tiles (n-fastest over W, so the tiles
+// in flight on the chip cover whole rows of W) and splits its waves by role:
 //   * waves 0-3 (math): the LDS-DMA ring + v_mfma_f32_16x16x32_bf16 main loop of tile i (the pipe core of
 //     ddpx_pipe.h), then its fp32 accumulators into one of two LDS tile buffers;
-//   * waves 4-7 (stream): the optimizer update of tile i-1 from the other buffer — master / momentum loads
-//     for tile i issued one iteration ahead, non-temporal, and the update spread over the K-steps —
-//     so a CU's HBM stream runs while its matrix cores work on the next tile.
+//   * waves 4.. (stream, NSW = 4 or 8): the optimizer update of tile i-1 from the other buffer, spread over
+//     the K-steps, master / momentum loads a 4-vector ring ahead (non-temporal, counted vmcnt waits) — so a
+//     CU's HBM stream runs while its matrix cores work on the next tile.
 // Both roles execute exactly nk + 1 s_barriers per iteration (nk K-steps of 64, then the buffer hand-off)
 // for nt + 1 iterations (one drain iteration), so the barrier sequence matches by construction.
 // The update arithmetic is sgd_apply's fma sequence: bitwise equal to the stored-gradient + flat-SGD path.
@@ -47,7 +48,7 @@ struct Cfg {
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
 template <int STAGES, bool FP8, int NSW, bool NORD>
-__global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1, int /*spread: unused*/) {
+__global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
   constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
@@ -286,17 +287,6 @@ static inline int stages(long long ntiles = 0, int num_cus = 256) {
   return ntiles >= 64LL * num_cus ? 4 : 3;
 }
 
-// DDPX_WSGD_SPREAD=s: the stream waves update each tile in the first ceil(nk / s) K-steps (default 1: one
-// share per K-step; front-loading measured slower, profiles/r2_spread)
-static inline int spread() {
-  static const int v = [] {
-    const char* e = getenv("DDPX_WSGD_SPREAD");
-    const int x = e ? atoi(e) : 1;
-    return x >= 1 ? x : 1;
-  }();
-  return v;
-}
-
 // Stream waves per workgroup: DDPX_WSGD_STREAM_WAVES=4|8 forces it; by default 8 once every CU owns >= 64
 // tiles (wide MLP, ~150 tiles per CU: 2.108 vs 2.175 ms/step) and 4 below (toy MLP, 14 tiles per CU: pair
 // 115.9 vs 120.4 us; profiles/r3_wsgd).
@@ -323,11 +313,11 @@ static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0,
                                int nsw) {
   const bool no = n_order();
   if (nsw == 8) {
-    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(768), 0, s, p0, p1, nt1, 1);
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(768), 0, s, p0, p1, nt1, 1);
+    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(768), 0, s, p0, p1, nt1);
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(768), 0, s, p0, p1, nt1);
   } else {
-    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
-    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, false>), grid, dim3(512), 0, s, p0, p1, nt1, 1);
+    if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true>), grid, dim3(512), 0, s, p0, p1, nt1);
+    else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, false>), grid, dim3(512), 0, s, p0, p1, nt1);
   }
 }
 
