@@ -558,6 +558,44 @@ __global__ void __launch_bounds__(256) head_logits_kernel(const float* __restric
   }
 }
 
+// The reference's 10-class head: one workgroup per row, the row's K / 4 vectors split over 256 threads with
+// every load issued before the FMAs, then a wave + workgroup reduction in fixed order.  (One wave per row
+// walking 16 dependent K-steps ran 63 us at M = 512, K = 4096: profiles/r3_models.)
+template <int NC>
+__global__ void __launch_bounds__(256) head_logits_row_kernel(const float* __restrict__ h, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, int K,
+                                                              float* __restrict__ logits) {
+  __shared__ float red[4][NC];
+  const int m = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int K4 = K / 4;
+  float acc[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j] = 0.f;
+  const f32x4* hp = reinterpret_cast<const f32x4*>(h + (size_t)m * K);
+  for (int k0 = tid; k0 < K4; k0 += 4 * 256) {
+    f32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = k0 + u * 256 < K4 ? hp[k0 + u * 256] : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const f32x4* wp = reinterpret_cast<const f32x4*>(w + (size_t)j * K);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 y = k0 + u * 256 < K4 ? wp[k0 + u * 256] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        acc[j] = fmaf(x[u][0], y[0], fmaf(x[u][1], y[1], fmaf(x[u][2], y[2], fmaf(x[u][3], y[3], acc[j]))));
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) red[wv][j] = v;
+  }
+  __syncthreads();
+  if (tid < NC) logits[(size_t)m * NC + tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + bias[tid];
+}
+
 // One workgroup: per-row log-softmax, loss = mean_m (lse - logit[target]), dl = (softmax - onehot) / M.
 __global__ void __launch_bounds__(1024) xent_kernel(const float* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                      int M, int NC, float* __restrict__ loss,
@@ -589,6 +627,7 @@ __global__ void __launch_bounds__(1024) xent_kernel(const float* __restrict__ lo
 // dW[j][k] (+)= go * sum_m dl[m][j] h[m][k];  db[j] (+)= go * sum_m dl[m][j]
 // Workgroups of 64 columns k x 16 row groups (h read once, coalesced; all NC classes per thread), fixed-order
 // LDS reduction over the row groups; the last workgroup also sums db (one wave per class).
+constexpr int kHeadDlLds = 8192;  // floats of dlogits staged in LDS (M * NC; 512 x 10 at the reference's batch)
 __global__ void __launch_bounds__(1024) head_wgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
                                                            const float* __restrict__ h, int M, int K, int NC,
                                                            float* __restrict__ dW, float* __restrict__ db,
@@ -609,15 +648,40 @@ __global__ void __launch_bounds__(1024) head_wgrad_kernel(const float* __restric
   float acc[kMaxNC];
 #pragma unroll
   for (int j = 0; j < kMaxNC; ++j) acc[j] = 0.f;
-  if (k < K)
-    for (int m = g; m < M; m += 16) {
+  // dlogits staged in LDS once per workgroup (every wave reads every row of it: broadcast LDS reads instead of
+  // 10 global loads per row per lane)
+  __shared__ float dls[kHeadDlLds];
+  auto rows = [&](const auto* dsrc) {
+    // 8 rows' loads in flight per thread (a dependent load per row was latency bound: 35 us at M = 512)
+    int m = g;
+    for (; m + 7 * 16 < M; m += 8 * 16) {
+      float hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv[u] = h[(size_t)(m + u * 16) * K + k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < kMaxNC; ++j) {
+          if (j >= NC) break;
+          acc[j] = fmaf(dsrc[(size_t)(m + u * 16) * NC + j], hv[u], acc[j]);
+        }
+    }
+    for (; m < M; m += 16) {
       const float hv = h[(size_t)m * K + k];
 #pragma unroll
       for (int j = 0; j < kMaxNC; ++j) {
         if (j >= NC) break;
-        acc[j] = fmaf(dl[(size_t)m * NC + j], hv, acc[j]);
+        acc[j] = fmaf(dsrc[(size_t)m * NC + j], hv, acc[j]);
       }
     }
+  };
+  if (M * NC <= kHeadDlLds) {
+    for (int i = threadIdx.x; i < M * NC; i += 1024) dls[i] = dl[i];
+    __syncthreads();
+    if (k < K) rows(dls);
+  } else if (k < K) {
+    rows(dl);
+  }
 #pragma unroll
   for (int j = 0; j < kMaxNC; ++j) red[g][j][cl] = acc[j];
   __syncthreads();
@@ -652,8 +716,18 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + cl;
   float acc = 0.f;
-  if (n < N)
-    for (int m = g; m < M; m += 16) acc += x[(size_t)m * N + n];
+  if (n < N) {
+    // 8 rows' loads in flight, summed in the same row order as one at a time (bitwise unchanged)
+    int m = g;
+    for (; m + 7 * 16 < M; m += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[(size_t)(m + u * 16) * N + n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; m < M; m += 16) acc += x[(size_t)m * N + n];
+  }
   red[g][cl] = acc;
   __syncthreads();
   if (g == 0 && n < N) {
@@ -804,7 +878,10 @@ DDPX_API int ddpx_f32_head_fwd(const float* h, const float* w, const float* bias
                                int NC, float* logits, float* loss, float* dl, hipStream_t s) {
   if (K % 4) return -1;
   if (NC > kMaxNC) return -2;
-  hipLaunchKernelGGL(head_logits_kernel, dim3(nblk(M, 4)), dim3(256), 0, s, h, w, bias, M, K, NC, logits);
+  if (NC == 10 && K % 4 == 0)
+    hipLaunchKernelGGL(head_logits_row_kernel<10>, dim3(M), dim3(256), 0, s, h, w, bias, K, logits);
+  else
+    hipLaunchKernelGGL(head_logits_kernel, dim3(nblk(M, 4)), dim3(256), 0, s, h, w, bias, M, K, NC, logits);
   if (tgt) hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(1024), 0, s, logits, tgt, M, NC, loss, dl);
   return (int)hipGetLastError();
 }
