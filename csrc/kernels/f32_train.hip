@@ -709,6 +709,33 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const float* __restrict
   dh[i] = acc;
 }
 
+// Same as head_dgrad_kernel with 4 consecutive columns per thread (16-B loads / stores of w, h, dh); the sum over
+// the classes runs in the same order, so the result is bitwise that of the scalar kernel.
+__global__ void __launch_bounds__(256) head_dgrad4_kernel(const float* __restrict__ dl, const float* __restrict__ go,
+                                                           const float* __restrict__ w, const float* __restrict__ h,
+                                                           int M, int K, int NC, int relu_mask,
+                                                           float* __restrict__ dh) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+  const int K4 = K / 4;
+  if (i4 >= (long)M * K4) return;
+  const int m = (int)(i4 / K4), k4 = (int)(i4 % K4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NC; ++j) {
+    const float d = dl[(size_t)m * NC + j];
+    const f32x4 wv = reinterpret_cast<const f32x4*>(w + (size_t)j * K)[k4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = fmaf(d, wv[q], acc[q]);
+  }
+  const float g = go ? *go : 1.f;
+  const f32x4 hv = reinterpret_cast<const f32x4*>(h + (size_t)m * K)[k4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc[q] *= g;
+    if (relu_mask && !(hv[q] > 0.f)) acc[q] = 0.f;
+  }
+  reinterpret_cast<f32x4*>(dh + (size_t)m * K)[k4] = acc;
+}
+
 // out[n] (+)= sum_m x[m][n]: workgroups of 64 columns x 16 row groups, fixed-order LDS reduction
 __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ x, int M, int N,
                                                        float* __restrict__ out, int accumulate) {
@@ -891,8 +918,12 @@ DDPX_API int ddpx_f32_head_bwd(const float* dl, const float* go, const float* h,
   if (NC > kMaxNC) return -2;
   if (dW) hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk(K, 64) + 1), dim3(1024), 0, s, dl, go, h, M, K, NC, dW, db,
                              accumulate);
-  if (dh) hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
-                             relu_mask, dh);
+  if (dh && K % 4 == 0 && !(((uintptr_t)w | (uintptr_t)h | (uintptr_t)dh) & 15))
+    hipLaunchKernelGGL(head_dgrad4_kernel, dim3(nblk((long)M * (K / 4))), dim3(256), 0, s, dl, go, w, h, M, K, NC,
+                       relu_mask, dh);
+  else if (dh)
+    hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
+                       relu_mask, dh);
   return (int)hipGetLastError();
 }
 
