@@ -16,13 +16,15 @@ Weak scaling: per-GPU batch fixed as N grows.
     python bench.py --device cpu [--gpus 2]      # BASELINE config 1 (CPU, gloo for N > 1)
 
 N > 1 averages fp32 gradients across ranks bucket by bucket while backward runs (reference
-``multigpu.py:89``).  Before the first step the gradient-communication plan is calibrated on the node's own
-links (``ddpx.parallel.calibrate``; ``--bucket_plan default`` skips it): the collective sequence of every
-candidate — fp32 all-reduce per bucket with torch's greedy size rule at several caps (replicated optimizer,
-stock DDP), or fp32 reduce-scatter + bf16 shadow all-gather per bucket (ZeRO-1: same fp32 gradients and
-update, 0.75x the bytes, 1/N of the optimizer stream per rank) — is timed and rank 0's choice is used by
-every rank; the line reports the plan and every timing (``bucket_plan``, ``calibration``).  bf16 gradient
-communication (``--grad_dtype bf16``) is opt-in only.
+``multigpu.py:89``).  Before the first step the gradient-communication plan is calibrated on the node
+(``ddpx.parallel.calibrate``; ``--bucket_plan default`` skips it): every candidate — fp32 all-reduce per
+bucket with torch's greedy size rule at several caps (replicated optimizer, stock DDP), or fp32
+reduce-scatter + bf16 shadow all-gather per bucket (ZeRO-1: same fp32 gradients and update, 0.75x the
+bytes, 1/N of the optimizer stream per rank) — is built for real and a few graph-captured TRAINING STEPS of
+it are timed (the max over ranks), so the choice accounts for overlap with backward and for the optimizer;
+the line reports the plan and every timing (``bucket_plan``, ``calibration``).  bf16 gradient communication
+(``--grad_dtype bf16``) is opt-in only.  ``--ddp_single`` runs the same machinery (calibration, RCCL reducer,
+digest; ``--stock_ddp 1``: the stock torch-DDP baseline) at world size 1.
 
 Every timed step does the whole job: batch gather+augment, forward, loss, backward, bucketed gradient
 communication (N > 1), optimizer step and LR update.  The step is captured in a HIP graph; if capture fails
@@ -113,6 +115,9 @@ def parse(argv=None):
                    help="1: also time the stock PyTorch recipe (torch.nn + torch DDP over RCCL at N > 1) in this "
                         "job, after the ddpx timing, on the same data (default 1)")
     p.add_argument("--stock_steps", type=int, default=30)
+    p.add_argument("--stock_ddp", type=int, default=0,
+                   help="1: wrap the stock recipe in torch DDP over its own RCCL group even at world size 1 "
+                        "(a rehearsal of the N > 1 baseline path; with --ddp_single)")
     p.add_argument("--digest", type=int, default=0,
                    help="1: report a SHA-256 of this rank's fp32 master weights + optimizer state after the timed "
                         "steps (``master_digest``; tests compare schedules for bitwise-identical training)")
@@ -233,7 +238,8 @@ def resolve_defaults(args, world):
     if args.overlap_optimizer is None:
         args.overlap_optimizer = int(multi)
     # N > 1 ddpx: bucket caps and replicated-vs-ZeRO-1 come from the start-up calibration unless given
-    args.calibrate = bool(world > 1 and args.impl == "ddpx" and args.bucket_plan == "calibrated"
+    # (--ddp_single: the same calibration at world size 1 on the real communicator, a rehearsal of the N > 1 path)
+    args.calibrate = bool((world > 1 or args.ddp_single) and args.impl == "ddpx" and args.bucket_plan == "calibrated"
                           and (args.shard_optimizer is None or args.bucket_cap_mb is None
                                or args.first_bucket_mb is None))
     if args.shard_optimizer is None and not args.calibrate:
@@ -242,6 +248,7 @@ def resolve_defaults(args, world):
         args.bucket_cap_mb = 25.0
     if args.first_bucket_mb is None and not args.calibrate:
         args.first_bucket_mb = 1.0
+    args.chunk_explicit = args.chunk_mb is not None
     if args.chunk_mb is None:
         args.chunk_mb = 0.0
     if args.fused_optimizer is None:
@@ -252,7 +259,8 @@ def resolve_defaults(args, world):
         args.fused_optimizer = 0
     resolve_zero_defaults(args)
     if args.stock_ref is None:
-        args.stock_ref = int(args.impl == "ddpx" and not args.ddp_single and args.comm == "rccl")
+        args.stock_ref = int(args.impl == "ddpx" and (not args.ddp_single or bool(args.stock_ddp))
+                             and args.comm == "rccl")
     if args.stock_first is None:
         # measured (profiles/r3_val): stock-first gives the stock recipe a cold GPU (0.88-0.90 vs 0.62-0.73 ms) and
         # ddpx no clear gain, so the baseline runs last unless asked
@@ -269,12 +277,22 @@ def resolve_zero_defaults(args):
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 
 
-def build_ddpx(args, device, world):
+def make_comm(args, device, world):
+    """The gradient communicator of the ddpx engine (None for a single process without ``--ddp_single``): one per
+    job, shared by the calibration trials and the timed run."""
+    if not (world > 1 or args.ddp_single) or args.impl != "ddpx":
+        return None
+    from ddpx.parallel.comm import HostStagedComm, RcclComm, TorchComm
+    if device.type == "cpu":
+        return TorchComm()
+    return HostStagedComm() if args.comm == "host" else RcclComm(device)
+
+
+def build_ddpx(args, device, world, comm=None):
     import torch
     from ddpx.models import build_model
     from ddpx.optim.schedule import one_cycle, resolve_steps_per_epoch
     from ddpx.optim.sgd import SGD
-    from ddpx.parallel.comm import HostStagedComm, RcclComm, TorchComm
     from ddpx.parallel.ddp import DistributedDataParallel
     from ddpx.runtime.setup import prepare_model
     torch.manual_seed(args.seed)
@@ -288,28 +306,7 @@ def build_ddpx(args, device, world):
               capturable=not (args.no_graph or cpu),
               fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not fp32))
     net = model
-    if world > 1 or args.ddp_single:
-        if cpu:
-            comm = TorchComm()
-        else:
-            comm = HostStagedComm() if args.comm == "host" else RcclComm(device)
-        if getattr(args, "calibrate", False):
-            from ddpx.parallel.calibrate import calibrate
-            from ddpx.runtime.flat_params import flat_of
-            f = flat_of(model)
-            shadow_only = [id(p) in f.shadow_only for p in f.params]
-            allow = (args.shard_optimizer is None and f.shadow is not None and any(shadow_only)
-                     and args.comm == "rccl")
-            plan, table = calibrate(comm, list(f.numels), shadow_only, device, allow_shard=allow,
-                                    reps=1 if cpu else 3)
-            if args.shard_optimizer is None:
-                args.shard_optimizer = int(plan["shard"])
-            if args.bucket_cap_mb is None:
-                args.bucket_cap_mb = plan["bucket_cap_mb"]
-            if args.first_bucket_mb is None:
-                args.first_bucket_mb = plan["first_bucket_mb"]
-            args.calibration = {"chosen": plan["name"], "ms": table}
-            resolve_zero_defaults(args)
+    if comm is not None:
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
                                       reduce_single=args.ddp_single,
                                       first_bucket_mb=args.first_bucket_mb,
@@ -345,7 +342,7 @@ def build_torch(args, device, world, group=None):
                 layers.append(nn.ReLU())
         model = nn.Sequential(nn.Flatten(), *layers).to(device)
     net = (TDDP(model, device_ids=[device.index] if device.type == "cuda" else None, process_group=group)
-           if world > 1 else model)
+           if (world > 1 or group is not None) else model)
     opt = torch.optim.SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, OneCycleLambda(resolve_steps_per_epoch("compat", 0, world > 1)))
     return model, net, opt, sched
@@ -380,95 +377,22 @@ def torch_runner(args, device, world, loader, idx_all, full, group=None):
     return model, net, opt, sched, run
 
 
-def measure_stock_same_run(args, device, world, rank, idx_all, full):
-    """The stock PyTorch-ROCm recipe timed in this job (after the ddpx timing unless --stock_first 1), on the
-    same data:
-    torch.nn model + bf16 autocast (fp32 when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its
-    own RCCL process group (the reference's ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same
-    timing rule as the ddpx line: barrier + synchronize on both sides, max over ranks.  Collective."""
+def make_runner(args, device, world, loader, idx_all, full, comm=None):
+    """The engine under test and ``run(k, n)`` for its steps k .. k+n-1 (returns the last loss).
+
+    ddpx on the GPU: every step (batch gather + augment from a device cursor, forward, backward with the
+    bucketed collectives, optimizer, LR) is captured in a HIP graph after two eager steps and replayed; if
+    capture fails on any rank every rank continues eagerly.  ddpx on the CPU and ``--impl torch``: eager steps.
+    Used for the timed run and for each start-up calibration trial (``comm`` is the job's communicator)."""
     import torch
     import torch.distributed as dist
-    a = argparse.Namespace(**vars(args))
-    a.impl, a.torch_amp = "torch", args.dtype != "fp32"
-    cuda = device.type == "cuda"
-    loader = make_data(a, device, rank, world)  # the stock model's own (NCHW / flat fp32) input layout
-    group = dist.new_group(backend="nccl" if cuda else "gloo") if world > 1 else None
-    _, _, _, _, run = torch_runner(a, device, world, loader, idx_all, full, group=group)
-
-    def sync():
-        if cuda:
-            torch.cuda.synchronize()
-
-    run(0, 5)
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    run(5, args.stock_steps)
-    sync()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        dist.destroy_process_group(group)
-    dt /= args.stock_steps
-    recipe = "torch.nn + " + ("fp32" if args.dtype == "fp32" or not cuda else "bf16 autocast") + " + foreach SGD"
-    if world > 1:
-        recipe += " + torch DDP (" + ("RCCL" if cuda else "gloo") + ", 25/1 MiB buckets)"
-    return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(world * args.batch_size / dt, 2),
-            "recipe": recipe, "steps": args.stock_steps}
-
-
-def replica_digest(net, flat=None):
-    """SHA-256 of this rank's fp32 master weights and optimizer state, byte for byte (after consolidate)."""
-    import hashlib
-    f = flat if flat is not None else net.flat
-    h = hashlib.sha256()
-    for t in [f.master] + [f.state_tensors[k] for k in sorted(f.state_tensors)]:
-        h.update(t.detach().cpu().contiguous().numpy().tobytes())
-    return h.hexdigest()
-
-
-def main(argv=None):
-    argv = sys.argv[1:] if argv is None else argv
-    args = parse(argv)
-    if needs_self_launch(args):
-        sys.exit(self_launch(args, argv))
-
-    import torch
-    import torch.distributed as dist
-
-    rank, world, local = setup_dist(args)
-    resolve_defaults(args, world)
-    cpu = args.device == "cpu"
-    if args.comm == "host" or cpu:
-        args.no_graph = True
-    from ddpx.models import native_kernels_for
-    if args.impl == "ddpx" and not native_kernels_for(args.model, "fp32" if args.dtype == "fp32" else "bf16",
-                                                      args.kernels):
-        # torch ops under the ddpx engine (VGG at fp32: MIOpen convolutions) run eagerly: capturing torch's
-        # autograd with AccumulateGrad nodes made by the eager warm-up steps crashed the process (exit -11);
-        # a ~20 ms step does not need the graph's launch savings
-        args.no_graph = True
-    device = torch.device("cpu") if cpu else torch.device("cuda", local)
-    loader = make_data(args, device, rank, world)
-    idx_all = loader._epoch_indices()
-    nb = len(loader)
-    full = [i for i in range(nb) if (i + 1) * args.batch_size <= idx_all.numel()]
+    cpu = device.type == "cpu"
     bs = args.batch_size
-
-    def sync():
-        if not cpu:
-            torch.cuda.synchronize()
-
-    net = model = None
     runner = None
     if args.impl == "ddpx" and not cpu:
-        from ddpx.runtime.graphs import CapturedStep, GraphedSteps
-        model, net, opt, sched = build_ddpx(args, device, world)
+        from ddpx.runtime.graphs import (CapturedStep, GraphedSteps, agree_all_ranks, restore_after_failed_capture,
+                                         step_state_snapshot)
+        model, net, opt, sched = build_ddpx(args, device, world, comm)
         static_x, static_y = loader.make_batch(idx_all[:bs], 0)
 
         # the LR schedule lives on the device: the captured step advances it (no per-step host write)
@@ -546,8 +470,7 @@ def main(argv=None):
 
         def make_graphs():
             # host-side step state a failed capture could leave half-done (restored by the fallback)
-            snap["ddp"] = net.iteration_state() if hasattr(net, "iteration_state") else None
-            snap["step_count"] = opt.step_count
+            snap.update(step_state_snapshot(net, opt))
             if prefetch:
                 gp = [CapturedStep(lambda x, y, par=par: pf_body(par), static_x, static_y, use_inputs_as_static=True,
                                    comm=comm_obj) for par in (0, 1)]
@@ -565,22 +488,11 @@ def main(argv=None):
         def fallback():
             # nothing of the aborted capture ran on the device: put the host bookkeeping back to where the
             # last eager step left it and continue eagerly (same process, same communicator)
-            torch.cuda.synchronize()
-            if snap.get("ddp") is not None:
-                net.restore_iteration_state(snap["ddp"])
-            opt.flat.pending_lr = None
-            opt.step_count = snap.get("step_count", opt.step_count)
-
-        def agree(ok):
-            if world == 1:
-                return ok
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)  # gloo group: CPU tensors
-            return bool(t.item())
+            restore_after_failed_capture(net, opt, snap)
 
         runner = GraphedSteps(pf_eager if prefetch else (lambda: step_body(static_x, static_y)), make_graphs,
                               steps_per_graph=S,
-                              use_graph=use_graph, agree=agree, on_fallback=fallback,
+                              use_graph=use_graph, agree=agree_all_ranks, on_fallback=fallback,
                               after=lambda m: [sched.step() for _ in range(m)])
 
         def run(k, n):
@@ -588,7 +500,7 @@ def main(argv=None):
             S-step graph and of a 1-step graph for the remainder (eager if capture failed on any rank)."""
             return runner.run(k, n)
     elif args.impl == "ddpx":  # CPU: the ddpx engine (flat store, flat SGD, DDP over gloo) on torch CPU kernels
-        model, net, opt, sched = build_ddpx(args, device, world)
+        model, net, opt, sched = build_ddpx(args, device, world, comm)
 
         def one_step(k):
             b = full[k % len(full)]
@@ -607,6 +519,179 @@ def main(argv=None):
             return loss
     else:
         model, net, opt, sched, run = torch_runner(args, device, world, loader, idx_all, full)
+
+    def close():
+        """Release this engine's reducer and captured graphs (not the shared communicator)."""
+        if runner is not None:
+            runner.graphs = None
+        if net is not model and hasattr(net, "close"):
+            net.close()
+
+    return argparse.Namespace(model=model, net=net, opt=opt, sched=sched, run=run, runner=runner,
+                              close=close)
+
+
+
+def calibrate_plan(args, device, world, loader, idx_all, full, comm):
+    """Start-up calibration (``ddpx.parallel.calibrate``): build every candidate gradient-communication plan for
+    real (its own model copy, DDP buckets and optimizer, graph-captured like the timed run), time a few
+    training steps of each, and set ``args``' bucket caps / ZeRO-1 choice to the fastest.  Collective."""
+    import gc
+
+    import torch
+    from ddpx.models import build_model
+    from ddpx.parallel.calibrate import calibrate_by_step, candidate_plans
+    from ddpx.runtime.flat_params import flat_of
+    from ddpx.runtime.setup import prepare_model
+    cpu = device.type == "cpu"
+    fp32 = cpu or args.dtype == "fp32"
+    probe = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype="fp32" if fp32 else "bf16",
+                        device=device, fp8=bool(args.fp8), kernels=args.kernels)
+    prepare_model(probe, device)
+    f = flat_of(probe)
+    numels = list(f.numels)
+    shapes = [tuple(p.shape) for p in f.params]
+    shadow_only = [id(p) in f.shadow_only for p in f.params]
+    del probe, f
+    allow = args.shard_optimizer is None and any(shadow_only) and args.comm == "rccl" and not cpu
+    plans = candidate_plans(numels, shadow_only, max(world, 2) if args.ddp_single else world, allow_shard=allow,
+                            shapes=None if args.chunk_explicit else shapes)
+    if args.shard_optimizer is not None:
+        plans = [p for p in plans if p["shard"] == bool(args.shard_optimizer)]
+    if args.bucket_cap_mb is not None or args.first_bucket_mb is not None:
+        plans = [dict(p, bucket_cap_mb=args.bucket_cap_mb if args.bucket_cap_mb is not None else p["bucket_cap_mb"],
+                      first_bucket_mb=(args.first_bucket_mb if args.first_bucket_mb is not None
+                                       else p["first_bucket_mb"])) for p in plans]
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
+
+    def apply(a, plan):
+        a.shard_optimizer = int(plan["shard"])
+        a.bucket_cap_mb = plan["bucket_cap_mb"]
+        a.first_bucket_mb = plan["first_bucket_mb"]
+        a.comm_side_optimizer = args.comm_side_optimizer
+        a.defer_gather = args.defer_gather
+        if not args.chunk_explicit:
+            a.chunk_mb = plan.get("chunk_mb") or 0.0
+        resolve_zero_defaults(a)
+
+    def make_trial(plan):
+        a = argparse.Namespace(**vars(args))
+        apply(a, plan)
+        a.calibrate = False
+        eng = make_runner(a, device, world, loader, idx_all, full, comm)
+        k = [0]
+
+        def step():
+            eng.run(k[0], 1)
+            k[0] += 1
+
+        def close():
+            sync()
+            eng.close()
+            eng.runner = eng.run = eng.net = eng.model = eng.opt = eng.sched = None
+            gc.collect()
+            if not cpu:
+                torch.cuda.empty_cache()
+        return step, close
+
+    chosen, table = calibrate_by_step(plans, make_trial, sync=sync, warm=3, reps=3 if cpu else 5,
+                                      rounds=1 if cpu else 3)
+    apply(args, chosen)
+    args.calibration = {"chosen": chosen["name"], "objective": "training step ms (max over ranks)",
+                        "step_ms": table}
+
+
+def measure_stock_same_run(args, device, world, rank, idx_all, full):
+    """The stock PyTorch-ROCm recipe timed in this job (after the ddpx timing unless --stock_first 1), on the
+    same data:
+    torch.nn model + bf16 autocast (fp32 when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its
+    own RCCL process group (the reference's ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same
+    timing rule as the ddpx line: barrier + synchronize on both sides, max over ranks.  Collective."""
+    import torch
+    import torch.distributed as dist
+    a = argparse.Namespace(**vars(args))
+    a.impl, a.torch_amp = "torch", args.dtype != "fp32"
+    cuda = device.type == "cuda"
+    loader = make_data(a, device, rank, world)  # the stock model's own (NCHW / flat fp32) input layout
+    use_ddp = world > 1 or bool(getattr(args, "stock_ddp", 0))
+    group = dist.new_group(backend="nccl" if cuda else "gloo") if use_ddp else None
+    _, _, _, _, run = torch_runner(a, device, world, loader, idx_all, full, group=group)
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    run(0, 5)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run(5, args.stock_steps)
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if group is not None:
+        dist.destroy_process_group(group)
+    dt /= args.stock_steps
+    recipe = "torch.nn + " + ("fp32" if args.dtype == "fp32" or not cuda else "bf16 autocast") + " + foreach SGD"
+    if use_ddp:
+        recipe += " + torch DDP (" + ("RCCL" if cuda else "gloo") + ", 25/1 MiB buckets)"
+    return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(world * args.batch_size / dt, 2),
+            "recipe": recipe, "steps": args.stock_steps}
+
+
+def replica_digest(net, flat=None):
+    """SHA-256 of this rank's fp32 master weights and optimizer state, byte for byte (after consolidate)."""
+    import hashlib
+    f = flat if flat is not None else net.flat
+    h = hashlib.sha256()
+    for t in [f.master] + [f.state_tensors[k] for k in sorted(f.state_tensors)]:
+        h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if needs_self_launch(args):
+        sys.exit(self_launch(args, argv))
+
+    import torch
+    import torch.distributed as dist
+
+    rank, world, local = setup_dist(args)
+    resolve_defaults(args, world)
+    cpu = args.device == "cpu"
+    if args.comm == "host" or cpu:
+        args.no_graph = True
+    from ddpx.models import native_kernels_for
+    if args.impl == "ddpx" and not native_kernels_for(args.model, "fp32" if args.dtype == "fp32" else "bf16",
+                                                      args.kernels):
+        # torch ops under the ddpx engine (VGG at fp32: MIOpen convolutions) run eagerly: capturing torch's
+        # autograd with AccumulateGrad nodes made by the eager warm-up steps crashed the process (exit -11);
+        # a ~20 ms step does not need the graph's launch savings
+        args.no_graph = True
+    device = torch.device("cpu") if cpu else torch.device("cuda", local)
+    loader = make_data(args, device, rank, world)
+    idx_all = loader._epoch_indices()
+    nb = len(loader)
+    full = [i for i in range(nb) if (i + 1) * args.batch_size <= idx_all.numel()]
+    bs = args.batch_size
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    comm = make_comm(args, device, world)
+    if getattr(args, "calibrate", False):
+        calibrate_plan(args, device, world, loader, idx_all, full, comm)
+    eng = make_runner(args, device, world, loader, idx_all, full, comm)
+    model, net, opt, sched, run, runner = eng.model, eng.net, eng.opt, eng.sched, eng.run, eng.runner
 
     stock = None
     if args.stock_ref and args.stock_first:
@@ -647,7 +732,7 @@ def main(argv=None):
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     multi = world > 1 or args.ddp_single
     ddpx_ddp = multi and args.impl == "ddpx"
-    comm = net.comm_stats() if (ddpx_ddp and hasattr(net, "comm_stats")) else None
+    cstats = net.comm_stats() if (ddpx_ddp and hasattr(net, "comm_stats")) else None
     consistent = None
     buckets_mb = None
     if ddpx_ddp:
@@ -715,8 +800,8 @@ def main(argv=None):
                    "final_loss": round(final_loss, 4), "ddp": bool(multi),
                    "replicas_consistent": consistent,
                    "master_digest": digest,
-                   "comm_ms_per_step": round(comm["comm_ms"], 4) if comm else None,
-                   "comm_exposed_ms_per_step": round(comm["comm_exposed_ms"], 4) if comm else None,
+                   "comm_ms_per_step": round(cstats["comm_ms"], 4) if cstats else None,
+                   "comm_exposed_ms_per_step": round(cstats["comm_exposed_ms"], 4) if cstats else None,
                    "stock_same_run": stock,
                    "vs_stock_same_run": (round(value / stock["samples_per_sec"], 4) if stock else None)},
     }
@@ -729,7 +814,8 @@ def main(argv=None):
     if multi:
         if args.impl == "ddpx" and hasattr(net, "close"):
             net.close()
-            net.comm.close()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -36,20 +36,24 @@ constexpr int VPT = BM * BN / 4 / 256;  // f32x4 vectors per stream thread per t
 //   4 stages: one more 24 KiB stage in flight (the math side's K-steps are L2->LDS latency bound with
 //             only 4 DMA-issuing waves), which fits the 160 KiB LDS only with unpadded rows (4-way
 //             conflicts on the once-per-tile accumulator store).
-template <int STAGES>
+template <int STAGES, int XTRA = 0>
 struct Cfg {
   static constexpr int ALD = STAGES >= 4 ? BN : BN + 4;
   static constexpr int ACC_BYTES = BM * ALD * 4;
-  static constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES;
+  static constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES + (XTRA >= 2 ? SLOT : 0);
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
-template <int STAGES, bool FP8, int NSW, bool NORD>
+// XTRA (measurement only, DDPX_WSGD_XTRA): 1 = every K-step runs its MFMAs twice (the second set into a
+// dead accumulator kept live), 2 = also a second operand stage of LDS-DMA per K-step into a dummy ring — the
+// math and L2->LDS load a fused data-gradient GEMM would add beside the weight-gradient tiles.
+template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0>
 __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
-  constexpr int ALD = Cfg<STAGES>::ALD, ACC_BYTES = Cfg<STAGES>::ACC_BYTES, LDS_BYTES = Cfg<STAGES>::LDS_BYTES;
+  constexpr int ALD = Cfg<STAGES, XTRA>::ALD, ACC_BYTES = Cfg<STAGES, XTRA>::ACC_BYTES;
+  constexpr int LDS_BYTES = Cfg<STAGES, XTRA>::LDS_BYTES;
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -107,6 +111,12 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, kt * 64, p.K, wave, lane);
       pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, kt * 64, p.K, wave,
                                                        lane);
+      if constexpr (XTRA >= 2) {  // dummy second stage (same operands, other k rows) into the extra ring
+        char* x = smem + STAGES * SLOT + 2 * ACC_BYTES;  // one dummy slot (its contents are never used)
+        const int kx = ((kt + 3) % (p.K / 64)) * 64;
+        pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, x, p.conv, lda, m0, Mg, kx, p.K, wave, lane);
+        pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, x + A_SUB, p.conv, ldb, n0, Ng, kx, p.K, wave, lane);
+      }
     };
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
@@ -115,17 +125,18 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       if (i == nt) {  // drain iteration: the stream waves finish the last tile
         for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
       } else {
-        f32x4 acc[FM][FN];
+        f32x4 acc[FM][FN], acc2[FM][FN];
 #pragma unroll
         for (int a = 0; a < FM; ++a)
 #pragma unroll
-          for (int b = 0; b < FN; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          for (int b = 0; b < FN; ++b) acc[a][b] = acc2[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
         for (int t = 0; t < nk; ++t) {
           const int g = i * nk + t;
           const int ahead = min(STAGES - 2, G - 1 - g);
+          constexpr int LW = XTRA >= 2 ? 2 * LPW : LPW;
           // stage g landed: everything but the (up to STAGES - 2) younger stages' DMAs
-          if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LPW>();
-          else if (ahead >= 1) pipe::wait_vmcnt<LPW>();
+          if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LW>();
+          else if (ahead >= 1) pipe::wait_vmcnt<LW>();
           else pipe::wait_vmcnt<0>();
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -141,7 +152,23 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
 #pragma unroll
               for (int b = 0; b < FN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+            if constexpr (XTRA >= 1) {
+              const char* xa = XTRA >= 2 ? smem + STAGES * SLOT + 2 * ACC_BYTES : sa;
+              bf16x8 af2[FM], bf2[FN];
+              pipe::load_frags<BM, false, FM, BN, false, FN>(xa, wm * 32, xa + A_SUB, wn * 64, kk, lane, af2, bf2);
+#pragma unroll
+              for (int a = 0; a < FM; ++a)
+#pragma unroll
+                for (int b = 0; b < FN; ++b)
+                  acc2[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af2[a], bf2[b], acc2[a][b], 0, 0, 0);
+            }
           }
+        }
+        if constexpr (XTRA >= 1) {
+#pragma unroll
+          for (int a = 0; a < FM; ++a)
+#pragma unroll
+            for (int b = 0; b < FN; ++b) asm volatile("" ::"v"(acc2[a][b]));
         }
         // accumulators -> tile buffer i&1 (C/D map: row 4*(lane>>4)+r, col lane&15 of each 16x16 block)
         float* T = accb + (i & 1) * (ACC_BYTES / 4);
@@ -281,7 +308,7 @@ static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
 static inline int stages(long long ntiles = 0, int num_cus = 256) {
   static const int forced = [] {
     const char* e = getenv("DDPX_WSGD_STAGES");
-    return e && e[0] == '3' ? 3 : (e && e[0] == '4' ? 4 : 0);
+    return e && e[0] == '2' ? 2 : (e && e[0] == '3' ? 3 : (e && e[0] == '4' ? 4 : 0));
   }();
   if (forced) return forced;
   return ntiles >= 64LL * num_cus ? 4 : 3;
@@ -308,10 +335,24 @@ static inline bool n_order() {
   return v;
 }
 
+static inline int xtra() {
+  static const int v = [] {
+    const char* e = getenv("DDPX_WSGD_XTRA");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int STAGES, bool FP8>
 static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1,
                                int nsw) {
   const bool no = n_order();
+  if constexpr (!FP8 && STAGES == 2) {
+    // measurement variants (DDPX_WSGD_XTRA=1|2, 2-stage ring so the dummy ring fits the LDS)
+    const int x = xtra();
+    if (x == 1) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 1>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
+    if (x == 2) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 2>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
+  }
   if (nsw == 8) {
     if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(768), 0, s, p0, p1, nt1);
     else hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, false>), grid, dim3(768), 0, s, p0, p1, nt1);
@@ -352,6 +393,8 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   if (stages(ntiles, num_cus) == 4) {
     if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1, nsw);
     else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1, nsw);
+  } else if (stages(ntiles, num_cus) == 2 && !fp8) {
+    launch_dist<2, false>(dim3(grid), s, p0, p1, nt1, nsw);
   } else {
     if (fp8) launch_dist<3, true>(dim3(grid), s, p0, p1, nt1, nsw);
     else launch_dist<3, false>(dim3(grid), s, p0, p1, nt1, nsw);

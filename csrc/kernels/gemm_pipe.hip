@@ -232,6 +232,7 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
     return -20;  // 32-bit buffer offsets
   if (!wsgd::eligible(q0, false, false) || !wsgd::eligible(q1, false, false) || !wsgd::pair_compatible(q0, q1))
     return -20;
+  if ((q80 != nullptr) != (q81 != nullptr)) return -20;  // one launch writes both MX-FP8 copies or neither
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)

@@ -46,6 +46,11 @@ struct Pending {
 //   abort  - also ncclCommAbort (serialised against collective issue, see Comm::issue_mu)
 //   exit   - raise, then terminate the process with exit code 3 after a grace period
 //            (DDPX_COMM_EXIT_GRACE_S, default 10 s) unless the owning thread exited first (default)
+// Escalation under raise / abort: an abort that cannot take issue_mu within ~2 s (the owning thread is stuck
+// INSIDE an RCCL call, e.g. an enqueue blocked behind a dead peer) cannot free the communicator safely, and
+// that thread will never return to observe a raised error either; the error state becomes 4 ("stuck in
+// RCCL", readable by any other thread through ddpx_comm_error) and the process ends with exit code 3, as
+// the exit action would (csrc/tests/rt_sanitize.cpp scenario "stuck").
 enum TimeoutAction : int { ACT_RAISE = 0, ACT_ABORT = 1, ACT_EXIT = 2 };
 
 struct Comm {
@@ -63,7 +68,7 @@ struct Comm {
   std::vector<hipEvent_t> free_events;
   std::thread watchdog;
   std::atomic<bool> stop{false};
-  std::atomic<int> error{0};  // 0 ok, 1 async nccl error, 2 timeout, 3 aborted
+  std::atomic<int> error{0};  // 0 ok, 1 async nccl error, 2 timeout, 3 aborted, 4 abort escalated (stuck in RCCL)
   // set by the owning thread (ddpx_comm_set_timeout), read by the watchdog: atomics (a host ThreadSanitizer
   // run of csrc/tests/rt_sanitize.cpp flagged the plain fields as a data race)
   std::atomic<double> timeout_s{0.0};
@@ -87,9 +92,11 @@ void abort_comm(Comm* c) {
     if (!locked) std::this_thread::sleep_for(std::chrono::milliseconds(10));
   }
   if (!locked) {
+    c->error.store(4);
     fprintf(stderr, "[ddpx rank %d] abort: a collective call is stuck inside RCCL; terminating (exit code 3)\n",
             c->rank);
     fflush(stderr);
+    std::this_thread::sleep_for(std::chrono::milliseconds(200));  // other threads' monitors can read code 4
     std::_Exit(3);
   }
   if (!c->aborted.exchange(true) && c->nccl) ncclCommAbort(c->nccl);

@@ -27,6 +27,7 @@
 // ---------------------------------------------------------------------------------------------- fakes
 namespace {
 std::atomic<bool> g_hang{false};
+std::atomic<bool> g_stuck{false};  // the next collective's enqueue never returns (scenario "stuck")
 std::atomic<int> g_violations{0};
 
 struct FakeEvent {
@@ -49,6 +50,7 @@ int collective(ncclComm_t comm) {
   FakeComm* c = reinterpret_cast<FakeComm*>(comm);
   c->in_flight.fetch_add(1);
   if (!c->alive.load()) violation("collective issued on an aborted/destroyed communicator");
+  while (g_stuck.load()) std::this_thread::sleep_for(std::chrono::milliseconds(5));
   std::this_thread::sleep_for(std::chrono::microseconds(50));  // the enqueue takes a while
   if (!c->alive.load()) violation("communicator aborted while a collective was being enqueued");
   c->in_flight.fetch_sub(1);
@@ -264,7 +266,37 @@ static int scenario_destroy_pending() {
   return ddpx_comm_destroy(c, 1) ? fail("destroy") : 0;
 }
 
-int main() {
+// (4) "stuck": the owning thread blocks inside an RCCL enqueue (issue_mu held) while an earlier collective
+// times out under the abort action.  The watchdog cannot abort underneath the call: it must set error 4 and
+// end the process with exit code 3 (checked by the caller: tests/test_runtime_sanitize.py).
+static int scenario_stuck() {
+  setenv("DDPX_COMM_TIMEOUT_ACTION", "abort", 1);
+  char uid[128] = {0};
+  int err = 0;
+  void* c = ddpx_comm_create(uid, 2, 0, 0, 1, 0.2, &err);
+  if (!c) return fail("create");
+  std::vector<float> buf(16);
+  g_hang.store(true);  // this collective's completion event never fires -> timeout after 0.2 s
+  if (ddpx_comm_allreduce(c, buf.data(), buf.data(), buf.size(), (int)ncclFloat32, (int)ncclSum, nullptr))
+    return fail("first allreduce");
+  g_stuck.store(true);
+  std::thread monitor([&] {  // another thread sees the escalation code before the process ends
+    for (;;) {
+      if (ddpx_comm_error(c) == 4) {
+        printf("rt_sanitize: stuck escalation observed\n");
+        fflush(stdout);
+        return;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  });
+  monitor.detach();
+  (void)ddpx_comm_allreduce(c, buf.data(), buf.data(), buf.size(), (int)ncclFloat32, (int)ncclSum, nullptr);
+  return fail("the stuck enqueue returned");  // unreachable: the watchdog ends the process first
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "stuck")) return scenario_stuck();
   int rc = scenario_timeout_abort();
   rc |= scenario_reducer();
   rc |= scenario_destroy_pending();

@@ -147,6 +147,8 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                 # fp8 model (DDPX_FP8_COPY=pair|1, default pair): the stream waves also emit both weights' MX-FP8 copies
                 emit = flat.shadow8 is not None and flat.fp8_from_optimizer
                 mx1, mx0 = (flat.mx8_views(w1), flat.mx8_views(w)) if emit else (None, None)
+                if mx1 is None or mx0 is None:  # both copies or neither (a store without 128-aligned offsets)
+                    mx1 = mx0 = None
                 paired = G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0, mx1, mx0)
                 if not paired:
                     G.linear_wgrad(d1, h1, None, sgd=s1)

@@ -172,6 +172,26 @@ class SGD(Optimizer):
                   g["weight_decay"], nesterov=g["nesterov"], mx8=mx8)
         f.fp8_mark(start, end, mx8 is not None)
 
+    def _stepped(self, ranges):
+        """``ranges`` (flat [start, end) pairs) minus the spans of parameters already stepped or skipped this
+        iteration (``FlatParams.updated``): what the optimizer still has to update."""
+        f = self.flat
+        if not any(f.updated):
+            return list(ranges)
+        holes = [f.span(i, i) for i, u in enumerate(f.updated) if u]
+        out = []
+        for (s, e) in ranges:
+            cur = s
+            for (hs, he) in sorted(holes):
+                if he <= cur or hs >= e:
+                    continue
+                if hs > cur:
+                    out.append((cur, hs))
+                cur = max(cur, he)
+            if cur < e:
+                out.append((cur, e))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -180,7 +200,11 @@ class SGD(Optimizer):
                 loss = closure()
         g = self.param_groups[0]
         if not (self.flat.master.is_cuda and torch.cuda.is_current_stream_capturing()):
-            self.flat.fix_unwritten()
+            # torch.optim.SGD skips a parameter whose .grad is None (no weight decay, no momentum step):
+            # a parameter nobody produced a gradient for this step is marked as already stepped, so every
+            # branch below leaves it alone (DDP's find_unused_parameters path marks the globally unused ones)
+            for i in self.flat.fix_unwritten():
+                self.flat.updated[i] = True
         src = self.bucket_source
         if src is not None and getattr(src, "sharded", False):
             # ZeRO-1: each rank updates only its shard of every sharded bucket (gradients were
@@ -189,7 +213,7 @@ class SGD(Optimizer):
             if side is None:
                 for b in src.bucket_order():
                     src.wait_bucket(b)
-                    for (start, end) in src.update_ranges(b):
+                    for (start, end) in self._stepped(src.update_ranges(b)):
                         self._update(start, end, g, fp8=False)
                     src.gather_bucket(b)
             else:
@@ -203,7 +227,7 @@ class SGD(Optimizer):
                 with torch.cuda.stream(side):
                     for b in src.bucket_order():
                         src.claim_bucket_on_comm_stream(b)
-                        for (start, end) in src.update_ranges(b):
+                        for (start, end) in self._stepped(src.update_ranges(b)):
                             self._update(start, end, g, fp8=False)
                         src.gather_bucket(b)
                 done = torch.cuda.Event()

@@ -262,7 +262,10 @@ class RcclComm(Comm):
         e = self._rt.ddpx_comm_error(self.handle)
         if e:
             raise CommError(f"[rank {self.rank}] " + {1: "RCCL asynchronous error", 2: "RCCL collective timed out",
-                                                      3: "RCCL communicator aborted"}.get(e, f"RCCL error {e}"))
+                                                      3: "RCCL communicator aborted",
+                                                      4: "RCCL abort escalated: a collective call is stuck inside "
+                                                         "RCCL, the process exits with code 3"
+                                                      }.get(e, f"RCCL error {e}"))
 
     def track(self, stream=None, what: str = "graph replay"):
         """Register everything enqueued on ``stream`` so far with the watchdog (call after each graph

@@ -181,10 +181,18 @@ class FlatParams:
             return None
         return self.shadow8[start:end], self.scale8[start // 32:end // 32]
 
-    def refresh_shadow(self):
+    def invalidate_derived(self):
+        """Treat every derived copy of the weights as stale: the MX-FP8 copy and any consumer-held layout keyed
+        by :meth:`version_of` (the VGG path's bf16 conv layouts) are re-derived by their next reader.
+
+        For host bookkeeping that ran without its device work, e.g. a HIP-graph capture that aborted after the
+        forward had recorded a weight re-layout or quantisation (and marked it current) that never executed."""
         self.fp8_fresh = [False] * len(self.params)
-        # every parameter moves past any version a consumer may hold (also across a relayout's re-indexing)
+        # every parameter moves past any version a consumer may hold
         self.version = [max(self.version, default=0) + 1] * len(self.params)
+
+    def refresh_shadow(self):
+        self.invalidate_derived()  # (also across a relayout's re-indexing)
         if self.shadow is None:
             return
         from ..ops.elementwise import cast_bf16_
@@ -361,7 +369,8 @@ class FlatParams:
         if missing:
             if not self._warned_unused:
                 names = [self.names.get(id(self.params[i]), str(i)) for i in missing]
-                warnings.warn(f"ddpx: parameters without gradient this step (zeroed): {names}")
+                warnings.warn(f"ddpx: parameters without gradient this step (gradient zeroed; the optimizer "
+                              f"does not step them, as torch.optim.SGD skips grad=None): {names}")
                 self._warned_unused = True
             for i in missing:
                 self.grad[self.slice(i)].zero_()

@@ -72,6 +72,54 @@ class CapturedStep:
         return self.static_loss
 
 
+def agree_all_ranks(ok: bool) -> bool:
+    """True iff ``ok`` on every rank of the default c10d group (CPU tensors: the gloo group that carries the
+    native communicator's bootstrap), or the local value without one."""
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def step_state_snapshot(net, opt):
+    """Host-side step bookkeeping a HIP-graph capture changes without running anything on the device."""
+    return {"ddp": net.iteration_state() if hasattr(net, "iteration_state") else None,
+            "step_count": getattr(opt, "step_count", None)}
+
+
+def restore_after_failed_capture(net, opt, snap):
+    """Put the host bookkeeping back to where the last eager step left it after an aborted capture (nothing
+    of it ran on the device): DDP bucket state, optimizer step count, a pending device-LR advance, and every
+    derived weight copy the capture recorded (and marked current) but never produced."""
+    torch.cuda.synchronize()
+    if snap.get("ddp") is not None:
+        net.restore_iteration_state(snap["ddp"])
+    flat = getattr(opt, "flat", None)
+    if flat is not None:
+        flat.pending_lr = None
+        flat.invalidate_derived()
+    if snap.get("step_count") is not None:
+        opt.step_count = snap["step_count"]
+
+
+def try_capture(fn, x, y, net, opt, comm=None, agree=agree_all_ranks):
+    """``CapturedStep(fn, x, y)`` if capture succeeds on EVERY rank, else None with the host state restored
+    (every rank then steps eagerly: a graph replay on one rank and eager collectives on another would pair
+    different collectives).  Returns (graph or None, error text or None)."""
+    snap = step_state_snapshot(net, opt)
+    g, err = None, None
+    try:
+        g = CapturedStep(fn, x, y, comm=comm)
+    except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager steps
+        err = f"{type(e).__name__}: {e}"
+    if agree(g is not None):
+        return g, None
+    restore_after_failed_capture(net, opt, snap)
+    return None, err or "graph capture failed on another rank"
+
+
 class GraphedSteps:
     """Training steps: eager for the first ``eager_first`` (allocator / lazy-init warm-up), then replays of
     captured graphs — or, if capture fails on ANY rank, eager steps on every rank in the same process.

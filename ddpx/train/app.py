@@ -50,18 +50,29 @@ def build_parser(description: str) -> argparse.ArgumentParser:
     p.add_argument("--data_root", default="data/cifar10")
     p.add_argument("--train_size", type=int, default=50000, help="synthetic train-set size")
     p.add_argument("--test_size", type=int, default=10000, help="synthetic test-set size")
-    p.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"])
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "auto"],
+                   help="compute precision: fp32 (default: the reference's recipe, /root/reference/singlegpu.py:134-141 "
+                        "trains without autocast) or bf16 (MFMA bf16 with fp32 master weights; auto = bf16 on a GPU)")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
                    help="auto: hand-written kernels, except VGG at fp32 (MIOpen convolutions are faster there)")
-    p.add_argument("--bucket_cap_mb", type=float, default=25.0)
-    p.add_argument("--first_bucket_mb", type=float, default=1.0)
+    p.add_argument("--bucket_cap_mb", type=float, default=None,
+                   help="DDP bucket cap (default: calibrated on the node at start-up, see --bucket_plan)")
+    p.add_argument("--first_bucket_mb", type=float, default=None)
+    p.add_argument("--bucket_plan", default="calibrated", choices=["calibrated", "default"],
+                   help="distributed: time a few training steps of every candidate gradient-communication plan "
+                        "(bucket caps; replicated vs --shard_optimizer) on this node before training and use the "
+                        "fastest (ddpx.parallel.calibrate); default = torch DDP's 25 / 1 MiB caps")
     p.add_argument("--steps_per_epoch", default="compat", help="'compat' (98/49 as the reference), 'auto' or N")
     p.add_argument("--seed", type=int, default=None, help="seed model init (reference: unseeded)")
     p.add_argument("--lr", type=float, default=REF_LR, help="peak LR of the one-cycle schedule (reference 0.4)")
-    p.add_argument("--graph", action="store_true", help="capture the training step in a HIP graph")
+    p.add_argument("--graph", action="store_true",
+                   help="capture the training step in a HIP graph (default on the GPU for the native kernels)")
+    p.add_argument("--no_graph", action="store_true", help="eager training steps")
     p.add_argument("--grad_dtype", default="fp32", choices=["fp32", "bf16"], help="gradient buffer / all-reduce dtype")
-    p.add_argument("--overlap_optimizer", action="store_true", help="per-bucket SGD as all-reduces land")
+    p.add_argument("--overlap_optimizer", action="store_true",
+                   help="per-bucket SGD as all-reduces land (default when distributed)")
+    p.add_argument("--no_overlap_optimizer", action="store_true", help="one SGD pass after all buckets landed")
     p.add_argument("--no_fused_optimizer", action="store_true",
                    help="single GPU: run SGD as its own pass instead of inside the backward kernels")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch", "host"],
@@ -196,6 +207,15 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
                                        test_size=args.test_size)
     if args.seed is not None:
         torch.manual_seed(args.seed)
+    model, optimizer = build_model_and_optimizer(args, device, distributed, comm)
+    spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)
+    scheduler = one_cycle(optimizer, spe)
+    return train_set, model, optimizer, test_set, scheduler
+
+
+def build_model_and_optimizer(args, device, distributed: bool = False, comm=None):
+    """The model (native kernels where ``build_model`` puts them, SyncBatchNorm on request) in a flat parameter
+    store, and its ddpx SGD (the reference's lr 0.4 / momentum 0.9 / wd 5e-4)."""
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels, fp8=getattr(args, "fp8", False))
     if getattr(args, "sync_bn", False) and distributed:
@@ -210,15 +230,125 @@ def load_train_objs(args=None, device=None, distributed: bool = False, world_siz
     if args.graph and device.type == "cuda" and not getattr(model, "use_native", True):
         # torch-op models (e.g. VGG at fp32 on MIOpen convolutions) step eagerly: capturing torch's autograd with
         # AccumulateGrad nodes created by the eager warm-up steps is not supported (it crashed in bench.py)
-        print("note: --graph ignored for the torch-op model path", flush=True)
+        if getattr(args, "graph_explicit", True):
+            print("note: --graph ignored for the torch-op model path", flush=True)
         args.graph = False
     prepare_model(model, device, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     optimizer = SGD(model.parameters(), lr=args.lr, momentum=REF_MOMENTUM, weight_decay=REF_WD,
                     capturable=bool(args.graph and device.type == "cuda"),
                     fused_backward=bool(not distributed and device.type == "cuda" and not args.no_fused_optimizer))
-    spe = resolve_steps_per_epoch(args.steps_per_epoch, loader_len_hint, distributed)
-    scheduler = one_cycle(optimizer, spe)
-    return train_set, model, optimizer, test_set, scheduler
+    return model, optimizer
+
+
+def resolve_run_defaults(args, device, distributed: bool):
+    """Defaults that depend on where the run happens (``run()``): HIP-graph steps on the GPU, and when
+    distributed the per-bucket optimizer overlap and the node-calibrated bucket plan — the tuned path the
+    benchmark measures, behind the reference's own entry points."""
+    args.graph_explicit = bool(getattr(args, "graph", False))
+    args.graph = bool(device.type == "cuda" and not getattr(args, "no_graph", False))
+    if distributed:
+        args.overlap_optimizer = bool(args.overlap_optimizer or not getattr(args, "no_overlap_optimizer", False))
+    args.calibrate = bool(distributed and getattr(args, "bucket_plan", "default") == "calibrated"
+                          and (args.bucket_cap_mb is None or args.first_bucket_mb is None))
+    if not args.calibrate:
+        if args.bucket_cap_mb is None:
+            args.bucket_cap_mb = 25.0
+        if args.first_bucket_mb is None:
+            args.first_bucket_mb = 1.0
+
+
+def make_ddp(args, model, optimizer, comm):
+    net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
+                                  first_bucket_mb=args.first_bucket_mb,
+                                  overlap_optimizer=args.overlap_optimizer,
+                                  shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
+                                  defer_gather=args.defer_gather,
+                                  comm_side_optimizer=args.comm_side_optimizer)
+    if args.overlap_optimizer or args.shard_optimizer:
+        net.attach_optimizer(optimizer)
+    return net
+
+
+def _loss_of(net, model, x, y):
+    if hasattr(model, "forward_loss"):
+        loss, _ = net.forward_loss(x, y)
+        return loss
+    return torch.nn.functional.cross_entropy(net(x), y)
+
+
+def calibrate_bucket_plan(args, device, comm, batch, world_size):
+    """Start-up calibration of the DDP bucket plan (``ddpx.parallel.calibrate``), the same as ``bench.py``'s:
+    every candidate (bucket caps; replicated, or ZeRO-1 when ``--shard_optimizer`` is given) is built for real
+    on this node and a few training steps of it are timed (graph-captured when the run's steps are), and the
+    fastest one's caps are written into ``args``.  Collective.  Returns {name, step_ms}."""
+    import gc
+    from ..parallel.calibrate import calibrate_by_step, candidate_plans
+    from ..runtime.flat_params import flat_of
+    from ..runtime.graphs import try_capture
+    probe, _ = build_model_and_optimizer(args, device, True, comm)
+    f = flat_of(probe)
+    numels = list(f.numels)
+    shapes = [tuple(p.shape) for p in f.params]
+    shadow_only = [id(p) in f.shadow_only for p in f.params]
+    del probe, f
+    plans = [p for p in candidate_plans(numels, shadow_only, world_size, allow_shard=bool(args.shard_optimizer),
+                                        shapes=None if args.chunk_mb else shapes)
+             if p["shard"] == bool(args.shard_optimizer)]
+    if not plans:
+        args.bucket_cap_mb = 25.0 if args.bucket_cap_mb is None else args.bucket_cap_mb
+        args.first_bucket_mb = 1.0 if args.first_bucket_mb is None else args.first_bucket_mb
+        return {"chosen": "default", "step_ms": {}}
+    x, y = batch
+    cuda = device.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+
+    def make_trial(plan):
+        a = argparse.Namespace(**vars(args))
+        a.bucket_cap_mb = plan["bucket_cap_mb"] if args.bucket_cap_mb is None else args.bucket_cap_mb
+        a.first_bucket_mb = plan["first_bucket_mb"] if args.first_bucket_mb is None else args.first_bucket_mb
+        if not args.chunk_mb:
+            a.chunk_mb = plan.get("chunk_mb")
+        model, opt = build_model_and_optimizer(a, device, True, comm)
+        net = make_ddp(a, model, opt, comm)
+        one = torch.ones((), device=device)
+        st = {"k": 0, "g": None}
+
+        def body(xx, yy):
+            opt.zero_grad()
+            loss = _loss_of(net, model, xx, yy)
+            loss.backward(one)
+            opt.step()
+            return loss
+
+        def step():
+            if a.graph and st["k"] >= 2 and st["g"] is None:
+                st["g"], _ = try_capture(body, x, y, net, opt, comm=comm)
+                if st["g"] is None:
+                    a.graph = False
+            if st["g"] is not None:
+                st["g"]()
+            else:
+                body(x, y)
+            st["k"] += 1
+
+        def close():
+            sync()
+            st["g"] = None
+            net.close()
+            gc.collect()
+            if cuda:
+                torch.cuda.empty_cache()
+        return step, close
+
+    chosen, table = calibrate_by_step(plans, make_trial, sync=sync, warm=3, reps=5 if cuda else 2,
+                                      rounds=3 if cuda else 1)
+    if args.bucket_cap_mb is None:
+        args.bucket_cap_mb = chosen["bucket_cap_mb"]
+    if args.first_bucket_mb is None:
+        args.first_bucket_mb = chosen["first_bucket_mb"]
+    if not args.chunk_mb:
+        args.chunk_mb = chosen.get("chunk_mb")
+    return {"chosen": chosen["name"], "step_ms": table}
 
 
 def prepare_dataloader(dataset, batch_size: int, device=None, layout: str = "nchw_f32", rank: int = 0,
@@ -251,20 +381,21 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
             comm = HostStagedComm()
         else:
             comm = TorchComm()
+    resolve_run_defaults(args, device, distributed)
     dataset, model, optimizer, testdata, scheduler = load_train_objs(
         args, device, distributed, world_size, _loader_len(train_n, args.batch_size, world_size), comm)
     layout = input_layout(model, device, args.dtype)
     train_data = prepare_dataloader(dataset, args.batch_size, device, layout, rank, world_size)
     net = model
     if distributed:
-        net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,
-                                      first_bucket_mb=args.first_bucket_mb,
-                                      overlap_optimizer=args.overlap_optimizer,
-                                      shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
-                                      defer_gather=args.defer_gather,
-                                      comm_side_optimizer=args.comm_side_optimizer)
-        if args.overlap_optimizer:
-            net.attach_optimizer(optimizer)
+        if args.calibrate:
+            bs = min(args.batch_size, len(dataset))
+            batch = train_data.make_batch(train_data._epoch_indices()[:bs], 0)
+            cal = calibrate_bucket_plan(args, device, comm, batch, world_size)
+            if rank == 0:
+                print(f"bucket plan: calibrated {cal['chosen']} (first {args.first_bucket_mb:g} MB, cap "
+                      f"{args.bucket_cap_mb:g} MB; training step ms per candidate: {cal['step_ms']})", flush=True)
+        net = make_ddp(args, model, optimizer, comm)
     metrics = MetricsWriter(args.metrics, rank) if args.metrics else None
     trainer = Trainer(net, train_data, optimizer, local_rank if device.type == "cuda" else rank, args.save_every,
                       scheduler, distributed=distributed, rank=rank, graph=args.graph, metrics=metrics,

@@ -16,7 +16,8 @@ Differences (all deliberate):
   (the reference's ``len(next(iter(loader))[0])`` augments one extra batch);
 * the loss uses the model's fused ``forward_loss`` when it has one;
 * ``graph=True`` captures the full-size step into a HIP graph after
-  ``graph_warmup`` eager steps and replays it (partial last batch runs eager);
+  ``graph_warmup`` eager steps and replays it (partial last batch runs eager); if the capture
+  fails on any rank, every rank continues eagerly (``graph_error`` says why);
 * optional JSON-lines metrics (``metrics``) and full-state checkpoints.
 """
 from __future__ import annotations
@@ -28,7 +29,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 from torch import nn
 
-from ..runtime.graphs import CapturedStep
+from ..runtime.graphs import try_capture
 from ..utils.profiling import trace_range
 from . import checkpoint as ckpt
 
@@ -55,6 +56,7 @@ class Trainer:
         self.ckpt_path = ckpt_path
         self._graph = None
         self._graph_batch = None
+        self.graph_error = None
         self.global_step = 0
         self.last_loss = None
         self.start_epoch = 0
@@ -88,12 +90,18 @@ class Trainer:
         if self.use_graph and self._graph is None and self.global_step >= self.graph_warmup \
                 and self._graph_batch is None:
             self._graph_batch = bs
-        if self.use_graph and self._graph_batch == bs:
+        if self.use_graph and self._graph_batch == bs and self._graph is None:
+            self.optimizer.sync_lr()
+            self._graph, err = try_capture(self._step_body, source, targets, self.model, self.optimizer,
+                                           comm=getattr(self.model, "comm", None))
             if self._graph is None:
-                self.optimizer.sync_lr()
-                self._graph = CapturedStep(self._step_body, source, targets, comm=getattr(self.model, "comm", None))
-            else:
-                self._graph.load(source, targets)
+                # capture failed on some rank: every rank steps eagerly from here on (same process)
+                self.use_graph = False
+                self.graph_error = err
+                if self.rank == 0:
+                    print(f"note: HIP-graph capture failed, training continues eagerly ({err})", flush=True)
+        if self.use_graph and self._graph_batch == bs:
+            self._graph.load(source, targets)
             self.optimizer.sync_lr()
             loss = self._graph()
         else:

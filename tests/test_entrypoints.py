@@ -84,6 +84,32 @@ def test_multigpu_torchrun(tmp_path):
     assert "[GPU1] Epoch 0 | Batchsize: 64 | Steps: 4" in out
 
 
+def test_multigpu_runs_the_calibrated_plan_by_default(tmp_path):
+    """The reference entry point runs the tuned path by default: the bucket plan is
+    calibrated on the node by timed training steps, once, on rank 0's print; explicit caps skip it."""
+    common = [os.path.join(ROOT, "multigpu.py"), "1", "1", "--batch_size", "64", "--device", "cpu", "--nprocs", "2",
+              "--model", "mlp", "--hidden", "1536", "--data", "synthetic", "--train_size", "256", "--test_size",
+              "64", "--no_eval"]
+    out = _run(common, tmp_path, extra_env={"MASTER_PORT": str(free_port())})
+    m = re.findall(r"bucket plan: calibrated (\S+) \(first [\d.]+ MB, cap [\d.]+ MB; training step ms per "
+                   r"candidate: (\{.*\})\)", out)
+    assert len(m) == 1, out
+    table = eval(m[0][1])  # noqa: S307 - our own dict repr
+    assert m[0][0] in table and len(table) >= 2 and all(v > 0 for v in table.values())
+    out = _run(common + ["--bucket_cap_mb", "25", "--first_bucket_mb", "1"], tmp_path,
+               extra_env={"MASTER_PORT": str(free_port())})
+    assert "bucket plan" not in out
+
+
+def test_reference_cli_defaults_to_reference_precision():
+    """``python singlegpu.py E S`` trains fp32 like the reference (no autocast, /root/reference/singlegpu.py:134-141);
+    bf16 is opt-in."""
+    from ddpx.train.app import build_parser
+    a = build_parser("x").parse_args(["20", "5"])
+    assert a.dtype == "fp32" and a.model == "vgg" and a.batch_size == 512
+    assert build_parser("x").parse_args(["1", "1", "--dtype", "bf16"]).dtype == "bf16"
+
+
 def test_resume_full_checkpoint(tmp_path):
     common = [os.path.join(ROOT, "singlegpu.py"), "--model", "mlp", "--hidden", "64", "--batch_size", "64",
               "--device", "cpu", "--data", "synthetic", "--train_size", "256", "--test_size", "64", "--no_eval",

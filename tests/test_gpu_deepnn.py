@@ -197,7 +197,7 @@ def test_deepnn_trains_through_entrypoint(gpu, tmp_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.join(root, "singlegpu.py"), "2", "1", "--model", "deepnn", "--data",
-                        "synthetic", "--train_size", "2048", "--test_size", "512", "--graph"],
+                        "synthetic", "--train_size", "2048", "--test_size", "512", "--graph", "--dtype", "bf16"],
                        cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "fp32 model has size=4.53 MiB" in r.stdout

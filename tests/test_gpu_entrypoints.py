@@ -47,16 +47,26 @@ def test_singlegpu_mlp_graph_on_gpu(gpu, tmp_path):
 
 def test_singlegpu_vgg_native_on_gpu(gpu, tmp_path):
     out = _run([os.path.join(ROOT, "singlegpu.py"), "1", "1", "--data", "synthetic", "--train_size", "2048",
-                "--test_size", "512"], tmp_path)
+                "--test_size", "512", "--dtype", "bf16"], tmp_path)
     assert "fp32 model has size=35.20 MiB" in out
     assert re.search(r"fp32 model has accuracy=\d+\.\d\d%", out)
+
+
+def test_singlegpu_reference_command_trains_fp32(gpu, tmp_path):
+    """``python singlegpu.py E S`` with no flags: the reference's VGG at the reference's precision (fp32)."""
+    out = _run([os.path.join(ROOT, "singlegpu.py"), "1", "1", "--data", "synthetic", "--train_size", "1024",
+                "--test_size", "512", "--metrics", "m.jsonl"], tmp_path)
+    assert "[GPU0] Epoch 0 | Batchsize: 512 | Steps: 2" in out
+    assert "fp32 model has size=35.20 MiB" in out
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    assert all(v.dtype in (torch.float32, torch.int64) for v in sd.values())
 
 
 def test_multigpu_single_rank_rccl_sharded(gpu, tmp_path):
     """The distributed entry point with the native RCCL communicator at world size 1 (ZeRO-1, bf16 grads)."""
     out = _run([os.path.join(ROOT, "multigpu.py"), "1", "1", "--nprocs", "1", "--model", "mlp", "--data",
                 "synthetic", "--train_size", "2048", "--test_size", "512", "--shard_optimizer", "--grad_dtype",
-                "bf16", "--overlap_optimizer", "--metrics", "m.jsonl"], tmp_path,
+                "bf16", "--overlap_optimizer", "--metrics", "m.jsonl", "--dtype", "bf16"], tmp_path,
                extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port())})
     assert "[GPU0] Epoch 0 | Batchsize: 512 | Steps: 4" in out
     recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
@@ -75,6 +85,26 @@ def test_bench_ddp_single_comm_stats(gpu, tmp_path, shard):
     assert rec["config"]["ddp"] and rec["config"]["replicas_consistent"]
     assert rec["config"]["sharded_optimizer"] is bool(shard)
     assert rec["config"]["comm_ms_per_step"] > 0
+
+
+def test_bench_n_gt_1_paths_at_world_size_1(gpu, tmp_path):
+    """Every bench.py branch that otherwise runs only at N > 1, executed on the GPU before the driver's 8-GPU
+    job does: the start-up calibration on the real RcclComm (replicated AND ZeRO-1
+    candidates, RCCL identity collectives really issued, each candidate graph-captured), the stock baseline
+    wrapped in torch DDP over its own ``dist.new_group(backend="nccl")``, and the replica digest exchange."""
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3", "--ddp_single",
+                "--stock_ddp", "1", "--stock_steps", "5", "--train_size", "8192"],
+               tmp_path, extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()),
+                                    "DDPX_COMM_SKIP_IDENTITY": "0"})
+    rec = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][0])
+    c = rec["config"]
+    assert c["bucket_plan"] == "calibrated", c
+    table = c["calibration"]["step_ms"]
+    assert any(k.startswith("zero1") for k in table) and any(k.startswith("allreduce") for k in table), table
+    assert all(v > 0 for v in table.values()) and c["calibration"]["chosen"] in table
+    assert c["graph"] is True and c["graph_error"] is None
+    assert c["stock_same_run"] is not None and "torch DDP" in c["stock_same_run"]["recipe"], c["stock_same_run"]
+    assert c["replicas_consistent"] is True and c["ddp"] is True
 
 
 def test_bench_contract_one_gpu(gpu, tmp_path):

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "csrc", "runtime", "rccl_comm.cpp"), os.path.join(ROOT, "csrc", "tests", "rt_sanitize.cpp")]
 
 
-def _build_and_run(tmp_path, flags, env_extra):
+def _build_and_run(tmp_path, flags, env_extra, argv=()):
     cxx = shutil.which("g++")
     if cxx is None or not os.path.exists("/opt/rocm/include/rccl/rccl.h"):
         pytest.skip("host C++ toolchain / ROCm headers not available")
@@ -26,7 +26,7 @@ def _build_and_run(tmp_path, flags, env_extra):
            "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", *SRC, "-o", exe, "-lpthread"]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     env = dict(os.environ, **env_extra)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=240, env=env)
+    r = subprocess.run([exe, *argv], capture_output=True, text=True, timeout=240, env=env)
     return r
 
 
@@ -43,3 +43,13 @@ def test_runtime_address_ub_sanitizer(tmp_path):
     out = r.stdout + r.stderr
     assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out, out[-4000:]
     assert r.returncode == 0 and "rt_sanitize: OK" in out, out[-4000:]
+
+
+def test_abort_escalates_when_owner_is_stuck_inside_rccl(tmp_path):
+    """Timeout action "abort" while the owning thread is blocked inside an RCCL enqueue (holding the issue
+    lock): the watchdog must not abort underneath the call; it publishes error 4 and exits with code 3
+    (advisor r3: the escalation was undocumented and untested)."""
+    r = _build_and_run(tmp_path, [], {}, argv=("stuck",))
+    out = r.stdout + r.stderr
+    assert r.returncode == 3, out[-4000:]
+    assert "stuck inside RCCL" in out and "rt_sanitize: stuck escalation observed" in out, out[-4000:]
