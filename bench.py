@@ -390,8 +390,8 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
     bs = args.batch_size
     runner = None
     if args.impl == "ddpx" and not cpu:
-        from ddpx.runtime.graphs import (CapturedStep, GraphedSteps, agree_all_ranks, restore_after_failed_capture,
-                                         step_state_snapshot)
+        from ddpx.runtime.graphs import (CapturedCycle, CapturedStep, GraphedSteps, agree_all_ranks,
+                                         pingpong_signature_of, restore_after_failed_capture, step_state_snapshot)
         model, net, opt, sched = build_ddpx(args, device, world, comm)
         static_x, static_y = loader.make_batch(idx_all[:bs], 0)
 
@@ -480,9 +480,15 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
                     pstate["k"] += 1
                     return loss
                 return {1: replay_pf}
-            g = {1: CapturedStep(step_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)}
+            # one version per state of the step's ping-pong weight copies (CapturedCycle: replays alternate)
+            sig = pingpong_signature_of(opt)
+            g = {1: CapturedCycle(step_body, static_x, static_y, signature=sig, use_inputs_as_static=True,
+                                  comm=comm_obj)}
             if S > 1:
-                g[S] = CapturedStep(multi_body, static_x, static_y, use_inputs_as_static=True, comm=comm_obj)
+                g[S] = CapturedCycle(multi_body, static_x, static_y, signature=sig, use_inputs_as_static=True,
+                                     comm=comm_obj)
+                if g[S].period > 1 or g[1].period > 1 and S % g[1].period:
+                    g.pop(S)  # S-step graphs only when they leave the copies where the 1-step cycle expects them
             return g
 
         def fallback():
@@ -553,7 +559,8 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
     shapes = [tuple(p.shape) for p in f.params]
     shadow_only = [id(p) in f.shadow_only for p in f.params]
     del probe, f
-    allow = args.shard_optimizer is None and any(shadow_only) and args.comm == "rccl" and not cpu
+    allow = (args.shard_optimizer is None and any(shadow_only) and args.comm == "rccl" and not cpu) or \
+        bool(args.shard_optimizer)
     plans = candidate_plans(numels, shadow_only, max(world, 2) if args.ddp_single else world, allow_shard=allow,
                             shapes=None if args.chunk_explicit else shapes)
     if args.shard_optimizer is not None:
@@ -563,6 +570,13 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
                       first_bucket_mb=(args.first_bucket_mb if args.first_bucket_mb is not None
                                        else p["first_bucket_mb"])) for p in plans]
     sync = (lambda: None) if cpu else torch.cuda.synchronize
+    if not plans:  # nothing to choose between: torch's caps
+        args.bucket_cap_mb = 25.0 if args.bucket_cap_mb is None else args.bucket_cap_mb
+        args.first_bucket_mb = 1.0 if args.first_bucket_mb is None else args.first_bucket_mb
+        if args.shard_optimizer is None:
+            args.shard_optimizer = 0
+        resolve_zero_defaults(args)
+        return
 
     def apply(a, plan):
         a.shard_optimizer = int(plan["shard"])

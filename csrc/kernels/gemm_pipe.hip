@@ -36,6 +36,7 @@
 #include "ddpx_gemm_dispatch.h"
 #include "ddpx_pipe.h"
 #include "ddpx_wgrad_sgd.h"
+#include "ddpx_wsgd_dgrad.h"
 
 namespace ddpx {
 namespace pipe {
@@ -239,3 +240,50 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
     cus = 256;
   return (int)wsgd::launch_pair(q0, q1, cus, stream);
 }
+
+// fc1's data gradient folded into the fc1 + fc0 weight-gradient + SGD launch (ddpx_wsgd_dgrad.h):
+//   dX = relu_mask(aux) * (dY1 W1)  [batch x N1]  (W1: the bf16 copy the forward read, [M1][N1] row-major),
+//   its column sums applied as SGD of the layer below's bias, then W1 -= sgd(dY1^T X1), W0 -= sgd(dX^T X0)
+//   with W1's new bf16 copy written to sh1 (the other buffer of W1's ping-pong pair).
+// scratch: colsum [batch / 64][N1] fp32; words: int32 [N1 / 128 + 2] rounded up to 4 (tickets, done, err),
+// zeroed by the launch.  Returns -20 when not eligible (nothing launched).
+DDPX_API int ddpx_wgrad_sgd_dgrad(const void* dY1, const void* X1, int M1, int N1, int ldy1, int ldx1, float* p1,
+                                  float* buf1, void* sh1, void* q81, void* s81, const void* W1, int ldw1,
+                                  void* dX, const void* aux, int ldaux, const void* X0, int N0, int ldx0, float* p0,
+                                  float* buf0, void* sh0, void* q80, void* s80, float* bp, float* bbuf, void* bsh,
+                                  float* colsum, int* words, int K, const float* lr, float mom, float wd,
+                                  hipStream_t stream) {
+  if (K <= 0 || M1 <= 0 || N1 <= 0 || N0 <= 0) return -20;
+  if (ldy1 % 8 || ldx1 % 8 || ldx0 % 8 || ldw1 % 8 || ldaux % 8 || M1 % 8 || N1 % 8 || N0 % 8) return -20;
+  if (((uintptr_t)dY1 | (uintptr_t)X1 | (uintptr_t)X0 | (uintptr_t)W1 | (uintptr_t)dX | (uintptr_t)aux) & 15)
+    return -20;
+  auto wp = [&](const void* A, const void* B, int M, int N, int lda, int ldb, float* pp, float* buf, void* sh,
+                void* q8, void* s8) {
+    const size_t a_bytes = ((size_t)(K - 1) * lda + M) * 2, b_bytes = ((size_t)(K - 1) * ldb + N) * 2;
+    return pipe::Params{(const unsigned short*)A, (const unsigned short*)B, pp, nullptr, nullptr, nullptr,
+                        M, N, K, lda, ldb, N, 0, pipe::EPI_SGD, 0, 1.f, (unsigned)a_bytes, (unsigned)b_bytes,
+                        SgdArgs{pp, buf, (unsigned short*)sh, lr, mom, wd, (unsigned char*)q8, (unsigned char*)s8},
+                        pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr, nullptr, 0, nullptr};
+  };
+  // fc1: W1 [M1][N1], dY1 [K][M1], X1 [K][N1];  fc0: W0 [N1][N0] (its outputs are fc1's inputs), A = dX [K][N1]
+  const pipe::Params q1 = wp(dY1, X1, M1, N1, ldy1, ldx1, p1, buf1, sh1, q81, s81);
+  const pipe::Params q0 = wp(dX, X0, N1, N0, N1, ldx0, p0, buf0, sh0, q80, s80);
+  if ((size_t)q1.a_bytes != ((size_t)(K - 1) * ldy1 + M1) * 2 || (size_t)q1.b_bytes != ((size_t)(K - 1) * ldx1 + N1) * 2 ||
+      (size_t)q0.b_bytes != ((size_t)(K - 1) * ldx0 + N0) * 2)
+    return -20;  // 32-bit buffer offsets
+  const int nb = N1 / wsgdd::BN;
+  wsgdd::DgArgs d{(const unsigned short*)dY1, (const unsigned short*)W1, (unsigned short*)dX,
+                  (const unsigned short*)aux, K, N1, M1, ldy1, ldw1, N1, ldaux,
+                  (unsigned)(((size_t)(K - 1) * ldy1 + M1) * 2), (unsigned)(((size_t)(M1 - 1) * ldw1 + N1) * 2),
+                  colsum, words, words + nb, words + nb + 1, SgdArgs{bp, bbuf, (unsigned short*)bsh, lr, mom, wd}};
+  if ((size_t)d.b_bytes != ((size_t)(M1 - 1) * ldw1 + N1) * 2) return -20;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  if (!wsgdd::eligible(q1, q0, d, cus)) return -20;
+  const size_t zero_bytes = (size_t)((nb + 2 + 3) / 4 * 4) * 4;
+  return (int)wsgdd::launch(q1, q0, d, cus, zero_bytes, stream);
+}
+
+DDPX_API int ddpx_wgrad_sgd_dgrad_words(int N1) { return (N1 / wsgdd::BN + 2 + 3) / 4 * 4; }

@@ -283,3 +283,100 @@ def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
         return False
     native.check(rc, "ddpx_wgrad_sgd_pair")
     return True
+
+
+native.register_kernel_sig("ddpx_wgrad_sgd_dgrad", native.c_int,
+                           *([native.c_void_p] * 2 + [native.c_int] * 4 + [native.c_void_p] * 5   # fc1 wgrad + SGD
+                             + [native.c_void_p, native.c_int]                                  # W1 (read copy)
+                             + [native.c_void_p, native.c_void_p, native.c_int]                 # dX, mask
+                             + [native.c_void_p, native.c_int, native.c_int] + [native.c_void_p] * 5  # fc0
+                             + [native.c_void_p] * 3                                            # bias SGD
+                             + [native.c_void_p, native.c_void_p, native.c_int, native.c_void_p,  # scratch, K, lr
+                                native.c_float, native.c_float, native.c_void_p]))
+native.register_kernel_sig("ddpx_wgrad_sgd_dgrad_words", native.c_int, native.c_int)
+
+_DG_SCRATCH: dict = {}
+
+
+def _dg_scratch(dev, rows, n):
+    """(colsum [rows, n] fp32, words int32) of the fused data-gradient launch, one pair per device and shape.
+    Kept for the process lifetime: captured graphs hold their addresses (the words are re-zeroed by every
+    launch's memset node)."""
+    key = (dev, rows, n)
+    t = _DG_SCRATCH.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("fused data-gradient scratch: first launch of this shape must happen outside capture")
+        nw = native.kernels().ddpx_wgrad_sgd_dgrad_words(n)
+        t = _DG_SCRATCH[key] = (torch.empty((rows, n), dtype=torch.float32, device=dev),
+                                torch.zeros((nw,), dtype=torch.int32, device=dev))
+    return t
+
+
+_CUS: dict = {}
+
+
+def wgrad_sgd_dgrad_eligible(K, M1, N1, N0, dev) -> bool:
+    """Shape check of :func:`wgrad_sgd_dgrad` (mirrors wsgdd::eligible): batch K = 512, 64 x 128 tiles, and
+    the fc1 weight-gradient and data-gradient tiles divide evenly over the CUs."""
+    if K != 512 or M1 % 64 or N1 % 128 or N0 % 128:
+        return False
+    cus = _CUS.get(dev)
+    if cus is None:
+        cus = _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    nt1, nd = (M1 // 64) * (N1 // 128), (K // 64) * (N1 // 128)
+    return nt1 % cus == 0 and nd % cus == 0 and (nt1 // cus) * (K // 64) == (nd // cus) * (M1 // 64)
+
+
+def wgrad_sgd_dgrad(dy1, x1, sgd1, w1, relu_mask_of, x0, sgd0, bias_sgd, mx1=None, mx0=None, out=None):
+    """fc1's data gradient folded into the fc1 + fc0 weight-gradient + SGD launch (ddpx_wsgd_dgrad.h):
+
+        dX = (dy1 @ w1) * (relu_mask_of > 0)     [batch, in1]    (bias_sgd: SGD of the layer below's bias by
+                                                                   the column sums of dX)
+        W1 -= sgd(dy1^T x1)  -> sgd1, whose bf16 copy target must NOT alias ``w1`` (the copy read here)
+        W0 -= sgd(dX^T x0)   -> sgd0
+
+    Returns dX, or None when the shapes are not eligible (nothing launched)."""
+    for t, n in ((dy1, "dy1"), (x1, "x1"), (w1, "w1"), (relu_mask_of, "relu_mask_of"), (x0, "x0")):
+        _check_bf16_2d(t, n)
+    K, M1 = dy1.shape
+    K2, N1 = x1.shape
+    K3, N0 = x0.shape
+    if K != K2 or K != K3 or tuple(w1.shape) != (M1, N1) or tuple(relu_mask_of.shape) != (K, N1):
+        return None
+    if sgd1[3] is not sgd0[3] or sgd1[3] is not bias_sgd[3] or sgd1[4] != sgd0[4] or sgd1[5] != sgd0[5]:
+        return None
+    if sgd1[2] is None or sgd1[2].data_ptr() == w1.data_ptr():
+        return None  # the weight's new bf16 copy must go to the other ping-pong buffer
+    _req(sgd1[0].numel() == M1 * N1 and sgd0[0].numel() == N1 * N0 and bias_sgd[0].numel() == N1,
+         "sgd target size mismatch")
+    if (mx1 is None) != (mx0 is None):
+        mx1 = mx0 = None
+    colsum, words = _dg_scratch(dy1.device, K // 64, N1)
+    if out is None:
+        out = torch.empty((K, N1), dtype=torch.bfloat16, device=dy1.device)
+    lr = sgd1[3]
+    args = [dy1.data_ptr(), x1.data_ptr(), M1, N1, dy1.stride(0), x1.stride(0), sgd1[0].data_ptr(), native.ptr(sgd1[1]),
+            native.ptr(sgd1[2]), native.ptr(mx1[0] if mx1 else None), native.ptr(mx1[1] if mx1 else None),
+            w1.data_ptr(), w1.stride(0), out.data_ptr(), relu_mask_of.data_ptr(), relu_mask_of.stride(0),
+            x0.data_ptr(), N0, x0.stride(0), sgd0[0].data_ptr(), native.ptr(sgd0[1]), native.ptr(sgd0[2]),
+            native.ptr(mx0[0] if mx0 else None), native.ptr(mx0[1] if mx0 else None),
+            bias_sgd[0].data_ptr(), native.ptr(bias_sgd[1]), native.ptr(bias_sgd[2]),
+            colsum.data_ptr(), words.data_ptr(), K, lr.data_ptr(), float(sgd1[4]), float(sgd1[5]),
+            native.stream_handle()]
+    rc = native.kernels().ddpx_wgrad_sgd_dgrad(*args)
+    if rc == -20:
+        return None
+    native.check(rc, "ddpx_wgrad_sgd_dgrad")
+    return out
+
+
+def wgrad_sgd_dgrad_state(dev, n1):
+    """(tiles published, spin give-up flag) of the last fused data-gradient launch on ``dev`` for fc1 width
+    ``n1`` (words = [n1 / 128 column tickets][done][err]); synchronises."""
+    for (d, _, n), (_, words) in _DG_SCRATCH.items():
+        if d == dev and n == n1:
+            nb = n1 // 128
+            w = words.cpu()
+            return int(w[nb]), int(w[nb + 1])
+    return None

@@ -32,6 +32,9 @@ from .head import head_backward, head_forward
 _PAIR_WGRAD = os.environ.get("DDPX_WGRAD_PAIR", "1") != "0"
 # DDPX_FP8_WGRAD=1: MX-FP8 weight-gradient GEMMs too (default: MX-FP8 forward GEMMs, bf16 backward)
 _FP8_WGRAD = os.environ.get("DDPX_FP8_WGRAD", "0") == "1"
+# DDPX_DGRAD_FUSE=0: launch fc1's data gradient on its own before the pair (default: inside the pair's launch,
+# csrc/include/ddpx_wsgd_dgrad.h, with fc1's bf16 weight copy ping-ponged between two buffers)
+_DGRAD_FUSE = os.environ.get("DDPX_DGRAD_FUSE", "1") != "0"
 
 
 def _to_bf16_2d(x):
@@ -131,12 +134,15 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                       sgd_w=flat.fused_spec(wl), sgd_b=flat.fused_spec(bl), sgd_prev=flat.fused_spec(bprev))
         for p in (wl, bl, bprev):
             flat.mark_updated(p)
+        if L == 2 and not saved8 and _PAIR_WGRAD and _DGRAD_FUSE and _fused_dgrad(model, flat, ps, hs, dpre):
+            return
         deferred = None  # layer 1's update, launched together with layer 0's (one warp-specialised launch)
         for l in range(L - 1, -1, -1):
             w, _ = ps[l]
             dnext = None
             if l > 0:  # data gradient first: it must read W_l before the fused update rewrites it
                 bp = ps[l - 1][1]
+                flat.normalize_pingpong()  # (the unfused update writes the main bf16 copy)
                 dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
                 flat.mark_updated(bp)
             if l == 1 and not saved8 and _PAIR_WGRAD:
@@ -193,6 +199,41 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                                    bias_grad_accumulate=accl)
             flat.grad_done(bp)
             dpre = dnext
+
+
+def _fused_dgrad(model, flat, ps, hs, dpre) -> bool:
+    """Two hidden layers, optimizer fused into backward: fc1's data gradient, fc1's and fc0's weight gradients
+    and all three SGD updates (W1, W0, b0) in ONE launch (G.wgrad_sgd_dgrad).  fc1's new bf16 copy goes to the
+    other buffer of its ping-pong pair (the launch's data gradient reads the current one).  False (nothing
+    launched) when the shapes are not eligible."""
+    (w0, b0), (w1, _) = ps[0], ps[1]
+    K, M1 = dpre.shape
+    N1, N0 = hs[1].shape[1], hs[0].shape[1]
+    if getattr(model, "_dg_fuse_ok", None) is False or not G.wgrad_sgd_dgrad_eligible(K, M1, N1, N0, dpre.device):
+        model._dg_fuse_ok = False
+        return False
+    if not flat.has_pingpong(w1):
+        if torch.cuda.is_current_stream_capturing():
+            return False  # first use must allocate the second buffer outside a capture
+        flat.enable_pingpong(w1)
+    s1, s0, sb = flat.fused_spec(w1), flat.fused_spec(w0), flat.fused_spec(b0)
+    if s1 is None or s0 is None or sb is None:
+        return False
+    s1 = (s1[0], s1[1], flat.shadow_next(w1), s1[3], s1[4], s1[5])
+    emit = flat.shadow8 is not None and flat.fp8_from_optimizer
+    mx1, mx0 = (flat.mx8_views(w1), flat.mx8_views(w0)) if emit else (None, None)
+    if mx1 is None or mx0 is None:
+        mx1 = mx0 = None
+    dx = G.wgrad_sgd_dgrad(dpre, hs[1], s1, flat.shadow_of(w1), hs[1], hs[0], s0, sb, mx1=mx1, mx0=mx0)
+    if dx is None:
+        model._dg_fuse_ok = False
+        return False
+    model._dg_fuse_ok = True
+    flat.flip_pingpong(w1)
+    flat.mark_updated(w1, fp8_written=mx1 is not None)
+    flat.mark_updated(w0, fp8_written=mx0 is not None)
+    flat.mark_updated(b0)
+    return True
 
 
 class _MLPLoss(torch.autograd.Function):

@@ -164,6 +164,8 @@ class SGD(Optimizer):
 
     def _update(self, start, end, g, fp8=True):
         f = self.flat
+        if f.pp_parity:
+            f.normalize_pingpong(start, end)  # the flat pass writes the main bf16 copy
         buf = self.momentum_buffer[start:end] if self.momentum_buffer is not None else f.master[start:end]
         sh = f.shadow[start:end] if f.shadow is not None else None
         # a store that keeps an MX-FP8 weight copy gets it written in the same pass (fp8 forward GEMMs)

@@ -152,6 +152,8 @@ def calibrate_by_step(plans, make_trial, sync=lambda: None, warm=3, reps=5, roun
             local.append(time_trial(step, sync, warm=warm, reps=reps, rounds=rounds))
         finally:
             close()
+    if not plans:
+        raise ValueError("calibrate_by_step: no candidate plans")
     ms = _max_over_ranks(local)
     best = min(ms)
     pick = min(i for i, v in enumerate(ms) if v <= best * (1.0 + tie))

@@ -68,6 +68,10 @@ class FlatParams:
         # per-parameter update counter: consumers that keep a derived copy of a weight (the VGG path's permuted
         # bf16 conv layouts) re-derive it when the counter moved since they last did
         self.version = [0] * len(self.params)
+        # ping-pong bf16 copies (enable_pingpong): param index -> the alternate buffer's view; pp_parity[i] = 1
+        # while the param's current copy (p._ddpx_shadow, what readers read) is the alternate buffer
+        self.pp_alt = {}
+        self.pp_parity = {}
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=grad_dtype, device=device)
         self.shadow = torch.zeros(self.total, dtype=shadow_dtype, device=device) if shadow_dtype else None
@@ -133,6 +137,66 @@ class FlatParams:
     def shadow_of(self, p):
         return getattr(p, "_ddpx_shadow", None)
 
+    # -- ping-pong bf16 copies ---------------------------------------------------
+    # A kernel that READS a weight's bf16 copy while an optimizer stream in the same launch rewrites that weight
+    # (the toy MLP's fc1 data gradient inside the fused weight-gradient + SGD launch, ops/mlp.py) writes the new
+    # copy into a second buffer instead; the copies then alternate every step, so a captured step exists in
+    # two versions (ddpx.runtime.graphs.CapturedCycle).  Generic writers of ``shadow`` (flat SGD, DDP gathers,
+    # refresh) see the main buffer: normalize_pingpong() moves a parameter back to it first.
+    def enable_pingpong(self, p):
+        i = self.index[id(p)]
+        if i in self.pp_alt:
+            return
+        if self.shadow is None:
+            raise RuntimeError("ping-pong copies need a bf16 shadow")
+        if torch.cuda.is_available() and self.master.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("enable_pingpong must run outside graph capture")
+        main = self.shadow[self.slice(i)].view(p.shape)
+        self.pp_alt[i] = main.clone()
+        self.pp_parity[i] = 0
+        p._ddpx_shadow = main
+
+    def has_pingpong(self, p) -> bool:
+        return self.index[id(p)] in self.pp_alt
+
+    def shadow_next(self, p):
+        """The buffer an update of p that must not overwrite its current copy writes the new copy to."""
+        i = self.index[id(p)]
+        main = self.shadow[self.slice(i)].view(p.shape)
+        return main if self.pp_parity[i] else self.pp_alt[i]
+
+    def flip_pingpong(self, p):
+        """p's new copy (written to shadow_next) becomes the current one."""
+        i = self.index[id(p)]
+        p._ddpx_shadow = self.shadow_next(p)
+        self.pp_parity[i] ^= 1
+
+    def pingpong_signature(self):
+        return tuple(sorted(self.pp_parity.items()))
+
+    def set_pingpong_signature(self, sig):
+        """Restore parities taken by pingpong_signature() (host bookkeeping of an aborted capture)."""
+        for i, par in sig:
+            if self.pp_parity.get(i) != par:
+                p = self.params[i]
+                p._ddpx_shadow = self.shadow_next(p)
+                self.pp_parity[i] = par
+
+    def normalize_pingpong(self, start=None, end=None):
+        """Parameters (overlapping [start, end)) whose current copy is the alternate buffer: copy it back into the
+        main shadow and make that current (before a generic writer updates the main buffer)."""
+        for i, par in list(self.pp_parity.items()):
+            if not par:
+                continue
+            o, n = self.offsets[i], self.numels[i]
+            if start is not None and (o >= end or o + n <= start):
+                continue
+            p = self.params[i]
+            main = self.shadow[self.slice(i)].view(p.shape)
+            main.copy_(self.pp_alt[i])
+            p._ddpx_shadow = main
+            self.pp_parity[i] = 0
+
     def enable_fp8_shadow(self):
         """Keep an MX-FP8 copy of the parameters for fp8 forward GEMMs: the optimizer kernels that can write it
         next to the bf16 copy do (flat SGD, fused weight-gradient + SGD pair), anything else marks it stale and
@@ -193,6 +257,10 @@ class FlatParams:
 
     def refresh_shadow(self):
         self.invalidate_derived()  # (also across a relayout's re-indexing)
+        for i in list(self.pp_parity):  # every copy back on the main buffer (rewritten just below)
+            p = self.params[i]
+            p._ddpx_shadow = self.shadow[self.slice(i)].view(p.shape)
+            self.pp_parity[i] = 0
         if self.shadow is None:
             return
         from ..ops.elementwise import cast_bf16_
@@ -209,6 +277,8 @@ class FlatParams:
         order = [i for g in groups for i in g]
         if sorted(order) != list(range(len(self.params))):
             raise ValueError("relayout groups must cover every parameter exactly once")
+        self.normalize_pingpong()
+        self.pp_alt, self.pp_parity = {}, {}  # (indices change; re-enabled by their user)
         if pad_to % ALIGN:
             raise ValueError("pad_to must be a multiple of the alignment")
         new_params = [self.params[i] for i in order]

@@ -72,6 +72,44 @@ class CapturedStep:
         return self.static_loss
 
 
+class CapturedCycle:
+    """A training step whose host-visible state alternates (a weight's bf16 copy ping-pongs between two buffers,
+    ``FlatParams.enable_pingpong``): captured once per state, ``signature()`` telling them apart, until the state
+    returns to the first one; replays cycle through the versions in capture order (period 1 for every other
+    step).  All versions share the first one's static input buffers."""
+
+    def __init__(self, fn, example_x, example_y, signature=None, max_period: int = 2, use_inputs_as_static=False,
+                 comm=None):
+        sig0 = signature() if signature is not None else None
+        first = CapturedStep(fn, example_x, example_y, use_inputs_as_static=use_inputs_as_static, comm=comm)
+        self.graphs = [first]
+        while signature is not None and signature() != sig0:
+            if len(self.graphs) >= max_period:
+                raise RuntimeError(f"training-step state does not return to its start within {max_period} steps")
+            self.graphs.append(CapturedStep(fn, first.static_x, first.static_y, use_inputs_as_static=True, comm=comm))
+        self.static_x, self.static_y = first.static_x, first.static_y
+        self.k = 0
+
+    @property
+    def period(self):
+        return len(self.graphs)
+
+    def load(self, x, y):
+        self.graphs[0].load(x, y)
+
+    def __call__(self, x=None, y=None):
+        if x is not None:
+            self.load(x, y)
+        g = self.graphs[self.k % len(self.graphs)]
+        self.k += 1
+        return g()
+
+
+def pingpong_signature_of(opt):
+    flat = getattr(opt, "flat", None)
+    return flat.pingpong_signature if flat is not None else None
+
+
 def agree_all_ranks(ok: bool) -> bool:
     """True iff ``ok`` on every rank of the default c10d group (CPU tensors: the gloo group that carries the
     native communicator's bootstrap), or the local value without one."""
@@ -85,8 +123,10 @@ def agree_all_ranks(ok: bool) -> bool:
 
 def step_state_snapshot(net, opt):
     """Host-side step bookkeeping a HIP-graph capture changes without running anything on the device."""
+    flat = getattr(opt, "flat", None)
     return {"ddp": net.iteration_state() if hasattr(net, "iteration_state") else None,
-            "step_count": getattr(opt, "step_count", None)}
+            "step_count": getattr(opt, "step_count", None),
+            "pingpong": flat.pingpong_signature() if flat is not None else None}
 
 
 def restore_after_failed_capture(net, opt, snap):
@@ -100,18 +140,20 @@ def restore_after_failed_capture(net, opt, snap):
     if flat is not None:
         flat.pending_lr = None
         flat.invalidate_derived()
+        if snap.get("pingpong") is not None:
+            flat.set_pingpong_signature(snap["pingpong"])  # (the aborted capture flipped copies it never wrote)
     if snap.get("step_count") is not None:
         opt.step_count = snap["step_count"]
 
 
 def try_capture(fn, x, y, net, opt, comm=None, agree=agree_all_ranks):
-    """``CapturedStep(fn, x, y)`` if capture succeeds on EVERY rank, else None with the host state restored
+    """``CapturedCycle(fn, x, y)`` if capture succeeds on EVERY rank, else None with the host state restored
     (every rank then steps eagerly: a graph replay on one rank and eager collectives on another would pair
     different collectives).  Returns (graph or None, error text or None)."""
     snap = step_state_snapshot(net, opt)
     g, err = None, None
     try:
-        g = CapturedStep(fn, x, y, comm=comm)
+        g = CapturedCycle(fn, x, y, signature=pingpong_signature_of(opt), comm=comm)
     except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager steps
         err = f"{type(e).__name__}: {e}"
     if agree(g is not None):

@@ -434,3 +434,98 @@ def test_wgrad_sgd_pair_matches_single_launches(gpu, mom):
         assert torch.equal(sha, shb)
         if mom:
             assert torch.equal(ba, bb)
+
+
+@pytest.mark.parametrize("mom", [0.9, 0.0])
+def test_wgrad_sgd_dgrad_matches_dgrad_plus_pair(gpu, mom):
+    """fc1's data gradient folded into the fc1 + fc0 weight-gradient + SGD launch (ddpx_wsgd_dgrad.h) == the
+    standalone dgrad (ReLU mask, bf16 dX, fused fc0-bias SGD) + the pair launch, bit for bit: dX, both
+    weights' master / momentum / bf16 copy, the bias' master / momentum.  Launched twice: the published-tile
+    counter and the column tickets are re-zeroed by every launch."""
+    from ddpx.ops import gemm as G
+    torch.manual_seed(11)
+    K, M1, N1, N0 = 512, 4096, 4096, 3072
+    dy1 = (torch.randn(K, M1, device=gpu) * 0.05).to(torch.bfloat16)
+    x1 = torch.relu(torch.randn(K, N1, device=gpu)).to(torch.bfloat16)  # H0 (half zeros: the mask matters)
+    x0 = torch.rand(K, N0, device=gpu).to(torch.bfloat16)
+    w1 = (torch.randn(M1, N1, device=gpu) * 0.02).to(torch.bfloat16)
+    lr = torch.full((), 0.05, device=gpu)
+
+    def state():
+        g = torch.Generator(device=gpu).manual_seed(12)
+        mk = lambda n: (torch.randn(n, device=gpu, generator=g) * 0.02,  # noqa: E731
+                        torch.randn(n, device=gpu, generator=g) * 0.01,
+                        torch.zeros(n, dtype=torch.bfloat16, device=gpu))
+        return [mk(M1 * N1), mk(N1 * N0), mk(N1)]
+
+    def spec(t):
+        p, b, sh = t
+        return (p, b if mom else None, sh, lr, mom, 5e-4)
+
+    fa, ra = state(), state()
+    for it in range(2):
+        dx = G.wgrad_sgd_dgrad(dy1, x1, spec(fa[0]), w1, x1, x0, spec(fa[1]), spec(fa[2]))
+        assert dx is not None, "toy-MLP shapes must be eligible"
+        dxr = G.linear_dgrad(dy1, w1, relu_mask_of=x1, bias_sgd=spec(ra[2]))
+        assert G.wgrad_sgd_pair(dy1, x1, spec(ra[0]), dxr, x0, spec(ra[1]))
+        torch.cuda.synchronize()
+        done, err = G.wgrad_sgd_dgrad_state(gpu, N1)
+        assert err == 0 and done == (K // 64) * (N1 // 128), (done, err)
+        assert torch.equal(dx, dxr), it
+        for (pa, ba, sa), (pb, bb, sb) in zip(fa, ra):
+            assert torch.equal(pa, pb), it
+            assert torch.equal(sa, sb), it
+            if mom:
+                assert torch.equal(ba, bb), it
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_toy_mlp_fused_dgrad_step_bitwise(gpu, graph):
+    """The toy MLP (3072-4096-4096-10, batch 512) with fc1's data gradient inside the fused weight-gradient +
+    SGD launch and fc1's bf16 copy ping-ponged between two buffers (eager, and as a 2-version captured cycle)
+    == materialised fp32 gradients + the flat SGD pass, bit for bit over 5 steps."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.optim.sgd import SGD
+    from ddpx.runtime.graphs import CapturedCycle, pingpong_signature_of
+    torch.manual_seed(13)
+    a, b = MLP(hidden=4096), MLP(hidden=4096)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        ddpx.prepare_model(m, gpu)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True, fused_backward=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    xs = [torch.rand(512, 3072, device=gpu).to(torch.bfloat16) for _ in range(5)]
+    ts = [torch.randint(0, 10, (512,), device=gpu) for _ in range(5)]
+
+    def body(x, y):
+        oa.zero_grad()
+        loss, _ = a.forward_loss(x, y)
+        loss.backward()
+        oa.step()
+        return loss
+
+    oa.sync_lr()
+    la = [body(xs[0], ts[0]).item()]
+    assert getattr(a, "_dg_fuse_ok", None) is True, "the fused data-gradient launch must be eligible here"
+    assert a.fc1.weight._ddpx_flat.has_pingpong(a.fc1.weight)
+    if graph:
+        g = CapturedCycle(body, xs[1], ts[1], signature=pingpong_signature_of(oa))
+        assert g.period == 2
+        la += [g(xs[i], ts[i]).item() for i in range(1, 5)]
+    else:
+        la += [body(xs[i], ts[i]).item() for i in range(1, 5)]
+    lb = []
+    for i in range(5):
+        ob.zero_grad()
+        loss, _ = b.forward_loss(xs[i], ts[i])
+        loss.backward()
+        ob.step()
+        lb.append(loss.item())
+    assert la == lb
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
+    assert torch.equal(oa.momentum_buffer, ob.momentum_buffer)
+    fa, fb = a.fc1.weight._ddpx_flat, b.fc1.weight._ddpx_flat
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):  # the CURRENT bf16 copies agree too
+        assert torch.equal(fa.shadow_of(p), fb.shadow_of(q)), n
