@@ -108,11 +108,22 @@ wgrad_sgd_dgrad_kernel(pipe::Params p1, pipe::Params p0, DgArgs d) {
     n0_ = (g % tn0) * BN;
     return 0;
   };
-  // data-gradient tile j of this workgroup: the 8 row tiles of a column block are consecutive tile ids
+  // data-gradient tile j of this workgroup.  The tmd row tiles of one column block read the same W1 column
+  // panel (K x 128 bf16, 1 MiB for the toy MLP): they are given workgroup ids of equal id % 8 — one XCD under
+  // round-robin placement (speed only, never correctness: MI355X_MICROARCH.md) — so the panel comes from
+  // that XCD's L2 after its first reader instead of 8 times from the Infinity Cache / HBM.
+  const int ncb = d.N / BN;
+  const bool xcd_map = (ncb % 8) == 0 && ((ndw * G) % 8) == 0;
   auto dtile = [&](int j, int& m0, int& n0_) {
     const int g = b + j * G;
-    m0 = (g % tmd) * BM;
-    n0_ = (g / tmd) * BN;
+    if (xcd_map) {
+      const int x = g & 7, s = g >> 3;  // (id % 8, id / 8)
+      m0 = (s % tmd) * BM;
+      n0_ = (x * (ncb / 8) + s / tmd) * BN;
+    } else {
+      m0 = (g % tmd) * BM;
+      n0_ = (g / tmd) * BN;
+    }
   };
   // a data-gradient tile completes at the end of weight-gradient iteration i (phase 1 only)
   auto dg_done_at = [&](int i) -> bool { return i < n1 && ((i + 1) * nk) % nkd == 0; };

@@ -32,9 +32,12 @@ from .head import head_backward, head_forward
 _PAIR_WGRAD = os.environ.get("DDPX_WGRAD_PAIR", "1") != "0"
 # DDPX_FP8_WGRAD=1: MX-FP8 weight-gradient GEMMs too (default: MX-FP8 forward GEMMs, bf16 backward)
 _FP8_WGRAD = os.environ.get("DDPX_FP8_WGRAD", "0") == "1"
-# DDPX_DGRAD_FUSE=0: launch fc1's data gradient on its own before the pair (default: inside the pair's launch,
-# csrc/include/ddpx_wsgd_dgrad.h, with fc1's bf16 weight copy ping-ponged between two buffers)
-_DGRAD_FUSE = os.environ.get("DDPX_DGRAD_FUSE", "1") != "0"
+# DDPX_DGRAD_FUSE=1: fc1's data gradient inside the pair's launch (csrc/include/ddpx_wsgd_dgrad.h, fc1's bf16
+# weight copy ping-ponged between two buffers).  Opt-in: measured slower than the two launches on MI355X
+# (toy step 0.2905 vs 0.2379-0.2391 ms, one box, profiles/r4_dgfuse): the pair's math waves are bound by their
+# L2 -> LDS operand DMA, not idle behind the optimizer stream, so the data gradient's operand stream adds its
+# full cost, and the LDS left for two rings allows only 2 stages each.
+_DGRAD_FUSE = os.environ.get("DDPX_DGRAD_FUSE", "0") == "1"
 
 
 def _to_bf16_2d(x):

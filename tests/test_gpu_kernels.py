@@ -485,9 +485,19 @@ def test_toy_mlp_fused_dgrad_step_bitwise(gpu, graph):
     SGD launch and fc1's bf16 copy ping-ponged between two buffers (eager, and as a 2-version captured cycle)
     == materialised fp32 gradients + the flat SGD pass, bit for bit over 5 steps."""
     import ddpx
+    import ddpx.ops.mlp as mlp_ops
     from ddpx.models import MLP
     from ddpx.optim.sgd import SGD
     from ddpx.runtime.graphs import CapturedCycle, pingpong_signature_of
+    old = mlp_ops._DGRAD_FUSE
+    mlp_ops._DGRAD_FUSE = True  # opt-in path (DDPX_DGRAD_FUSE=1)
+    try:
+        _fused_dgrad_step(gpu, graph, ddpx, MLP, SGD, CapturedCycle, pingpong_signature_of)
+    finally:
+        mlp_ops._DGRAD_FUSE = old
+
+
+def _fused_dgrad_step(gpu, graph, ddpx, MLP, SGD, CapturedCycle, pingpong_signature_of):
     torch.manual_seed(13)
     a, b = MLP(hidden=4096), MLP(hidden=4096)
     b.load_state_dict(a.state_dict())
