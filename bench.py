@@ -220,7 +220,7 @@ def make_data(args, device, rank, world, layout=None):
         if native and args.model in ("vgg", "deepnn"):
             layout = "nhwc8_bf16"
         if native and fp32:
-            layout = {"vgg": "nhwc4_f32", "deepnn": "nchw_f32"}.get(args.model, "flat_f32")
+            layout = {"vgg": "nhwc4_f32", "deepnn": "nhwc4_f32"}.get(args.model, "flat_f32")
         if device.type == "cpu":
             layout = "nchw_f32"
     return DeviceLoader(ds, args.batch_size, device, sampler=sampler, train=True, layout=layout, seed=rank)
@@ -799,7 +799,9 @@ def main(argv=None):
                    "graph_error": (runner.graph_error if runner is not None else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (
                        " fused-into-backward" if (args.impl == "ddpx" and not multi and args.fused_optimizer
-                                                  and not cpu) else ""),
+                                                  and not cpu) else "") + (
+                       " ZeRO-1 (fp32 master + momentum sharded over ranks, bf16 compute copy all-gathered; same "
+                       "update arithmetic as the replicated step)" if (ddpx_ddp and args.shard_optimizer) else ""),
                    "grad_comm": grad_comm, "grad_dtype": args.grad_dtype if args.impl == "ddpx" else "fp32",
                    "bucket_cap_mb": args.bucket_cap_mb, "first_bucket_mb": args.first_bucket_mb,
                    "bucket_plan": (("calibrated" if getattr(args, "calibration", None) else "explicit")

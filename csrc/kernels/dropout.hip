@@ -68,6 +68,36 @@ dropout_fwd_kernel(const unsigned short* __restrict__ x, unsigned short* __restr
   }
 }
 
+// fp32 variant (the reference's precision): one thread = 4 consecutive floats = one Philox block (counter word
+// 3 = 2 keeps its stream apart from the bf16 kernel's two blocks per thread).
+__global__ void __launch_bounds__(256)
+dropout_fwd_f32_kernel(const float* __restrict__ x, float* __restrict__ out, int64_t n4, float p, float scale,
+                       int64_t* __restrict__ state, unsigned* __restrict__ done) {
+  const uint64_t seed = (uint64_t)state[0];
+  const uint64_t offset = (uint64_t)state[1];
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + t * 4);
+    const u32x4s r = philox4x32_10(u32x4s{(unsigned)t, (unsigned)(t >> 32), (unsigned)offset, 2u}, (unsigned)seed,
+                                   (unsigned)(seed >> 32));
+    const unsigned rr[4] = {r.x, r.y, r.z, r.w};
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[j] * (u01(rr[j]) >= p ? scale : 0.f);
+    *reinterpret_cast<f32x4*>(out + t * 4) = o;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      state[1] = (int64_t)(offset + 1);
+      *done = 0u;
+      __threadfence();
+    }
+  }
+}
+
 }  // namespace rng
 }  // namespace ddpx
 
@@ -84,5 +114,18 @@ DDPX_API int ddpx_dropout_fwd(const void* x, void* out, int64_t n, float p, int6
   if (blocks < 1 || blocks > 0x7fffffff) return -4;
   hipLaunchKernelGGL(rng::dropout_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const unsigned short*)x,
                      (unsigned short*)out, n8, p, 1.f / (1.f - p), state, done);
+  return (int)hipGetLastError();
+}
+
+// fp32 inverted dropout, n % 4 == 0 (same device-resident generator state protocol as ddpx_dropout_fwd).
+DDPX_API int ddpx_dropout_fwd_f32(const void* x, void* out, int64_t n, float p, int64_t* state, unsigned* done,
+                                  hipStream_t s) {
+  if (n % 4 || p < 0.f || p >= 1.f) return -1;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) return -3;
+  const int64_t n4 = n / 4;
+  const int64_t blocks = (n4 + 255) / 256;
+  if (blocks < 1 || blocks > 0x7fffffff) return -4;
+  hipLaunchKernelGGL(rng::dropout_fwd_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)x,
+                     (float*)out, n4, p, 1.f / (1.f - p), state, done);
   return (int)hipGetLastError();
 }

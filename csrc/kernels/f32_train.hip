@@ -694,17 +694,19 @@ __global__ void __launch_bounds__(1024) head_wgrad_kernel(const float* __restric
   }
 }
 
-// dh[m][k] = go * sum_j dl[m][j] w[j][k]   [* (h[m][k] > 0)]
+// dh[m][k] = go * dh_scale * sum_j dl[m][j] w[j][k]   [* (h[m][k] > 0)]
+// (dh_scale = 1/(1-p) when h is the output of an inverted Dropout(p) after a ReLU: h > 0 is then exactly "kept
+// and positive", so the dropout + ReLU backward costs nothing extra; 1 otherwise)
 __global__ void __launch_bounds__(256) head_dgrad_kernel(const float* __restrict__ dl, const float* __restrict__ go,
                                                           const float* __restrict__ w, const float* __restrict__ h,
-                                                          int M, int K, int NC, int relu_mask,
+                                                          int M, int K, int NC, int relu_mask, float dh_scale,
                                                           float* __restrict__ dh) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)M * K) return;
   const int m = (int)(i / K), k = (int)(i % K);
   float acc = 0.f;
   for (int j = 0; j < NC; ++j) acc = fmaf(dl[(size_t)m * NC + j], w[(size_t)j * K + k], acc);
-  acc *= go ? *go : 1.f;
+  acc *= (go ? *go : 1.f) * dh_scale;
   if (relu_mask && !(h[i] > 0.f)) acc = 0.f;
   dh[i] = acc;
 }
@@ -713,7 +715,7 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const float* __restrict
 // the classes runs in the same order, so the result is bitwise that of the scalar kernel.
 __global__ void __launch_bounds__(256) head_dgrad4_kernel(const float* __restrict__ dl, const float* __restrict__ go,
                                                            const float* __restrict__ w, const float* __restrict__ h,
-                                                           int M, int K, int NC, int relu_mask,
+                                                           int M, int K, int NC, int relu_mask, float dh_scale,
                                                            float* __restrict__ dh) {
   const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
   const int K4 = K / 4;
@@ -726,7 +728,7 @@ __global__ void __launch_bounds__(256) head_dgrad4_kernel(const float* __restric
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = fmaf(d, wv[q], acc[q]);
   }
-  const float g = go ? *go : 1.f;
+  const float g = (go ? *go : 1.f) * dh_scale;
   const f32x4 hv = reinterpret_cast<const f32x4*>(h + (size_t)m * K)[k4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -762,6 +764,22 @@ __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ 
     for (int q = 0; q < 16; ++q) t += red[q][cl];
     out[n] = accumulate ? out[n] + t : t;
   }
+}
+
+// torch.flatten(x, 1) of an NCHW activation held as NHWC: out[n][c * S + s] = x[n][s][c] (backward = 0), or the
+// inverse for its gradient: out[n][s][c] = x[n][c * S + s] (backward = 1).  One thread per element, the NHWC
+// side read / written contiguously.
+__global__ void __launch_bounds__(256) nchw_flatten_kernel(const float* __restrict__ x, int N, int S, int C,
+                                                            int backward, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // NHWC index
+  if (i >= (long)N * S * C) return;
+  const int c = (int)(i % C);
+  const long r = i / C;
+  const int sp = (int)(r % S);
+  const long n = r / S;
+  const size_t f = (size_t)n * S * C + (size_t)c * S + sp;
+  if (backward) out[i] = x[f];
+  else out[f] = x[i];
 }
 
 static int ilog2(int v) {
@@ -914,20 +932,26 @@ DDPX_API int ddpx_f32_head_fwd(const float* h, const float* w, const float* bias
 }
 
 DDPX_API int ddpx_f32_head_bwd(const float* dl, const float* go, const float* h, const float* w, int M, int K, int NC,
-                               float* dW, float* db, int accumulate, float* dh, int relu_mask, hipStream_t s) {
+                               float* dW, float* db, int accumulate, float* dh, int relu_mask, float dh_scale,
+                               hipStream_t s) {
   if (NC > kMaxNC) return -2;
   if (dW) hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk(K, 64) + 1), dim3(1024), 0, s, dl, go, h, M, K, NC, dW, db,
                              accumulate);
   if (dh && K % 4 == 0 && !(((uintptr_t)w | (uintptr_t)h | (uintptr_t)dh) & 15))
     hipLaunchKernelGGL(head_dgrad4_kernel, dim3(nblk((long)M * (K / 4))), dim3(256), 0, s, dl, go, w, h, M, K, NC,
-                       relu_mask, dh);
+                       relu_mask, dh_scale, dh);
   else if (dh)
     hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
-                       relu_mask, dh);
+                       relu_mask, dh_scale, dh);
   return (int)hipGetLastError();
 }
 
 DDPX_API int ddpx_f32_colsum(const float* x, int M, int N, float* out, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(colsum_kernel, dim3(nblk(N, 64)), dim3(1024), 0, s, x, M, N, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_nchw_flatten(const float* x, int N, int S, int C, int backward, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(nchw_flatten_kernel, dim3(nblk((long)N * S * C)), dim3(256), 0, s, x, N, S, C, backward, out);
   return (int)hipGetLastError();
 }

@@ -38,7 +38,8 @@ def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", de
         m.native_dtype = "fp32" if dtype == "fp32" else "bf16"
     elif name == "deepnn":
         m = DeepNN()
-        m.use_native = native and dev.type == "cuda" and dtype != "fp32"
+        m.use_native = native and dev.type == "cuda"
+        m.native_dtype = "fp32" if dtype == "fp32" else "bf16"
     elif name in ("mlp", "mlp_wide"):
         h = hidden or (16384 if name == "mlp_wide" else 4096)
         m = MLP(hidden=h, layers=layers, compute_dtype=cdt)

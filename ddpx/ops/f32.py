@@ -34,7 +34,9 @@ for _sig in (
         ("ddpx_f32_bn_bwd_apply", _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_avgpool", _I, _P, _I, _I, _I, _P, _I, _P),
         ("ddpx_f32_head_fwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P),
-        ("ddpx_f32_head_bwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _I, _P),
+        ("ddpx_f32_head_bwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _I, _F, _P),
+        ("ddpx_f32_nchw_flatten", _I, _P, _I, _I, _I, _I, _P, _P),
+        ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
 ):
     native.register_kernel_sig(*_sig)
@@ -121,14 +123,41 @@ def head_forward(h, w, b, targets=None):
     return loss, logits, dl
 
 
-def head_backward(dl, grad_out, h, w, dW, db, accumulate=False, relu_mask=False, want_dh=True):
+def head_backward(dl, grad_out, h, w, dW, db, accumulate=False, relu_mask=False, want_dh=True, dh_scale=1.0):
     M, K = h.shape
     NC = w.shape[0]
     go = grad_out.float().contiguous() if grad_out is not None else None
     dh = torch.empty_like(h) if want_dh else None
     _call("ddpx_f32_head_bwd", dl.data_ptr(), native.ptr(go), h.data_ptr(), w.data_ptr(), M, K, NC, native.ptr(dW),
-          native.ptr(db), int(accumulate), native.ptr(dh), int(relu_mask))
+          native.ptr(db), int(accumulate), native.ptr(dh), int(relu_mask), float(dh_scale))
     return dh
+
+
+def nchw_flatten(x):
+    """torch.flatten(x, 1) of the NCHW tensor an NHWC fp32 activation [N,H,W,C] stands for: [N, C*H*W]."""
+    N, H, W, C = x.shape
+    _f32(x, "x")
+    out = torch.empty((N, C * H * W), dtype=torch.float32, device=x.device)
+    _call("ddpx_f32_nchw_flatten", x.data_ptr(), N, H * W, C, 0, out.data_ptr())
+    return out
+
+
+def nchw_unflatten(g, N, H, W, C):
+    """Gradient of nchw_flatten: [N, C*H*W] -> NHWC [N,H,W,C]."""
+    _f32(g, "g")
+    out = torch.empty((N, H, W, C), dtype=torch.float32, device=g.device)
+    _call("ddpx_f32_nchw_flatten", g.data_ptr(), N, H * W, C, 1, out.data_ptr())
+    return out
+
+
+def dropout_(x, p, rng, rng_done):
+    """Inverted Dropout(p) of an fp32 tensor; generator state (seed, offset) device-resident in ``rng``."""
+    _f32(x, "x")
+    _req(x.numel() % 4 == 0, "dropout: numel % 4 != 0")
+    out = torch.empty_like(x)
+    _call("ddpx_dropout_fwd_f32", x.data_ptr(), out.data_ptr(), x.numel(), float(p), rng.data_ptr(),
+          rng_done.data_ptr())
+    return out
 
 
 # ---------------------------------------------------------------------------------------------- conv / BN
@@ -351,6 +380,151 @@ def vgg_logits(model, x):
     """Inference logits (no autograd through the native fp32 path)."""
     with torch.no_grad():
         _, _, _, logits, _ = _vgg_forward(model, prep_vgg_input(x), None, model.training)
+    return logits
+
+
+# ---------------------------------------------------------------------------------------------- DeepNN
+# /root/reference/singlegpu.py:18-44 at the reference's precision: [conv3x3+bias -> ReLU] x2 -> MaxPool2 ->
+# [conv3x3+bias -> ReLU] x2 -> MaxPool2 -> flatten (C,H,W) -> Linear(2048,512) -> ReLU -> Dropout(0.1) ->
+# Linear(512,10).  Conv bias + ReLU in the GEMM epilogue; the pool (and the backward's ReLU mask + first-max
+# routing + bias gradient) through the BatchNorm kernels with the identity affine (a = 1, b = 0, mean = 0,
+# rstd = 1, and c1 = c2 = 0 in the apply: dy = routed, masked gradient).
+class _DeepNNPlan:
+    def __init__(self, model):
+        mods = list(model.features.children())
+        self.blocks, i = [], 0
+        while i < len(mods):
+            conv = mods[i]
+            i += 2  # conv, relu
+            pool = i < len(mods) and isinstance(mods[i], torch.nn.MaxPool2d)
+            if pool:
+                i += 1
+            self.blocks.append((conv, pool))
+        cls = list(model.classifier.children())
+        self.lin0, self.drop, self.lin1 = cls[0], cls[2], cls[3]
+        dev = self.lin0.weight.device
+        self.wf, self.wd = [], []
+        for conv, _ in self.blocks:
+            Co, Ci = conv.weight.shape[:2]
+            self.wf.append(torch.empty(9 * conv_channels(Ci) * Co, dtype=torch.float32, device=dev))
+            self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev) if Ci % 4 == 0 else None)
+        cmax = max(c.weight.shape[0] for c, _ in self.blocks)
+        self.ones = torch.ones(cmax, dtype=torch.float32, device=dev)
+        self.zeros = torch.zeros(cmax, dtype=torch.float32, device=dev)
+        self.scratch = torch.empty(2 * cmax, dtype=torch.float32, device=dev)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.rng = torch.tensor([seed, 0], dtype=torch.int64, device=dev)
+        self.rng_done = torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+def _deepnn_plan(model):
+    p = getattr(model, "_ddpx_plan_f32", None)
+    if p is None:
+        p = _DeepNNPlan(model)
+        model._ddpx_plan_f32 = p
+    return p
+
+
+def bias_act_backward(g, y, N, H, W, C, pool, plan, dbias, accumulate=False):
+    """dy [P, C] and dbias (+)= sum dy of out = [maxpool2](y), y = relu(conv + bias) (the ReLU mask and the pool's
+    first-max routing recomputed from y)."""
+    _f32(g, "g")
+    P = N * H * W
+    R = bn_chunk_rows(P, C)
+    T = (P + R - 1) // R
+    one, zero = plan.ones[:C], plan.zeros[:C]
+    part = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
+    _call("ddpx_f32_bn_bwd_sums", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
+          one.data_ptr(), N, H, W, C, int(pool), R, part.data_ptr())
+    c1, c2 = plan.scratch[:C], plan.scratch[C:2 * C]
+    _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), None, dbias.data_ptr(),
+          int(accumulate))
+    dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
+    _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
+          one.data_ptr(), zero.data_ptr(), zero.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
+    return dy
+
+
+def _deepnn_forward(model, x, targets, training):
+    plan = _deepnn_plan(model)
+    saved = []
+    N, H, W, C = x.shape
+    for bi, (conv, pool) in enumerate(plan.blocks):
+        Co = conv.weight.shape[0]
+        conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
+        P = N * H * W
+        y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
+        gemm(IM2COL_KC, x, 0, DENSE_OC, plan.wf[bi], Co, P, Co, 9 * C, y, geom=(C, H, W, 1), bias=conv.bias,
+             relu=True)
+        if pool:
+            xn = torch.empty((N, H // 2, W // 2, Co), dtype=torch.float32, device=x.device)
+            _call("ddpx_f32_bn_apply", y.data_ptr(), plan.ones.data_ptr(), plan.zeros.data_ptr(),
+                  plan.zeros.data_ptr(), N, H, W, Co, 1, 1, xn.data_ptr())
+        else:
+            xn = y.view(N, H, W, Co)
+        saved.append((x, y, (N, H, W, C, Co), pool))
+        x = xn
+        H, W, C = xn.shape[1], xn.shape[2], Co
+    feat = nchw_flatten(x)
+    l0, l1 = plan.lin0, plan.lin1
+    a0 = linear_fwd(feat, l0.weight, l0.bias, relu=True)
+    p = float(plan.drop.p)
+    drop = training and p > 0.0
+    d0 = dropout_(a0, p, plan.rng, plan.rng_done) if drop else a0
+    loss, logits, dl = head_forward(d0, l1.weight, l1.bias, targets)
+    scale = 1.0 / (1.0 - p) if drop else 1.0
+    return saved, (x.shape, feat, d0, scale), loss, logits, dl
+
+
+def _deepnn_backward(model, saved, last, dl, grad_out):
+    plan = _deepnn_plan(model)
+    l0, l1 = plan.lin0, plan.lin1
+    flat = l0.weight._ddpx_flat
+    xshape, feat, d0, scale = last
+    dW1, acc = flat.grad_target(l1.weight)
+    db1, _ = flat.grad_target(l1.bias)
+    # Dropout + ReLU backward folded into the head's dh: mask d0 > 0 (kept and positive), scale 1/(1-p)
+    dd0 = head_backward(dl, grad_out, d0, l1.weight, dW1, db1, accumulate=acc, relu_mask=True, dh_scale=scale)
+    flat.grad_done(l1.weight)
+    flat.grad_done(l1.bias)
+    _grad_write(flat, l0.bias, lambda o, ac: colsum(dd0, o, ac))
+    _grad_write(flat, l0.weight, lambda o, ac: linear_wgrad(dd0, feat, o, ac))
+    g = nchw_unflatten(linear_dgrad(dd0, l0.weight), *xshape)
+    for bi in range(len(plan.blocks) - 1, -1, -1):
+        conv, pool = plan.blocks[bi]
+        x, y, (N, H, W, C, Co), _ = saved[bi]
+        dy = None
+
+        def bias_grad(o, ac):
+            nonlocal dy
+            dy = bias_act_backward(g, y, N, H, W, Co, pool, plan, o, ac)
+        _grad_write(flat, conv.bias, bias_grad)
+        _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
+        if bi > 0:
+            g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+
+
+class _DeepNNLossF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, targets, model, *params):
+        saved, last, loss, _, dl = _deepnn_forward(model, x, targets, model.training)
+        ctx.model, ctx.saved, ctx.last, ctx.dl, ctx.n = model, saved, last, dl, len(params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        _deepnn_backward(ctx.model, ctx.saved, ctx.last, ctx.dl, grad_loss)
+        ctx.saved = ctx.last = ctx.dl = None
+        return (None, None, None) + (None,) * ctx.n
+
+
+def deepnn_loss(model, x, targets):
+    return _DeepNNLossF32.apply(prep_vgg_input(x), targets, model, *model.parameters())
+
+
+def deepnn_logits(model, x):
+    with torch.no_grad():
+        _, _, _, logits, _ = _deepnn_forward(model, prep_vgg_input(x), None, model.training)
     return logits
 
 

@@ -145,3 +145,62 @@ def test_graph_capture_with_rccl(gpu, pg, shard, chunk_mb, defer, side):
         assert torch.equal(a.fc0.weight._ddpx_shadow, b.fc0.weight._ddpx_shadow)
     da.close()
     comm.close()
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_capture_aborted_after_rccl_collectives_then_eager(gpu, pg, shard):
+    """A capture that dies AFTER the backward's bucket collectives were recorded on the real RCCL communicator
+    (what an N > 1 rank sees when a peer's capture fails): the graph is dropped, the host step state restored
+    (ddpx.runtime.graphs.try_capture), and the following eager steps on the same communicator must match a
+    run that never tried to capture, bitwise."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import RcclComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from ddpx.runtime.graphs import try_capture
+    torch.manual_seed(2)
+    a, b = MLP(hidden=512), MLP(hidden=512)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        ddpx.prepare_model(m, gpu)
+    comm = RcclComm(gpu)
+    da = DistributedDataParallel(a, comm=comm, bucket_cap_mb=1.0, first_bucket_mb=0.25, reduce_single=True,
+                                 shard_optimizer=shard)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    xs = [torch.rand(128, 3072, device=gpu).to(torch.bfloat16) for _ in range(4)]
+    ts = [torch.randint(0, 10, (128,), device=gpu) for _ in range(4)]
+    inject = {"on": False, "hit": 0}
+
+    def body(x, y):
+        oa.zero_grad()
+        loss, _ = da.forward_loss(x, y)
+        loss.backward()
+        if inject["on"]:
+            inject["hit"] += 1
+            raise RuntimeError("injected capture failure after the backward's collectives")
+        oa.step()
+        return loss
+
+    oa.sync_lr()
+    losses = [body(xs[0], ts[0]).item()]
+    inject["on"] = True
+    g, err = try_capture(body, xs[1], ts[1], da, oa, comm=comm)
+    assert g is None and "injected" in err and inject["hit"] == 1
+    inject["on"] = False
+    for i in range(1, 4):
+        oa.sync_lr()
+        losses.append(body(xs[i], ts[i]).item())
+    for i in range(4):
+        ob.zero_grad()
+        loss, _ = b.forward_loss(xs[i], ts[i])
+        loss.backward()
+        ob.step()
+        assert loss.item() == losses[i], (i, loss.item(), losses[i])
+    da.consolidate()
+    torch.cuda.synchronize()
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
+    da.close()
+    comm.close()

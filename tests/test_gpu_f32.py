@@ -282,3 +282,118 @@ def test_error_no_worse_than_stock(gpu, case):
     with open("gpurun_out/f32_error.jsonl", "a") as f:
         f.write(json.dumps(rec) + "\n")
     assert e_ours["rel_l2"] <= 1.5 * e_stock["rel_l2"] + 1e-9, rec
+
+
+# ---------------------------------------------------------------------------------------------- DeepNN fp32
+def _deepnn_pair(gpu, seed, p=0.1):
+    import copy
+
+    import ddpx
+    from ddpx.models import build_model
+    torch.manual_seed(seed)
+    native = build_model("deepnn", dtype="fp32", device=gpu, kernels="native")
+    native.classifier[2].p = p
+    ref = copy.deepcopy(native).to(gpu)
+    ref.use_native = False
+    ddpx.prepare_model(native, gpu)
+    assert native.input_layout(gpu) == "nhwc4_f32"
+    return native, ref
+
+
+def test_deepnn_fp32_gradients_match_fp64(gpu):
+    """DeepNN at the reference's precision on the exact-f32 kernels (dropout off on both sides): every gradient
+    against fp64, with torch's own fp32 error as the yardstick below the max-pools."""
+    import copy
+    native, ref = _deepnn_pair(gpu, seed=11, p=0.0)
+    x = torch.rand(64, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (64,), device=gpu)
+    loss, logits = native.forward_loss(x, y)
+    assert logits is None  # the native fp32 path ran
+    loss.backward()
+    rl = F.cross_entropy(ref(x), y)
+    rl.backward()
+    assert abs(loss.item() - rl.item()) < 1e-5
+    r64 = copy.deepcopy(ref).cpu().double()
+    r64.zero_grad()
+    F.cross_entropy(r64(x.cpu().double()), y.cpu()).backward()
+    rp, p64 = dict(ref.named_parameters()), dict(r64.named_parameters())
+    bad = []
+    for n, p in native.named_parameters():
+        e_native, e_torch = _rel(p.main_grad.cpu(), p64[n].grad), _rel(rp[n].grad.cpu(), p64[n].grad)
+        print(f"{n}: native {e_native:.2e} torch-fp32 {e_torch:.2e}")
+        top = n.startswith("classifier")
+        if not e_native < (1e-5 if top else max(5e-3, 3 * e_torch)):
+            bad.append((n, e_native, e_torch))
+    assert not bad, bad
+    native.eval()
+    ref.eval()
+    with torch.no_grad():
+        assert _rel(native(x), ref(x)) < 1e-5
+
+
+def test_deepnn_fp32_dropout_semantics(gpu):
+    """Dropout(0.1) active: the native backward equals torch fp32's for the mask the kernel drew (recovered from
+    the dropped activation: kept = d0 > 0 where the ReLU output is > 0)."""
+    from ddpx.ops import f32 as Fk
+    native, ref = _deepnn_pair(gpu, seed=12)
+    native.train()
+    x = torch.rand(64, 3, 32, 32, device=gpu)
+    t = torch.randint(0, 10, (64,), device=gpu)
+    saved, last, loss, _, dl = Fk._deepnn_forward(native, Fk.prep_vgg_input(x), t, True)
+    _, feat, d0, scale = last
+    assert abs(scale - 1 / 0.9) < 1e-6
+    a0 = F.relu(ref.classifier[0](ref.features(x).flatten(1)))
+    mask = (d0 > 0).float()
+    live = (a0 > 0).float()
+    frac = (mask.sum() / live.sum()).item()
+    assert 0.85 < frac < 0.95, frac
+    kept = d0[d0 > 0] / a0[d0 > 0]
+    assert torch.allclose(kept, torch.full_like(kept, 1 / 0.9), rtol=1e-5)
+    rl = F.cross_entropy(ref.classifier[3](a0 * mask * scale), t)
+    assert abs(loss.item() - rl.item()) < 1e-5 * max(1.0, rl.item())
+    rl.backward()
+    Fk._deepnn_backward(native, saved, last, dl, torch.ones((), device=gpu))
+    for (n, p), (_, q) in zip(native.named_parameters(), ref.named_parameters()):
+        assert _rel(p.main_grad, q.grad) < (1e-5 if n.startswith("classifier") else 5e-3), n
+
+
+def test_dropout_f32_kernel(gpu):
+    from ddpx.ops.f32 import dropout_
+    rng = torch.tensor([99, 0], dtype=torch.int64, device=gpu)
+    done = torch.zeros(1, dtype=torch.int32, device=gpu)
+    x = torch.ones(512, 512, device=gpu)
+    a = dropout_(x, 0.1, rng, done)
+    b = dropout_(x, 0.1, rng, done)
+    torch.cuda.synchronize()
+    assert int(rng[1]) == 2 and int(done[0]) == 0
+    keep = (a > 0).float().mean().item()
+    assert abs(keep - 0.9) < 5e-3, keep
+    assert torch.equal(a[a > 0], torch.full_like(a[a > 0], 1.0 / (1.0 - 0.1)))
+    assert not torch.equal(a, b)
+    rng[1] = 0
+    assert torch.equal(dropout_(x, 0.1, rng, done), a)  # same (seed, offset): same mask
+
+
+def test_deepnn_fp32_trains_like_torch(gpu):
+    """Five SGD steps with dropout off: the native fp32 DeepNN follows torch fp32's trajectory."""
+    from ddpx.optim.sgd import SGD
+    native, ref = _deepnn_pair(gpu, seed=13, p=0.0)
+    opt = SGD(native.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    gen = torch.Generator().manual_seed(3)
+    for _ in range(5):
+        x = torch.rand(64, 3, 32, 32, generator=gen).to(gpu)
+        y = torch.randint(0, 10, (64,), generator=gen).to(gpu)
+        opt.zero_grad()
+        loss, logits = native.forward_loss(x, y)
+        assert logits is None
+        loss.backward()
+        opt.step()
+        ropt.zero_grad()
+        rl = F.cross_entropy(ref(x), y)
+        rl.backward()
+        ropt.step()
+        assert abs(loss.item() - rl.item()) < 2e-3 * max(1.0, rl.item())
+    for (n, p), (_, q) in zip(native.named_parameters(), ref.named_parameters()):
+        err = (p.detach().double() - q.detach().double()).norm().item()
+        assert err < 5e-3 * max(1.0, q.detach().double().norm().item()), n
