@@ -256,16 +256,27 @@ __global__ void __launch_bounds__(256) wprep_kernel(const float* __restrict__ w,
 }
 
 // grad[co][ci][r][s] (+)= sum_z part[z][co][(r*3+s)*Cp + ci]   (fixed order over z)
+// Threads walk the slab layout (ci fastest: coalesced reads of every slab, 8 slabs' loads in flight) and scatter
+// into torch's [Co][Ci][3][3] order; the sum over z runs in the same order as before (bitwise unchanged).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S, int Co, int Ci,
                                                             int Cp, float* __restrict__ grad, int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over Co * Ci * 9, torch order
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over Co * 9 * Ci, slab order
   if (i >= Co * Ci * 9) return;
-  const int rs = i % 9, ci = (i / 9) % Ci, co = i / (9 * Ci);
+  const int ci = i % Ci, rs = (i / Ci) % 9, co = i / (9 * Ci);
   const size_t stride = (size_t)Co * 9 * Cp;
   const float* p = part + (size_t)co * 9 * Cp + rs * Cp + ci;
   float acc = 0.f;
-  for (int z = 0; z < S; ++z) acc += p[z * stride];
-  grad[i] = accumulate ? grad[i] + acc : acc;
+  int z = 0;
+  for (; z + 8 <= S; z += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(z + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; z < S; ++z) acc += p[(size_t)z * stride];
+  const size_t o = ((size_t)co * Ci + ci) * 9 + rs;
+  grad[o] = accumulate ? grad[o] + acc : acc;
 }
 
 // out[i] (+)= sum_z part[z][i]
@@ -335,8 +346,17 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
   float mu = 0.f, var = 0.f;
   if (training) {
     double sm = 0.0;
-    if (ok)
-      for (int t = g; t < T; t += 16) sm += (double)min(R, P - t * R) * part[(size_t)t * 2 * C + c];
+    if (ok) {  // 8 chunks' loads in flight, summed in the same chunk order as one at a time
+      int t = g;
+      for (; t + 7 * 16 < T; t += 8 * 16) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sm += (double)min(R, P - (t + 16 * u) * R) * v[u];
+      }
+      for (; t < T; t += 16) sm += (double)min(R, P - t * R) * part[(size_t)t * 2 * C + c];
+    }
     red[g][cl] = sm;
     __syncthreads();
     double m = 0.0;
@@ -344,11 +364,26 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
     m /= P;
     __syncthreads();
     double m2 = 0.0;
-    if (ok)
-      for (int t = g; t < T; t += 16) {
+    if (ok) {
+      int t = g;
+      for (; t + 7 * 16 < T; t += 8 * 16) {
+        float mv[8], qv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          mv[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+          qv[u] = part[(size_t)(t + 16 * u) * 2 * C + C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double d = mv[u] - m;
+          m2 += qv[u] + (double)min(R, P - (t + 16 * u) * R) * d * d;
+        }
+      }
+      for (; t < T; t += 16) {
         const double d = part[(size_t)t * 2 * C + c] - m;
         m2 += part[(size_t)t * 2 * C + C + c] + (double)min(R, P - t * R) * d * d;
       }
+    }
     red[g][cl] = m2;
     __syncthreads();
     m2 = 0.0;
@@ -469,11 +504,26 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
-  if (c < C)
-    for (int t = g; t < T; t += 16) {
+  if (c < C) {  // 8 chunks' loads in flight, same summation order
+    int t = g;
+    for (; t + 7 * 16 < T; t += 8 * 16) {
+      float v1[8], v2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v1[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+        v2[u] = part[(size_t)(t + 16 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += v1[u];
+        s2 += v2[u];
+      }
+    }
+    for (; t < T; t += 16) {
       s1 += part[(size_t)t * 2 * C + c];
       s2 += part[(size_t)t * 2 * C + C + c];
     }
+  }
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
   __syncthreads();
@@ -506,6 +556,144 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* __restri
   const float gz = routed_grad(g, y, av, bv, mu, n, h, w, H, W, C, c, pool, fmaf(av, yv - mu, bv));
   const float xh = (yv - mu) * rstd[c];
   dy[i] = av * (gz - c1[c] - xh * c2[c]);
+}
+
+// Vectorised BatchNorm(+ReLU+MaxPool) backward: a thread owns 4 channels of one "unit" — a 2x2 pool window (its 4
+// pre-pool pixels and its pooled gradient are read once, 16-B accesses) or, without a pool, one pixel.  The
+// per-element kernels above re-read the whole window for every pixel (4x the loads) and moved 4 B per access.
+// Same routing (first maximum in row-major window order) and ReLU mask as routed_grad.
+struct Win4 {
+  f32x4 gz[4], xh[4];
+};
+
+__device__ __forceinline__ Win4 window_grads(const float* __restrict__ g, const float* __restrict__ y, f32x4 av,
+                                             f32x4 bv, f32x4 mu, f32x4 rs, size_t pix0, int W, size_t gpix, int C,
+                                             int c, int pool) {
+  Win4 o;
+  const int nq = pool ? 4 : 1;
+  f32x4 yv[4], pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < nq) {
+      const size_t pp = pix0 + (size_t)(q >> 1) * W + (q & 1);
+      yv[q] = *reinterpret_cast<const f32x4*>(y + pp * C + c);
+    } else {
+      yv[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  const f32x4 gv = *reinterpret_cast<const f32x4*>(g + gpix * C + c);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pre[q][e] = fmaf(av[e], yv[q][e] - mu[e], bv[e]);
+      o.xh[q][e] = (yv[q][e] - mu[e]) * rs[e];
+    }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int first = 0;
+    if (pool) {
+      float best = -INFINITY;
+      first = -1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float zz = fmaxf(pre[q][e], 0.f);
+        if (zz > best) { best = zz; first = q; }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o.gz[q][e] = (q < nq && q == first && pre[q][e] > 0.f) ? gv[e] : 0.f;
+  }
+  return o;
+}
+
+// unit u of the tensor -> its first pre-pool pixel and its gradient pixel
+__device__ __forceinline__ void unit_pixels(long u, int H, int W, int pool, size_t& pix0, size_t& gpix) {
+  if (!pool) {
+    pix0 = gpix = (size_t)u;
+    return;
+  }
+  const int Wo = W / 2, Ho = H / 2;
+  const int wo = (int)(u % Wo);
+  const long r = u / Wo;
+  const int ho = (int)(r % Ho);
+  const long n = r / Ho;
+  pix0 = ((size_t)n * H + 2 * ho) * W + 2 * wo;
+  gpix = (size_t)u;
+}
+
+// part[t][0][c] = sum gz, part[t][1][c] = sum gz * xhat over the units of chunk t (R pre-pool pixels, a multiple
+// of 2W when pooled: whole window rows).  256 threads = (C/4 channel quads) x G unit groups, fixed order.
+__global__ void __launch_bounds__(256) bn_bwd_sums4_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                            const float* __restrict__ a, const float* __restrict__ b,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, int N, int H, int W, int C,
+                                                            int pool, int R, float* __restrict__ part) {
+  __shared__ f32x4 red[2][256];
+  const int tid = threadIdx.x, C4 = C / 4, cq = tid % C4, gi = tid / C4, G = 256 / C4;
+  const int c = 4 * cq;
+  const long P = (long)N * H * W;
+  const long r0 = (long)blockIdx.x * R, r1 = min(P, r0 + (long)R);
+  const long u0 = pool ? r0 / 4 : r0, u1 = pool ? r1 / 4 : r1;  // windows: 4 pixels each, chunks window-aligned
+  const f32x4 av = *reinterpret_cast<const f32x4*>(a + c), bv = *reinterpret_cast<const f32x4*>(b + c);
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c), rs = *reinterpret_cast<const f32x4*>(rstd + c);
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  for (long u = u0 + gi; u < u1; u += G) {
+    size_t pix0, gpix;
+    unit_pixels(u, H, W, pool, pix0, gpix);
+    const Win4 w = window_grads(g, y, av, bv, mu, rs, pix0, W, gpix, C, c, pool);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += w.gz[q][e];
+        s2[e] = fmaf(w.gz[q][e], w.xh[q][e], s2[e]);
+      }
+  }
+  red[0][tid] = s1;
+  red[1][tid] = s2;
+  __syncthreads();
+  if (gi == 0) {
+    f32x4 t1 = {0.f, 0.f, 0.f, 0.f}, t2 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < G; ++k) {
+      t1 += red[0][k * C4 + cq];
+      t2 += red[1][k * C4 + cq];
+    }
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * 2 * C + c) = t1;
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * 2 * C + C + c) = t2;
+  }
+}
+
+// dy = a * (gz - c1 - xhat * c2) for every pixel of one unit (window or pixel), 4 channels, 16-B stores.
+__global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                             const float* __restrict__ a, const float* __restrict__ b,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ c1, const float* __restrict__ c2,
+                                                             int N, int H, int W, int C, int pool,
+                                                             float* __restrict__ dy) {
+  const int C4 = C / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long units = pool ? (long)N * (H / 2) * (W / 2) : (long)N * H * W;
+  if (i >= units * C4) return;
+  const int c = (int)(i % C4) * 4;
+  const long u = i / C4;
+  size_t pix0, gpix;
+  unit_pixels(u, H, W, pool, pix0, gpix);
+  const f32x4 av = *reinterpret_cast<const f32x4*>(a + c), bv = *reinterpret_cast<const f32x4*>(b + c);
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c), rs = *reinterpret_cast<const f32x4*>(rstd + c);
+  const f32x4 k1 = *reinterpret_cast<const f32x4*>(c1 + c), k2 = *reinterpret_cast<const f32x4*>(c2 + c);
+  const Win4 w = window_grads(g, y, av, bv, mu, rs, pix0, W, gpix, C, c, pool);
+  const int nq = pool ? 4 : 1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= nq) break;
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = av[e] * (w.gz[q][e] - k1[e] - w.xh[q][e] * k2[e]);
+    const size_t pp = pix0 + (size_t)(q >> 1) * W + (q & 1);
+    *reinterpret_cast<f32x4*>(dy + pp * C + c) = o;
+  }
 }
 
 // ------------------------------------------------------------------ pooling / head
@@ -887,9 +1075,25 @@ DDPX_API int ddpx_f32_bn_apply(const float* y, const float* a, const float* b, c
   return (int)hipGetLastError();
 }
 
+// The vectorised backward kernels need 4-channel quads that split a 256-thread block evenly and (pooled) chunks
+// of whole window rows; DDPX_F32_BN_VEC=0 keeps the per-element kernels (A/B checks).
+static bool bn_vec_ok(int C, int W, int pool, int R) {
+  static const bool on = [] {
+    const char* e = getenv("DDPX_F32_BN_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on && C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 && (!pool || R % (2 * W) == 0);
+}
+
 DDPX_API int ddpx_f32_bn_bwd_sums(const float* g, const float* y, const float* a, const float* b, const float* mean,
                                   const float* rstd, int N, int H, int W, int C, int pool, int R, float* part,
                                   hipStream_t s) {
+  if (pool && (H % 2 || W % 2)) return -1;
+  if (bn_vec_ok(C, W, pool, R)) {
+    hipLaunchKernelGGL(bn_bwd_sums4_kernel, dim3(nblk((long)N * H * W, R)), dim3(256), 0, s, g, y, a, b, mean, rstd,
+                       N, H, W, C, pool, R, part);
+    return (int)hipGetLastError();
+  }
   if (C > 512 || (256 % C && C % 256)) return -1;
   hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nblk((long)N * H * W, R)), dim3(bn_threads(C)), 0, s, g, y, a, b, mean,
                      rstd, N, H, W, C, pool, R, part);
@@ -906,6 +1110,12 @@ DDPX_API int ddpx_f32_bn_bwd_finalize(const float* part, int T, int P, int C, fl
 DDPX_API int ddpx_f32_bn_bwd_apply(const float* g, const float* y, const float* a, const float* b, const float* mean,
                                    const float* rstd, const float* c1, const float* c2, int N, int H, int W, int C,
                                    int pool, float* dy, hipStream_t s) {
+  if (bn_vec_ok(C, W, pool, pool ? 2 * W : 1)) {
+    const long units = pool ? (long)N * (H / 2) * (W / 2) : (long)N * H * W;
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(nblk(units * (C / 4))), dim3(256), 0, s, g, y, a, b, mean, rstd, c1,
+                       c2, N, H, W, C, pool, dy);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk((long)N * H * W * C)), dim3(256), 0, s, g, y, a, b, mean, rstd,
                      c1, c2, N, H, W, C, pool, dy);
   return (int)hipGetLastError();

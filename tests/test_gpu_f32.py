@@ -71,10 +71,10 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-def test_bn_relu_pool_fwd_bwd(gpu, pool):
+@pytest.mark.parametrize("N,H,C", [(16, 8, 128), (8, 4, 512), (4, 32, 64)])
+def test_bn_relu_pool_fwd_bwd(gpu, pool, N, H, C):
     from ddpx.ops import f32
     torch.manual_seed(1)
-    N, H, C = 16, 8, 128
     y = torch.randn(N * H * H, C, device=gpu) * 2 + 0.5
     bn = torch.nn.BatchNorm2d(C).to(gpu)
     with torch.no_grad():
