@@ -199,6 +199,169 @@ gemm_f32_kernel(const Operand A, const Operand B, int M, int N, int K, int kchun
       }
 }
 
+// ------------------------------------------------------------------ LDS-DMA ring variant
+// Same tiles, fragments, MFMA sequence and summation order as gemm_f32_kernel (bitwise-identical results), but the
+// operand tiles go global -> LDS by `buffer_load_dword ... lds` (LDS-DMA: no staging VGPRs, no ds_write pass, no
+// per-element transposing stores) into an S-stage ring with S-1 K-steps in flight, one raw s_barrier per K-step
+// and counted vmcnt waits — the register-staged kernel above exposed a whole K-step of global-load latency per
+// barrier with only 2 waves per SIMD (244 VGPRs) to hide it.
+// LDS images (16-B chunks = 4 floats, lane-linear DMA writes, bank swizzles applied to the SOURCE chunk):
+//   KC operand  [rows][16 k]   row = 64 B, chunk c at c ^ ((row >> 2) & 3)        (conflict-free b32 fragment reads)
+//   OC operand  [16 k][rows]   row = 4*rows B, chunk c at c ^ (4 * (k & 3))        (rows >= 64)
+constexpr unsigned kOOB32 = 0x80000000u;
+
+template <int MODE>
+__device__ __forceinline__ unsigned f32_chunk_off(const Operand& X, int o, int k, int kend) {
+  if (o >= X.O || k >= kend) return kOOB32;
+  if constexpr (MODE == DENSE_KC) return (unsigned)(((size_t)o * X.ld + k) * 4);
+  if constexpr (MODE == DENSE_OC) return (unsigned)(((size_t)k * X.ld + o) * 4);
+  const int m = MODE == IM2COL_KC ? o : k, q = MODE == IM2COL_KC ? k : o;
+  const int n = m >> (X.lh + X.lw);
+  const int h = (m >> X.lw) & ((1 << X.lh) - 1);
+  const int w = m & ((1 << X.lw) - 1);
+  const int rs = q >> X.lc;
+  const int c = q & ((1 << X.lc) - 1);
+  const int r = (rs * 11) >> 5;
+  const int s2 = rs - 3 * r;
+  const int ih = h + X.sgn * (r - 1), iw = w + X.sgn * (s2 - 1);
+  if (rs >= 9 || ih < 0 || iw < 0 || ih >= (1 << X.lh) || iw >= (1 << X.lw)) return kOOB32;
+  return (unsigned)((((((size_t)n << X.lh | ih) << X.lw | iw) << X.lc) | c) * 4);
+}
+
+// Stage one operand tile (ROWS x 16 k) of K-step k0 into an LDS slot: ROWS*64/1024 wave-instructions over 4 waves.
+template <int MODE, int ROWS>
+__device__ __forceinline__ void f32_stage(__amdgpu_buffer_rsrc_t rs, char* slot, const Operand& X, int o0, int k0,
+                                          int kend, int wave, int lane) {
+  constexpr bool KC = (MODE == DENSE_KC || MODE == IM2COL_KC);
+  constexpr int NI = ROWS * 64 / 1024 / 4;  // instructions per wave
+  static_assert(NI * 4 * 1024 == ROWS * 64, "tile must split over 4 waves");
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int inst = j * 4 + wave;
+    const int pc = inst * 64 + lane;  // LDS chunk position
+    unsigned off;
+    if constexpr (KC) {
+      const int row = pc >> 2, cpos = pc & 3;
+      const int kc = cpos ^ ((row >> 2) & 3);
+      off = f32_chunk_off<MODE>(X, o0 + row, k0 + 4 * kc, kend);
+    } else {
+      constexpr int CPR = ROWS / 4;  // chunks per k-row
+      const int krow = pc / CPR, cpos = pc % CPR;
+      const int oc = cpos ^ (4 * (krow & 3));
+      off = f32_chunk_off<MODE>(X, o0 + 4 * oc, k0 + krow, kend);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(slot + inst * 1024), 16, off, 0, 0, 0);
+  }
+}
+
+template <int MODE, int ROWS>
+__device__ __forceinline__ float f32_frag(const char* img, int r, int k) {
+  constexpr bool KC = (MODE == DENSE_KC || MODE == IM2COL_KC);
+  int byte;
+  if constexpr (KC) byte = r * 64 + ((((k >> 2) ^ ((r >> 2) & 3)) << 4) | ((k & 3) << 2));
+  else byte = k * (ROWS * 4) + ((((r >> 2) ^ (4 * (k & 3)))) << 4) + ((r & 3) << 2);
+  return *reinterpret_cast<const float*>(img + byte);
+}
+
+template <int BM, int BN, int AM, int BMD, bool PLAIN, int STAGES>
+__global__ void __launch_bounds__(NT)
+gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C,
+                    int ldc, long split_stride, const float* __restrict__ bias, const float* __restrict__ mask,
+                    int flags, int tiles_m, int tiles_n, unsigned a_bytes, unsigned b_bytes) {
+  constexpr int A_SUB = BM * 64, B_SUB = BN * 64, SLOT = A_SUB + B_SUB;
+  constexpr int LW = (BM + BN) * 64 / 1024 / 4;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = tiles_m * tiles_n;
+  const int z = bid / per, t2 = bid - z * per;
+  const int tm = t2 % tiles_m, tn = t2 / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int k0 = z * kchunk, k1 = min(K, k0 + kchunk);
+  const int nk = (k1 - k0 + BK - 1) / BK;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A.p, 0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B.p, 0, b_bytes, 0x00020000);
+
+  constexpr int FM = BM / 32, FN = BN / 32;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int t) {
+    char* slot = smem + (t % STAGES) * SLOT;
+    f32_stage<AM, BM>(ra, slot, A, m0, k0 + t * BK, k1, wave, lane);
+    f32_stage<BMD, BN>(rb, slot + A_SUB, B, n0, k0 + t * BK, k1, wave, lane);
+  };
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+  const int lr = lane >> 4, lc = lane & 15;
+  for (int it = 0; it < nk; ++it) {
+    const int ahead = min(STAGES - 2, nk - 1 - it);  // younger stages allowed in flight
+    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LW) : "memory");
+    else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + STAGES - 1 < nk) issue(it + STAGES - 1);
+    const char* sa = smem + (it % STAGES) * SLOT;
+    const char* sb = sa + A_SUB;
+    f32x4 part[FM][FN];
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) part[i][j] = acc[i][j];
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = f32_frag<AM, BM>(sa, wm * (BM / 2) + i * 16 + lc, kk + lr);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = f32_frag<BMD, BN>(sb, wn * (BN / 2) + j * 16 + lc, kk + lr);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a[i], b[j], (PLAIN || kk) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (PLAIN) acc[i][j] = part[i][j];
+        else acc[i][j] += part[i][j];
+      }
+  }
+
+  float* out = (flags & F_SPLIT) ? C + (size_t)z * split_stride : C;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * (BM / 2) + i * 16 + lr * 4 + e;
+        const int col = n0 + wn * (BN / 2) + j * 16 + lc;
+        if (row >= M || col >= N) continue;
+        float v = acc[i][j][e];
+        const size_t o = (size_t)row * ldc + col;
+        if (!(flags & F_SPLIT)) {
+          if (bias) v += bias[col];
+          if (flags & F_ACCUM) v += out[o];
+          if (flags & F_RELU) v = fmaxf(v, 0.f);
+          if (mask && !(mask[o] > 0.f)) v = 0.f;
+        }
+        out[o] = v;
+      }
+}
+
 // Summation order of the f32 core (DDPX_F32_SUM=plain|blocked|auto, default auto).  The bar is the stock fp32
 // libraries' own error vs fp64 on the same inputs (tests/test_gpu_f32.py::test_error_no_worse_than_stock,
 // MI355X: profiles/r3_f32): the plain chain matches hipBLASLt on the MLP's fc1 (1.15e-6 vs 1.15e-6 rel-L2)
@@ -214,16 +377,38 @@ static int f32_sum_mode() {  // 0 auto, 1 plain, 2 blocked
   return v;
 }
 
+// Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring, default) | reg (register-staged, double-buffered LDS).
+static int g_f32_staging = -1;  // -1: from the environment; ddpx_f32_set_staging() overrides (tests, A/B)
+static bool f32_dma() {
+  if (g_f32_staging < 0) {
+    const char* e = getenv("DDPX_F32_STAGING");
+    g_f32_staging = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return g_f32_staging == 1;
+}
+constexpr int kF32Stages = 4;
+
 template <int BM, int BN, int AM, int BMD>
 static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
-                   long split_stride, const float* bias, const float* mask, int flags, hipStream_t s) {
+                   long split_stride, const float* bias, const float* mask, int flags, hipStream_t s,
+                   unsigned a_bytes, unsigned b_bytes) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   int kchunk = (K + splits - 1) / splits;
   kchunk = (kchunk + BK - 1) / BK * BK;
   const int nwg = tm * tn * splits;
   const int mode = f32_sum_mode();
   const bool conv = AM == IM2COL_KC || BMD == IM2COL_OC;
-  if (mode == 1 || (mode == 0 && !conv))
+  const bool plain = mode == 1 || (mode == 0 && !conv);
+  if (f32_dma() && a_bytes && b_bytes) {
+    if (plain)
+      hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
+                         N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+    else
+      hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,
+                         M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+    return;
+  }
+  if (plain)
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, AM, BMD, true>), dim3(nwg), dim3(NT), 0, s, A, B, M, N, K, kchunk, C,
                        ldc, split_stride, bias, mask, flags, tm, tn);
   else
@@ -233,12 +418,22 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
 
 template <int AM, int BMD>
 static void dispatch_tile(int tile, const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C,
-                          int ldc, long ss, const float* bias, const float* mask, int flags, hipStream_t s) {
+                          int ldc, long ss, const float* bias, const float* mask, int flags, hipStream_t s,
+                          unsigned ab, unsigned bb) {
   switch (tile) {
-    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
-    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
-    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s); break;
+    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
+    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
+    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
   }
+}
+
+// Bytes an operand spans (the LDS-DMA buffer resource's bound; 0 = too large for 32-bit offsets: register path)
+static unsigned operand_bytes(int mode, int ld, int O, int K, int C, int npix) {
+  size_t n;
+  if (mode == DENSE_KC) n = ((size_t)(O - 1) * ld + K) * 4;
+  else if (mode == DENSE_OC) n = ((size_t)(K - 1) * ld + O) * 4;
+  else n = (size_t)npix * C * 4;
+  return n >= 0x80000000ull ? 0u : (unsigned)n;
 }
 
 // ------------------------------------------------------------------ conv helpers
@@ -1006,6 +1201,7 @@ DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const 
     return -4;
   if (splits > 1) flags |= F_SPLIT;
   Operand A{a, lda, M, lc, lh, lw, sgn}, B{b, ldb, N, lc, lh, lw, sgn};
+  const unsigned ab = operand_bytes(amode, lda, M, K, gc, M), bb = operand_bytes(bmode, ldb, N, K, gc, K);
   if (tile < 0) {
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
     tile = N <= 64 ? 1 : (t128 >= 512 ? 0 : 2);
@@ -1013,19 +1209,24 @@ DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const 
   const int key = amode * 4 + bmode;
   switch (key) {
     case DENSE_KC * 4 + DENSE_KC:
-      dispatch_tile<DENSE_KC, DENSE_KC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      dispatch_tile<DENSE_KC, DENSE_KC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s, ab,
+                                          bb);
       break;
     case DENSE_KC * 4 + DENSE_OC:
-      dispatch_tile<DENSE_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      dispatch_tile<DENSE_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s, ab,
+                                          bb);
       break;
     case DENSE_OC * 4 + DENSE_OC:
-      dispatch_tile<DENSE_OC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      dispatch_tile<DENSE_OC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s, ab,
+                                          bb);
       break;
     case IM2COL_KC * 4 + DENSE_OC:
-      dispatch_tile<IM2COL_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      dispatch_tile<IM2COL_KC, DENSE_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s, ab,
+                                          bb);
       break;
     case DENSE_OC * 4 + IM2COL_OC:
-      dispatch_tile<DENSE_OC, IM2COL_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s);
+      dispatch_tile<DENSE_OC, IM2COL_OC>(tile, A, B, M, N, K, splits, c, ldc, split_stride, bias, mask, flags, s, ab,
+                                          bb);
       break;
     default:
       return -5;
@@ -1164,4 +1365,11 @@ DDPX_API int ddpx_f32_colsum(const float* x, int M, int N, float* out, int accum
 DDPX_API int ddpx_f32_nchw_flatten(const float* x, int N, int S, int C, int backward, float* out, hipStream_t s) {
   hipLaunchKernelGGL(nchw_flatten_kernel, dim3(nblk((long)N * S * C)), dim3(256), 0, s, x, N, S, C, backward, out);
   return (int)hipGetLastError();
+}
+
+// 1 = LDS-DMA ring GEMM core, 0 = register-staged; returns the previous setting.
+DDPX_API int ddpx_f32_set_staging(int dma) {
+  const int prev = f32_dma() ? 1 : 0;
+  g_f32_staging = dma ? 1 : 0;
+  return prev;
 }

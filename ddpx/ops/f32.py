@@ -36,6 +36,7 @@ for _sig in (
         ("ddpx_f32_head_fwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P),
         ("ddpx_f32_head_bwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _I, _F, _P),
         ("ddpx_f32_nchw_flatten", _I, _P, _I, _I, _I, _I, _P, _P),
+        ("ddpx_f32_set_staging", _I, _I),
         ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
 ):
@@ -57,6 +58,12 @@ def _req(c, msg):
 def _f32(t, name):
     _req(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous(), f"{name} must be contiguous fp32 on GPU")
     _req(t.data_ptr() % 16 == 0, f"{name} must be 16-B aligned")
+
+
+def set_staging(dma: bool) -> bool:
+    """GEMM operand staging of the f32 core: LDS-DMA ring (True, default) or register-staged (False).
+    Returns the previous setting."""
+    return bool(native.kernels().ddpx_f32_set_staging(int(bool(dma))))
 
 
 def _call(name, *args):

@@ -397,3 +397,59 @@ def test_deepnn_fp32_trains_like_torch(gpu):
     for (n, p), (_, q) in zip(native.named_parameters(), ref.named_parameters()):
         err = (p.detach().double() - q.detach().double()).norm().item()
         assert err < 5e-3 * max(1.0, q.detach().double().norm().item()), n
+
+
+@pytest.mark.parametrize("case", ["fwd", "dgrad", "wgrad", "lin_fwd", "lin_dgrad", "lin_wgrad", "ragged"])
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_f32_dma_core_bitwise_equals_register_core(gpu, case, tile):
+    """The LDS-DMA ring GEMM (default) runs the register-staged kernel's fragment / MFMA / summation sequence:
+    results must be bitwise equal for every operand mode, tile and split."""
+    from ddpx.ops import f32 as Fk
+    torch.manual_seed(21)
+    if case in ("fwd", "dgrad", "wgrad"):
+        N, H, C, Co = 4, 8, 64, 128
+        x = torch.randn(N, H, H, C, device=gpu)
+        dy = torch.randn(N * H * H, Co, device=gpu)
+        w = torch.randn(9 * C * Co, device=gpu)
+        if case == "fwd":
+            args = (Fk.IM2COL_KC, x, 0, Fk.DENSE_OC, w, Co, N * H * H, Co, 9 * C)
+            kw = dict(geom=(C, H, H, 1))
+            shape = (N * H * H, Co)
+        elif case == "dgrad":
+            args = (Fk.IM2COL_KC, dy, 0, Fk.DENSE_OC, w, C, N * H * H, C, 9 * Co)
+            kw = dict(geom=(Co, H, H, -1))
+            shape = (N * H * H, C)
+        else:
+            S = 3
+            args = (Fk.DENSE_OC, dy, Co, Fk.IM2COL_OC, x, 0, Co, 9 * C, N * H * H)
+            kw = dict(geom=(C, H, H, 1), splits=S, split_stride=Co * 9 * C)
+            shape = (S, Co, 9 * C)
+    else:
+        M, Nn, K = (256, 192, 320) if case != "ragged" else (200, 132, 516)
+        a = torch.randn(M, K, device=gpu)
+        b = torch.randn(Nn, K, device=gpu)
+        if case in ("lin_fwd", "ragged"):
+            args = (Fk.DENSE_KC, a, K, Fk.DENSE_KC, b, K, M, Nn, K)
+            shape = (M, Nn)
+        elif case == "lin_dgrad":
+            bt = torch.randn(K, Nn, device=gpu)
+            args = (Fk.DENSE_KC, a, K, Fk.DENSE_OC, bt, Nn, M, Nn, K)
+            shape = (M, Nn)
+        else:
+            at = torch.randn(K, M, device=gpu)
+            bt = torch.randn(K, Nn, device=gpu)
+            args = (Fk.DENSE_OC, at, M, Fk.DENSE_OC, bt, Nn, M, Nn, K)
+            shape = (M, Nn)
+        kw = {}
+    outs = []
+    prev = Fk.set_staging(True)
+    try:
+        for dma in (True, False):
+            Fk.set_staging(dma)
+            o = torch.full(shape, float("nan"), device=gpu)
+            Fk.gemm(*args, o, tile=tile, **kw)
+            outs.append(o)
+    finally:
+        Fk.set_staging(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
