@@ -377,12 +377,13 @@ static int f32_sum_mode() {  // 0 auto, 1 plain, 2 blocked
   return v;
 }
 
-// Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring, default) | reg (register-staged, double-buffered LDS).
+// Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring) | reg (register-staged, double-buffered LDS; default until
+// the ring is measured faster on MI355X).
 static int g_f32_staging = -1;  // -1: from the environment; ddpx_f32_set_staging() overrides (tests, A/B)
 static bool f32_dma() {
   if (g_f32_staging < 0) {
     const char* e = getenv("DDPX_F32_STAGING");
-    g_f32_staging = (e && e[0] == 'r') ? 0 : 1;
+    g_f32_staging = (e && e[0] == 'd') ? 1 : 0;
   }
   return g_f32_staging == 1;
 }

@@ -61,7 +61,8 @@ def _f32(t, name):
 
 
 def set_staging(dma: bool) -> bool:
-    """GEMM operand staging of the f32 core: LDS-DMA ring (True, default) or register-staged (False).
+    """GEMM operand staging of the f32 core: LDS-DMA ring (True; DDPX_F32_STAGING=dma) or register-staged (False,
+    the default).
     Returns the previous setting."""
     return bool(native.kernels().ddpx_f32_set_staging(int(bool(dma))))
 
