@@ -263,7 +263,9 @@ __device__ __forceinline__ float f32_frag(const char* img, int r, int k) {
   return *reinterpret_cast<const float*>(img + byte);
 }
 
-template <int BM, int BN, int AM, int BMD, bool PLAIN, int STAGES>
+// KB (blocked summation only): K-steps of 16 per fresh block accumulator.  1 = the register-staged kernel's order
+// (bitwise equal); 2 = 32-k blocks, half the block adds (DDPX_F32_BLOCK=2).
+template <int BM, int BN, int AM, int BMD, bool PLAIN, int STAGES, int KB = 1>
 __global__ void __launch_bounds__(NT)
 gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C,
                     int ldc, long split_stride, const float* __restrict__ bias, const float* __restrict__ mask,
@@ -300,16 +302,8 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s);
   const int lr = lane >> 4, lc = lane & 15;
-  for (int it = 0; it < nk; ++it) {
-    const int ahead = min(STAGES - 2, nk - 1 - it);  // younger stages allowed in flight
-    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LW) : "memory");
-    else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (it + STAGES - 1 < nk) issue(it + STAGES - 1);
-    const char* sa = smem + (it % STAGES) * SLOT;
-    const char* sb = sa + A_SUB;
+  constexpr int KBE = PLAIN ? 1 : KB;
+  for (int it0 = 0; it0 < nk; it0 += KBE) {
     f32x4 part[FM][FN];
     if constexpr (PLAIN) {
 #pragma unroll
@@ -318,18 +312,32 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
         for (int j = 0; j < FN; ++j) part[i][j] = acc[i][j];
     }
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      float a[FM], b[FN];
+    for (int u = 0; u < KBE; ++u) {
+      const int it = it0 + u;
+      if (KBE > 1 && it >= nk) break;
+      const int ahead = min(STAGES - 2, nk - 1 - it);  // younger stages allowed in flight
+      if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LW) : "memory");
+      else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it + STAGES - 1 < nk) issue(it + STAGES - 1);
+      const char* sa = smem + (it % STAGES) * SLOT;
+      const char* sb = sa + A_SUB;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = f32_frag<AM, BM>(sa, wm * (BM / 2) + i * 16 + lc, kk + lr);
+      for (int kk = 0; kk < BK; kk += 4) {
+        float a[FM], b[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = f32_frag<BMD, BN>(sb, wn * (BN / 2) + j * 16 + lc, kk + lr);
+        for (int i = 0; i < FM; ++i) a[i] = f32_frag<AM, BM>(sa, wm * (BM / 2) + i * 16 + lc, kk + lr);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j) b[j] = f32_frag<BMD, BN>(sb, wn * (BN / 2) + j * 16 + lc, kk + lr);
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[i], b[j], (PLAIN || kk) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                a[i], b[j], (PLAIN || u || kk) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -388,6 +396,13 @@ static bool f32_dma() {
   return g_f32_staging == 1;
 }
 constexpr int kF32Stages = 4;
+static int f32_block() {  // DDPX_F32_BLOCK=2: 32-k summation blocks on the LDS-DMA core
+  static const int v = [] {
+    const char* e = getenv("DDPX_F32_BLOCK");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  return v;
+}
 
 template <int BM, int BN, int AM, int BMD>
 static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
@@ -404,6 +419,9 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
     if (plain)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
                          N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+    else if (f32_block() == 2)
+      hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 2>), dim3(nwg), dim3(NT), 0, s, A,
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
     else
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,
                          M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
