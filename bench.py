@@ -76,9 +76,12 @@ def parse(argv=None):
                         "opening each step; same batches, same seeds, one augment per step.  Default 0: the "
                         "side-stream fork/join inside the graph costs more than the 8 us augment "
                         "(0.2753-0.2782 vs 0.2521-0.2531 ms/step, profiles/r3_val/NOTES.md)")
-    p.add_argument("--graph_steps", type=int, default=1,
+    p.add_argument("--graph_steps", type=int, default=None,
                    help="training steps per captured HIP graph (the launch gap between replays is paid once "
-                        "per graph); the timed region still runs exactly --steps steps")
+                        "per graph); the timed region still runs exactly --steps steps, every one of them a full "
+                        "step (batch gather + augment, LR advance, forward, backward, optimizer).  Default: "
+                        "min(20, --steps) (toy MLP, 20-step window: 0.2471-0.2542 ms vs 0.2566-0.2610 for one "
+                        "step per graph; 200 steps in graphs of 5: 0.2339 vs 0.2368 ms, profiles/r4_graphsteps)")
     p.add_argument("--overlap_optimizer", type=int, default=None,
                    help="1: per-bucket optimizer as each collective lands (default 1 for N>1)")
     p.add_argument("--shard_optimizer", type=int, default=None,
@@ -227,6 +230,8 @@ def make_data(args, device, rank, world, layout=None):
 
 
 def resolve_defaults(args, world):
+    if args.graph_steps is None:
+        args.graph_steps = max(1, min(20, args.steps))
     if args.hidden is None:
         args.hidden = 16384 if args.model == "mlp_wide" else 4096
     multi = world > 1 or args.ddp_single
@@ -592,6 +597,7 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
         a = argparse.Namespace(**vars(args))
         apply(a, plan)
         a.calibrate = False
+        a.graph_steps = 1  # trials replay one step at a time: no multi-step graph to capture
         eng = make_runner(a, device, world, loader, idx_all, full, comm)
         k = [0]
 

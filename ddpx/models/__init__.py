@@ -13,15 +13,18 @@ __all__ = ["VGG", "DeepNN", "MLP", "build_model", "native_kernels_for"]
 def native_kernels_for(name: str, dtype: str, kernels: str = "auto") -> bool:
     """Whether ``build_model`` puts ``name`` on the hand-written kernels for ``kernels`` = auto|native|torch.
 
-    auto = native everywhere except VGG at fp32: there MIOpen's fp32 convolutions (19.5 ms per step) beat the
-    exact-f32 MFMA implicit-GEMM path (21.2-23.7 ms, profiles/r3_f32), so the reference's own precision runs its
-    convolutions, BatchNorm and pooling on torch/MIOpen under the ddpx engine (flat store, fused flat SGD,
-    native DDP); ``--kernels native`` selects the exact-f32 kernels."""
+    auto = native everywhere except the CNNs at fp32: there MIOpen's fp32 convolutions (Winograd F(2,3) for the
+    forward / data gradient: VGG 19.44 ms per step, DeepNN 4.36 ms) beat the exact-f32 MFMA implicit-GEMM path
+    (VGG 21.28 ms, DeepNN 5.46 ms, profiles/r4_f32), so the reference's own precision runs its convolutions,
+    BatchNorm and pooling on torch/MIOpen under the ddpx engine (flat store, fused flat SGD, native DDP);
+    ``--kernels native`` selects the exact-f32 kernels."""
     if kernels == "torch":
         return False
     if kernels == "native":
         return True
-    return not (name == "vgg" and dtype == "fp32")
+    # measured (profiles/r4_f32): DeepNN fp32 native 5.457 ms vs stock 4.357 ms per step (MIOpen's Winograd
+    # convolutions), so auto keeps torch/MIOpen there too until the native path wins
+    return not (name in ("vgg", "deepnn") and dtype == "fp32")
 
 
 def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "auto",
