@@ -324,20 +324,25 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
       if (it + STAGES - 1 < nk) issue(it + STAGES - 1);
       const char* sa = smem + (it % STAGES) * SLOT;
       const char* sb = sa + A_SUB;
+      // every fragment of the K-step read up front (one LDS-latency exposure per K-step; reading them kk by kk
+      // into reused registers made hipcc wait lgkmcnt(0) every 8 MFMAs)
+      float a[BK / 4][FM], b[BK / 4][FN];
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 4) {
-        float a[FM], b[FN];
+      for (int q = 0; q < BK / 4; ++q) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) a[i] = f32_frag<AM, BM>(sa, wm * (BM / 2) + i * 16 + lc, kk + lr);
+        for (int i = 0; i < FM; ++i) a[q][i] = f32_frag<AM, BM>(sa, wm * (BM / 2) + i * 16 + lc, 4 * q + lr);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) b[j] = f32_frag<BMD, BN>(sb, wn * (BN / 2) + j * 16 + lc, kk + lr);
+        for (int j = 0; j < FN; ++j) b[q][j] = f32_frag<BMD, BN>(sb, wn * (BN / 2) + j * 16 + lc, 4 * q + lr);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep every read issued before the first MFMA (counted lgkmcnt waits)
+#pragma unroll
+      for (int q = 0; q < BK / 4; ++q)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                a[i], b[j], (PLAIN || u || kk) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      }
+                a[q][i], b[q][j], (PLAIN || u || q) ? part[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)

@@ -347,8 +347,8 @@ def test_deepnn_fp32_dropout_semantics(gpu):
     live = (a0 > 0).float()
     frac = (mask.sum() / live.sum()).item()
     assert 0.85 < frac < 0.95, frac
-    kept = d0[d0 > 0] / a0[d0 > 0]
-    assert torch.allclose(kept, torch.full_like(kept, 1 / 0.9), rtol=1e-5)
+    k = d0 > 0  # kept elements carry a0 / (1 - p) (a0 from torch: fp32 round-off apart from the native one)
+    assert torch.allclose(d0[k], a0[k].detach() * scale, rtol=1e-4, atol=1e-6)
     rl = F.cross_entropy(ref.classifier[3](a0 * mask * scale), t)
     assert abs(loss.item() - rl.item()) < 1e-5 * max(1.0, rl.item())
     rl.backward()
