@@ -231,7 +231,8 @@ def make_data(args, device, rank, world, layout=None):
 
 def resolve_defaults(args, world):
     if args.graph_steps is None:
-        args.graph_steps = max(1, min(20, args.steps))
+        # (--prefetch_batch alternates two single-step graphs)
+        args.graph_steps = 1 if args.prefetch_batch else max(1, min(20, args.steps))
     if args.hidden is None:
         args.hidden = 16384 if args.model == "mlp_wide" else 4096
     multi = world > 1 or args.ddp_single

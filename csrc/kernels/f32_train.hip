@@ -404,7 +404,7 @@ constexpr int kF32Stages = 4;
 static int f32_block() {  // DDPX_F32_BLOCK=2: 32-k summation blocks on the LDS-DMA core
   static const int v = [] {
     const char* e = getenv("DDPX_F32_BLOCK");
-    return (e && e[0] == '2') ? 2 : 1;
+    return (e && e[0] == '2') ? 2 : (e && e[0] == '4') ? 4 : 1;
   }();
   return v;
 }
@@ -426,6 +426,9 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
                          N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
     else if (f32_block() == 2)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 2>), dim3(nwg), dim3(NT), 0, s, A,
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+    else if (f32_block() == 4)
+      hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 4>), dim3(nwg), dim3(NT), 0, s, A,
                          B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
     else
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,

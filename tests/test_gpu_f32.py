@@ -277,7 +277,8 @@ def test_error_no_worse_than_stock(gpu, case):
         ref, stock = ref.permute(0, 2, 3, 1), stock.permute(0, 2, 3, 1)
         ours = ours.permute(0, 2, 3, 1)
     e_stock, e_ours = _err_vs_fp64(stock, ref), _err_vs_fp64(ours, ref)
-    rec = {"case": case, "stock": e_stock, "native": e_ours, "sum": os.environ.get("DDPX_F32_SUM", "plain")}
+    rec = {"case": case, "stock": e_stock, "native": e_ours, "sum": os.environ.get("DDPX_F32_SUM", "auto"),
+           "staging": os.environ.get("DDPX_F32_STAGING", "reg"), "block": os.environ.get("DDPX_F32_BLOCK", "1")}
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/f32_error.jsonl", "a") as f:
         f.write(json.dumps(rec) + "\n")
