@@ -136,8 +136,9 @@ def test_augment_nhwc4_f32_matches_cpu(gpu):
     assert torch.equal(yg.cpu(), yc)
 
 
-def _train_pair(gpu, name, steps, lr=0.05):
-    """(native fp32 losses, torch fp32 losses, native model, torch model) from one init."""
+def _train_pair(gpu, name, steps, lr=0.05, fp64=None):
+    """(native fp32 losses, torch fp32 losses, native model, torch model) from one init; with ``fp64`` = a list,
+    an fp64 torch copy trained on the same batches is appended to it (the arbiter for both fp32 runs)."""
     import copy
 
     import ddpx
@@ -150,6 +151,12 @@ def _train_pair(gpu, name, steps, lr=0.05):
     ddpx.prepare_model(native, gpu)
     opt = SGD(native.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
     ropt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    r64 = o64 = None
+    if fp64 is not None:
+        r64 = copy.deepcopy(ref).double()
+        r64.compute_dtype = torch.float64
+        o64 = torch.optim.SGD(r64.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+        fp64.append(r64)
     gen = torch.Generator().manual_seed(5)
     ln, lt = [], []
     for _ in range(steps):
@@ -166,6 +173,10 @@ def _train_pair(gpu, name, steps, lr=0.05):
         rl.backward()
         ropt.step()
         lt.append(rl.item())
+        if r64 is not None:
+            o64.zero_grad()
+            F.cross_entropy(r64(x.double()), y).backward()
+            o64.step()
     return ln, lt, native, ref
 
 
@@ -213,18 +224,28 @@ def test_native_fp32_gradients_match_torch_fp32(gpu, name):
 
 @pytest.mark.parametrize("name", ["vgg", "mlp"])
 def test_native_fp32_training_tracks_torch_fp32(gpu, name):
-    ln, lt, native, ref = _train_pair(gpu, name, steps=5, lr=0.01)
-    # exact-f32 kernels: the first loss agrees to round-off, later ones to fp32 trajectory drift
+    r64 = []
+    ln, lt, native, ref = _train_pair(gpu, name, steps=5, lr=0.01, fp64=r64)
+    r64 = r64[0]
+    # fp32 kernels: the first loss agrees to round-off, later ones to fp32 trajectory drift
     assert abs(ln[0] - lt[0]) < 1e-4 * max(1.0, abs(lt[0])), (ln, lt)
     for a, b in zip(ln, lt):
         assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (ln, lt)
-    sd, rsd = native.state_dict(), ref.state_dict()
+    sd, rsd, sd64 = native.state_dict(), ref.state_dict(), r64.state_dict()
     assert sd.keys() == rsd.keys()
+    bad = []
     for k in sd:
         if sd[k].is_floating_point():
-            # matrices relative; BatchNorm / bias vectors start at 0 or 1 and move by ~lr*grad, so absolute
-            err = (sd[k].double() - rsd[k].double()).norm().item()
-            assert err < 5e-3 * max(1.0, rsd[k].double().norm().item()), (k, err)
+            # matrices relative; BatchNorm / bias vectors start at 0 or 1 and move by ~lr*grad, so absolute.
+            # Max-pool routing flips make any two fp32 trajectories drift apart; the bar is the fp64 run: the
+            # native weights may be no further from it than twice torch fp32's own drift (or 5e-3 relative).
+            scale = max(1.0, rsd[k].double().norm().item())
+            e_nat = (sd[k].double() - sd64[k].double()).norm().item()
+            e_tor = (rsd[k].double() - sd64[k].double()).norm().item()
+            print(f"{k}: native-fp64 {e_nat / scale:.2e}  torch32-fp64 {e_tor / scale:.2e}")
+            if not e_nat < max(5e-3 * scale, 2.0 * e_tor):
+                bad.append((k, e_nat / scale, e_tor / scale))
+    assert not bad, bad
 
 
 def test_vgg_fp32_eval_logits(gpu):
