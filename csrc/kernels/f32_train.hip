@@ -269,7 +269,8 @@ template <int BM, int BN, int AM, int BMD, bool PLAIN, int STAGES, int KB = 1>
 __global__ void __launch_bounds__(NT)
 gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C,
                     int ldc, long split_stride, const float* __restrict__ bias, const float* __restrict__ mask,
-                    int flags, int tiles_m, int tiles_n, unsigned a_bytes, unsigned b_bytes) {
+                    int flags, int tiles_m, int tiles_n, unsigned a_bytes, unsigned b_bytes,
+                    float* __restrict__ stats) {
   constexpr int A_SUB = BM * 64, B_SUB = BN * 64, SLOT = A_SUB + B_SUB;
   constexpr int LW = (BM + BN) * 64 / 1024 / 4;  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
@@ -353,6 +354,58 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
       }
   }
 
+  if (stats) {
+    // BatchNorm training statistics of this output tile, straight from the accumulators (the conv forward's raw
+    // output): per column, the tile mean and M2 over its valid rows -> stats[tile_m][0 / 1][col] (the chunk
+    // statistics bn_finalize merges with Chan's formula; chunk = BM rows).  Fixed reduction order: the 4 lanes
+    // sharing a column (xor 16, 32), then the two row-halves of the tile in order.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done with the LDS ring: reuse it
+    float* red = reinterpret_cast<float*>(smem);  // [4][BN]: sums of the 2 row halves, then their M2
+    const int rows_t = min(BM, M - m0);
+    float mean[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m0 + wm * (BM / 2) + i * 16 + lr * 4 + e < M) sm += acc[i][j][e];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      if (lr == 0) red[wm * BN + wn * (BN / 2) + j * 16 + lc] = sm;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * (BN / 2) + j * 16 + lc;
+      mean[j] = (red[col] + red[BN + col]) / (float)rows_t;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m0 + wm * (BM / 2) + i * 16 + lr * 4 + e < M) {
+            const float d = acc[i][j][e] - mean[j];
+            q = fmaf(d, d, q);
+          }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lr == 0) red[(2 + wm) * BN + col] = q;
+    }
+    __syncthreads();
+    if (wm == 0 && lr == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + lc;
+        if (n0 + col < N) {
+          stats[(size_t)tm * 2 * N + n0 + col] = mean[j];
+          stats[(size_t)tm * 2 * N + N + n0 + col] = red[2 * BN + col] + red[3 * BN + col];
+        }
+      }
+    }
+  }
   float* out = (flags & F_SPLIT) ? C + (size_t)z * split_stride : C;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -390,29 +443,35 @@ static int f32_sum_mode() {  // 0 auto, 1 plain, 2 blocked
   return v;
 }
 
-// Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring) | reg (register-staged, double-buffered LDS; default until
-// the ring is measured faster on MI355X).
+// Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring, default) | reg (register-staged, double-buffered LDS).
 static int g_f32_staging = -1;  // -1: from the environment; ddpx_f32_set_staging() overrides (tests, A/B)
 static bool f32_dma() {
   if (g_f32_staging < 0) {
     const char* e = getenv("DDPX_F32_STAGING");
-    g_f32_staging = (e && e[0] == 'd') ? 1 : 0;
+    g_f32_staging = (e && e[0] == 'r') ? 0 : 1;
   }
   return g_f32_staging == 1;
 }
 constexpr int kF32Stages = 4;
-static int f32_block() {  // DDPX_F32_BLOCK=2: 32-k summation blocks on the LDS-DMA core
-  static const int v = [] {
+// Summation block of the LDS-DMA core's blocked mode, in 16-k K-steps (DDPX_F32_BLOCK=1|2|4, default 4): a fresh
+// block accumulator per 64 k, added to the running sum.  Measured on MI355X (profiles/r4_f32): the rounding
+// error of a length-K dot product is smallest near blocks of sqrt(K) (~64 at VGG's K = 2304-4608: conv7 / conv4
+// outputs 0.26x MIOpen's own error vs fp64, against 0.42x / 0.37x with 16-k blocks), and the adds of fewer
+// blocks cost less (VGG fp32 step 19.07 ms vs 21.35 ms with 16-k blocks).  1 = the register-staged kernel's
+// exact summation order (bitwise equal to it).
+static int g_f32_block = -1;
+static int f32_block() {
+  if (g_f32_block < 0) {
     const char* e = getenv("DDPX_F32_BLOCK");
-    return (e && e[0] == '2') ? 2 : (e && e[0] == '4') ? 4 : 1;
-  }();
-  return v;
+    g_f32_block = (e && e[0] == '1') ? 1 : (e && e[0] == '2') ? 2 : 4;
+  }
+  return g_f32_block;
 }
 
 template <int BM, int BN, int AM, int BMD>
 static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
                    long split_stride, const float* bias, const float* mask, int flags, hipStream_t s,
-                   unsigned a_bytes, unsigned b_bytes) {
+                   unsigned a_bytes, unsigned b_bytes, float* stats = nullptr) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   int kchunk = (K + splits - 1) / splits;
   kchunk = (kchunk + BK - 1) / BK * BK;
@@ -423,16 +482,16 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
   if (f32_dma() && a_bytes && b_bytes) {
     if (plain)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
-                         N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+                         N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     else if (f32_block() == 2)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 2>), dim3(nwg), dim3(NT), 0, s, A,
-                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     else if (f32_block() == 4)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 4>), dim3(nwg), dim3(NT), 0, s, A,
-                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     else
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,
-                         M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes);
+                         M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     return;
   }
   if (plain)
@@ -446,11 +505,11 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
 template <int AM, int BMD>
 static void dispatch_tile(int tile, const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C,
                           int ldc, long ss, const float* bias, const float* mask, int flags, hipStream_t s,
-                          unsigned ab, unsigned bb) {
+                          unsigned ab, unsigned bb, float* stats = nullptr) {
   switch (tile) {
-    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
-    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
-    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb); break;
+    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
+    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
+    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
   }
 }
 
@@ -1192,6 +1251,11 @@ __global__ void __launch_bounds__(256) nchw_flatten_kernel(const float* __restri
   else out[f] = x[i];
 }
 
+static int auto_tile(int M, int N, int splits) {
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
+  return N <= 64 ? 1 : (t128 >= 512 ? 0 : 2);
+}
+
 static int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -1229,10 +1293,7 @@ DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const 
   if (splits > 1) flags |= F_SPLIT;
   Operand A{a, lda, M, lc, lh, lw, sgn}, B{b, ldb, N, lc, lh, lw, sgn};
   const unsigned ab = operand_bytes(amode, lda, M, K, gc, M), bb = operand_bytes(bmode, ldb, N, K, gc, K);
-  if (tile < 0) {
-    const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
-    tile = N <= 64 ? 1 : (t128 >= 512 ? 0 : 2);
-  }
+  if (tile < 0) tile = auto_tile(M, N, splits);
   const int key = amode * 4 + bmode;
   switch (key) {
     case DENSE_KC * 4 + DENSE_KC:
@@ -1394,9 +1455,35 @@ DDPX_API int ddpx_f32_nchw_flatten(const float* x, int N, int S, int C, int back
   return (int)hipGetLastError();
 }
 
+// Summation block (1, 2 or 4 K-steps of 16) of the LDS-DMA core; returns the previous setting.
+DDPX_API int ddpx_f32_set_block(int kb) {
+  const int prev = f32_block();
+  g_f32_block = (kb == 1 || kb == 2) ? kb : 4;
+  return prev;
+}
+
 // 1 = LDS-DMA ring GEMM core, 0 = register-staged; returns the previous setting.
 DDPX_API int ddpx_f32_set_staging(int dma) {
   const int prev = f32_dma() ? 1 : 0;
   g_f32_staging = dma ? 1 : 0;
   return prev;
+}
+
+// Forward 3x3 convolution y [N*H*W][Co] = conv(x NHWC [N][H][W][C], wf) on the LDS-DMA core with the BatchNorm
+// tile statistics emitted by its epilogue: stats[tiles_m][2][Co] (tile mean, M2).  Returns the tile's row count
+// (the chunk size bn_finalize needs), or a negative code when the fused path does not apply (register-staged
+// core selected, or an operand beyond 32-bit offsets): the caller then runs the separate statistics pass.
+DDPX_API int ddpx_f32_conv_fwd_stats(const float* x, const float* wf, float* y, int N, int H, int W, int C, int Co,
+                                     float* stats, hipStream_t s) {
+  if (!f32_dma()) return -10;
+  const int lc = ilog2(C), lh = ilog2(H), lw = ilog2(W);
+  if (lc < 2 || lh < 0 || lw < 0 || Co % 4) return -2;
+  const int M = N * H * W, K = 9 * C;
+  Operand A{x, 0, M, lc, lh, lw, 1}, B{wf, Co, Co, lc, lh, lw, 1};
+  const unsigned ab = operand_bytes(IM2COL_KC, 0, M, K, C, M), bb = operand_bytes(DENSE_OC, Co, Co, K, C, K);
+  if (!ab || !bb) return -11;
+  const int tile = auto_tile(M, Co, 1);
+  dispatch_tile<IM2COL_KC, DENSE_OC>(tile, A, B, M, Co, K, 1, y, Co, 0, nullptr, nullptr, 0, s, ab, bb, stats);
+  const int err = (int)hipGetLastError();
+  return err ? -err : (tile == 2 ? 64 : 128);
 }

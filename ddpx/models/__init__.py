@@ -13,18 +13,18 @@ __all__ = ["VGG", "DeepNN", "MLP", "build_model", "native_kernels_for"]
 def native_kernels_for(name: str, dtype: str, kernels: str = "auto") -> bool:
     """Whether ``build_model`` puts ``name`` on the hand-written kernels for ``kernels`` = auto|native|torch.
 
-    auto = native everywhere except the CNNs at fp32: there MIOpen's fp32 convolutions (Winograd F(2,3) for the
-    forward / data gradient: VGG 19.44 ms per step, DeepNN 4.36 ms) beat the exact-f32 MFMA implicit-GEMM path
-    (VGG 21.28 ms, DeepNN 5.46 ms, profiles/r4_f32), so the reference's own precision runs its convolutions,
-    BatchNorm and pooling on torch/MIOpen under the ddpx engine (flat store, fused flat SGD, native DDP);
-    ``--kernels native`` selects the exact-f32 kernels."""
+    auto = native everywhere except DeepNN at fp32: there MIOpen's fp32 convolutions (Winograd F(2,3) for the
+    forward / data gradient, 4.30 ms per step) still beat the exact-f32 MFMA implicit-GEMM path (4.81 ms), so that
+    model's convolutions run on torch/MIOpen under the ddpx engine (flat store, fused flat SGD, native DDP);
+    ``--kernels native`` selects the exact-f32 kernels.  VGG at fp32 (the reference's own recipe) runs native:
+    19.07 ms vs MIOpen's 19.43 ms per step on the same box (profiles/r4_f32)."""
     if kernels == "torch":
         return False
     if kernels == "native":
         return True
-    # measured (profiles/r4_f32): DeepNN fp32 native 5.457 ms vs stock 4.357 ms per step (MIOpen's Winograd
-    # convolutions), so auto keeps torch/MIOpen there too until the native path wins
-    return not (name in ("vgg", "deepnn") and dtype == "fp32")
+    # measured (profiles/r4_f32): VGG fp32 native 19.07 ms vs MIOpen 19.43 ms per step (same box) -> native;
+    # DeepNN fp32 native 4.81 ms vs stock 4.30 ms (MIOpen's Winograd convolutions) -> torch until native wins
+    return not (name == "deepnn" and dtype == "fp32")
 
 
 def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "auto",

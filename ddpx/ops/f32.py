@@ -37,6 +37,8 @@ for _sig in (
         ("ddpx_f32_head_bwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _I, _F, _P),
         ("ddpx_f32_nchw_flatten", _I, _P, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_set_staging", _I, _I),
+        ("ddpx_f32_set_block", _I, _I),
+        ("ddpx_f32_conv_fwd_stats", _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
 ):
@@ -61,10 +63,15 @@ def _f32(t, name):
 
 
 def set_staging(dma: bool) -> bool:
-    """GEMM operand staging of the f32 core: LDS-DMA ring (True; DDPX_F32_STAGING=dma) or register-staged (False,
-    the default).
-    Returns the previous setting."""
+    """GEMM operand staging of the f32 core: LDS-DMA ring (True, the default) or register-staged (False;
+    DDPX_F32_STAGING=reg).  Returns the previous setting."""
     return bool(native.kernels().ddpx_f32_set_staging(int(bool(dma))))
+
+
+def set_block(kb: int) -> int:
+    """Summation block of the LDS-DMA core's blocked mode in 16-k K-steps (1, 2 or 4 = default); 1 reproduces the
+    register-staged kernel bitwise.  Returns the previous setting."""
+    return int(native.kernels().ddpx_f32_set_block(int(kb)))
 
 
 def _call(name, *args):
@@ -191,6 +198,25 @@ def conv_fwd(x, wf, Co):
     return y
 
 
+def conv_fwd_stats(x, wf, Co):
+    """(y, (stats, T, R)) — the forward convolution with the BatchNorm tile statistics (mean, M2 of every R-row
+    output tile) emitted by the GEMM epilogue (LDS-DMA core), or (y, None) when that path does not apply."""
+    N, H, W, C = x.shape
+    _f32(x, "x")
+    P = N * H * W
+    y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
+    T = (P + 63) // 64  # enough rows of statistics for the smaller tile
+    stats = torch.empty((T, 2, Co), dtype=torch.float32, device=x.device)
+    r = native.kernels().ddpx_f32_conv_fwd_stats(x.data_ptr(), wf.data_ptr(), y.data_ptr(), N, H, W, C, Co,
+                                                 stats.data_ptr(), native.stream_handle())
+    if r < 0:
+        if r == -10:  # register-staged core selected: plain forward, statistics by their own pass
+            gemm(IM2COL_KC, x, 0, DENSE_OC, wf, Co, P, Co, 9 * C, y, geom=(C, H, W, 1))
+            return y, None
+        native.check(r, "ddpx_f32_conv_fwd_stats")
+    return y, (stats, (P + r - 1) // r, r)
+
+
 def conv_dgrad(dy, wd, N, H, W, C, Co):
     """dx [N,H,W,C] = transposed conv of dy [N*H*W, Co] with wd [(r,s,co), ci]."""
     _f32(dy, "dy")
@@ -217,18 +243,21 @@ def conv_wgrad(dy, x, Co, Ci, out, accumulate=False):
     _call("ddpx_f32_conv_wgrad_reduce", part.data_ptr(), S, Co, Ci, Cp, out.data_ptr(), int(accumulate))
 
 
-def bn_forward(y, N, H, W, C, bn, training, pool):
+def bn_forward(y, N, H, W, C, bn, training, pool, stats=None):
     """(x_next, a, b, mean, rstd): statistics + running-stat update + [pool](relu(a*(y-mean)+b)), a = gamma*rstd,
-    b = beta."""
+    b = beta.  ``stats`` = (part, T, R): chunk statistics already made (the conv GEMM epilogue)."""
     dev = y.device
     P = N * H * W
     a = torch.empty(C, dtype=torch.float32, device=dev)
     b, mean, rstd = torch.empty_like(a), torch.empty_like(a), torch.empty_like(a)
-    R = bn_chunk_rows(P, C)
-    T = (P + R - 1) // R
-    part = torch.empty((T, 2, C), dtype=torch.float32, device=dev) if training else a
-    if training:
-        _call("ddpx_f32_bn_stats", y.data_ptr(), P, C, R, part.data_ptr())
+    if training and stats is not None:
+        part, T, R = stats
+    else:
+        R = bn_chunk_rows(P, C)
+        T = (P + R - 1) // R
+        part = torch.empty((T, 2, C), dtype=torch.float32, device=dev) if training else a
+        if training:
+            _call("ddpx_f32_bn_stats", y.data_ptr(), P, C, R, part.data_ptr())
     nbt = bn.num_batches_tracked if (training and bn.num_batches_tracked is not None) else None
     _call("ddpx_f32_bn_finalize", part.data_ptr(), T, R, P, C, bn.weight.data_ptr(), bn.bias.data_ptr(),
           bn.running_mean.data_ptr(), bn.running_var.data_ptr(), native.ptr(nbt), float(bn.momentum),
@@ -331,8 +360,11 @@ def _vgg_forward(model, x, targets, training):
     for bi, (conv, bn, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
         conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
-        y = conv_fwd(x, plan.wf[bi], Co)
-        xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool)
+        if training:
+            y, st = conv_fwd_stats(x, plan.wf[bi], Co)
+        else:
+            y, st = conv_fwd(x, plan.wf[bi], Co), None
+        xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool, stats=st)
         saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co

@@ -464,7 +464,7 @@ def test_f32_dma_core_bitwise_equals_register_core(gpu, case, tile):
             shape = (M, Nn)
         kw = {}
     outs = []
-    prev = Fk.set_staging(True)
+    prev, pblock = Fk.set_staging(True), Fk.set_block(1)
     try:
         for dma in (True, False):
             Fk.set_staging(dma)
@@ -473,5 +473,40 @@ def test_f32_dma_core_bitwise_equals_register_core(gpu, case, tile):
             outs.append(o)
     finally:
         Fk.set_staging(prev)
+        Fk.set_block(pblock)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
+
+
+@pytest.mark.parametrize("N,H,C,Co", [(8, 32, 4, 64), (16, 8, 128, 256), (64, 4, 512, 512)])
+def test_conv_fwd_stats_epilogue(gpu, N, H, C, Co):
+    """BatchNorm tile statistics from the LDS-DMA conv GEMM's epilogue: y bitwise equal to the plain forward, and
+    every tile's (mean, M2) equal to the statistics of its rows (fp64 arbiter)."""
+    from ddpx.ops import f32 as Fk
+    torch.manual_seed(9)
+    x = torch.randn(N, H, H, C, device=gpu)
+    wf = torch.randn(9 * C * Co, device=gpu) / (9 * C) ** 0.5
+    prev = Fk.set_staging(True)
+    try:
+        y, st = Fk.conv_fwd_stats(x, wf, Co)
+        y2 = Fk.conv_fwd(x, wf, Co)
+    finally:
+        Fk.set_staging(prev)
+    assert st is not None
+    part, T, R = st
+    assert torch.equal(y, y2)
+    P = N * H * H
+    assert T == (P + R - 1) // R
+    yd = y.double().cpu()
+    for t in range(T):
+        rows = yd[t * R:min(P, (t + 1) * R)]
+        mu = rows.mean(0)
+        m2 = ((rows - mu) ** 2).sum(0)
+        assert _rel(part[t, 0].cpu(), mu) < 1e-5, t
+        assert _rel(part[t, 1].cpu(), m2) < 1e-5, t
+    prev = Fk.set_staging(False)
+    try:
+        y3, st3 = Fk.conv_fwd_stats(x, wf, Co)  # register-staged core: no fused statistics
+    finally:
+        Fk.set_staging(prev)
+    assert st3 is None and torch.equal(y3, y2)
