@@ -509,6 +509,7 @@ static void dispatch_tile(int tile, const Operand& A, const Operand& B, int M, i
   switch (tile) {
     case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
     case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
+    case 3: launch<64, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
     default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
   }
 }
@@ -1251,7 +1252,10 @@ __global__ void __launch_bounds__(256) nchw_flatten_kernel(const float* __restri
   else out[f] = x[i];
 }
 
+// 0 = 128x128, 1 = 128x64, 2 = 64x64, 3 = 64x128.  Thin operands get the tile that does not compute padding:
+// M <= 64 (the weight gradients of 64-channel layers: M = Co) takes 64-row tiles.
 static int auto_tile(int M, int N, int splits) {
+  if (M <= 64) return N <= 64 ? 2 : 3;
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128) * splits;
   return N <= 64 ? 1 : (t128 >= 512 ? 0 : 2);
 }
@@ -1272,7 +1276,7 @@ static inline unsigned nblk(long n, int b = 256) { return (unsigned)((n + b - 1)
 
 // C (+)= A B on the f32 MFMA core.  amode/bmode: Mode; conv geometry (C, H, W of the NHWC tensor an
 // IM2COL operand reads, and the tap sign) applies to whichever operand is IM2COL.  splits > 1: raw partial
-// slabs C + z*split_stride (no epilogue).  tile: 0 = 128x128, 1 = 128x64, 2 = 64x64, -1 = auto.
+// slabs C + z*split_stride (no epilogue).  tile: 0 = 128x128, 1 = 128x64, 2 = 64x64, 3 = 64x128, -1 = auto.
 DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const float* b, int ldb, int M, int N, int K,
                            int gc, int gh, int gw, int sgn, int splits, float* c, int ldc, int64_t split_stride,
                            const float* bias, const float* mask, int flags, int tile, hipStream_t s) {
@@ -1485,5 +1489,5 @@ DDPX_API int ddpx_f32_conv_fwd_stats(const float* x, const float* wf, float* y, 
   const int tile = auto_tile(M, Co, 1);
   dispatch_tile<IM2COL_KC, DENSE_OC>(tile, A, B, M, Co, K, 1, y, Co, 0, nullptr, nullptr, 0, s, ab, bb, stats);
   const int err = (int)hipGetLastError();
-  return err ? -err : (tile == 2 ? 64 : 128);
+  return err ? -err : ((tile == 2 || tile == 3) ? 64 : 128);
 }

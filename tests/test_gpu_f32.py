@@ -422,7 +422,7 @@ def test_deepnn_fp32_trains_like_torch(gpu):
 
 
 @pytest.mark.parametrize("case", ["fwd", "dgrad", "wgrad", "lin_fwd", "lin_dgrad", "lin_wgrad", "ragged"])
-@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
 def test_f32_dma_core_bitwise_equals_register_core(gpu, case, tile):
     """The LDS-DMA ring GEMM (default) runs the register-staged kernel's fragment / MFMA / summation sequence:
     results must be bitwise equal for every operand mode, tile and split."""
