@@ -507,6 +507,7 @@ def test_conv_fwd_stats_epilogue(gpu, N, H, C, Co):
     prev = Fk.set_staging(False)
     try:
         y3, st3 = Fk.conv_fwd_stats(x, wf, Co)  # register-staged core: no fused statistics
+        y4 = Fk.conv_fwd(x, wf, Co)
     finally:
         Fk.set_staging(prev)
-    assert st3 is None and torch.equal(y3, y2)
+    assert st3 is None and torch.equal(y3, y4)
