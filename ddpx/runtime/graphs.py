@@ -18,6 +18,28 @@ from __future__ import annotations
 import torch
 
 
+_UPLOAD_SIG = False
+
+
+def _upload(graph):
+    """Upload the instantiated executable now (csrc/kernels/graph_util.hip), not on its first replay: a graph
+    first launched inside a timed region would otherwise pay the upload there.  Best effort."""
+    global _UPLOAD_SIG
+    import os
+    if os.environ.get("DDPX_GRAPH_UPLOAD", "1") == "0":
+        return
+    try:
+        from . import native
+        if not _UPLOAD_SIG:
+            native.register_kernel_sig("ddpx_graph_upload", native.c_int, native.c_void_p, native.c_void_p)
+            _UPLOAD_SIG = True
+        exec_ptr = graph.raw_cuda_graph_exec()
+        if exec_ptr:
+            native.kernels().ddpx_graph_upload(exec_ptr, native.stream_handle())
+    except Exception:  # noqa: BLE001 - an older torch without raw_cuda_graph_exec(): upload on first launch
+        pass
+
+
 class CapturedStep:
     """Capture ``fn(x, y) -> loss`` into a graph; ``__call__`` replays it."""
 
@@ -51,6 +73,7 @@ class CapturedStep:
             pre_replay()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.static_loss = self.fn(self.static_x, self.static_y)
+        _upload(self.graph)
         torch.cuda.synchronize()
 
     def load(self, x: torch.Tensor, y: torch.Tensor):
