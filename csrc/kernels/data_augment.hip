@@ -137,71 +137,6 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
   }
 }
 
-// NCHW / flat layouts with 32-pixel rows (CIFAR): one thread per (sample, channel, row) — the row's 32 source
-// bytes come in two 16-B loads once and all 32 outputs go out as 16-B stores, so the sample's index load and
-// crop/flip hash are done once per row instead of once per 8 pixels (4x fewer threads than augment_body).
-// Same outputs as augment_body (tests/test_gpu_kernels.py::test_augment_matches_cpu).
-__device__ __forceinline__ void augment_rows32(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
-                                               const int64_t* __restrict__ idx, int B, int C, int H, int pad,
-                                               uint64_t seed, int train, int layout, void* __restrict__ out,
-                                               int64_t* __restrict__ tgt_out) {
-  constexpr int W = 32;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= B * C * H) return;
-  const int y = t % H, c = (t / H) % C, b = t / (H * C);
-  const int64_t src = idx ? idx[b] : b;
-  int dy = pad, dx = pad, flip = 0;
-  if (train) {
-    const uint64_t r = splitmix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(b + 1)));
-    dy = (int)mod64(r, 2 * pad + 1);
-    dx = (int)mod64(r >> 16, 2 * pad + 1);
-    flip = (int)((r >> 40) & 1);
-  }
-  if (tgt_out && y == 0 && c == 0) tgt_out[b] = labels[src];
-  const int sy = y + dy - pad;
-  const bool row_ok = (sy >= 0) && (sy < H);
-  const float inv = 1.f / 255.f;
-  const uint8_t* row = images + (size_t)src * C * H * W + (size_t)c * H * W + (size_t)(row_ok ? sy : 0) * W;
-  const u32x4 lo = *reinterpret_cast<const u32x4*>(row), hi = *reinterpret_cast<const u32x4*>(row + 16);
-  const size_t o = (((size_t)b * C + c) * H + y) * W;
-#pragma unroll
-  for (int xg = 0; xg < 4; ++xg) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ox = xg * 8 + j;
-      const int x = flip ? (W - 1 - ox) : ox;
-      const int sx = x + dx - pad;
-      const int d = (sx >> 2) & 7;
-      const unsigned w = d < 4 ? (d < 2 ? (d == 0 ? lo[0] : lo[1]) : (d == 2 ? lo[2] : lo[3]))
-                               : (d < 6 ? (d == 4 ? hi[0] : hi[1]) : (d == 6 ? hi[2] : hi[3]));
-      const unsigned byte = (w >> (8 * (sx & 3))) & 0xFFu;
-      v[j] = (row_ok && sx >= 0 && sx < W) ? (float)byte * inv : 0.f;
-    }
-    if (layout == OUT_NCHW_BF16) {
-      const u32x4 pk = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
-      *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned short*>(out) + o + xg * 8) = pk;
-    } else {
-      f32x4* dd = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + o + xg * 8);
-      dd[0] = (f32x4){v[0], v[1], v[2], v[3]};
-      dd[1] = (f32x4){v[4], v[5], v[6], v[7]};
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256)
-augment_rows_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
-                    const int64_t* __restrict__ idx, int B, int C, int H, int pad, uint64_t seed, int train,
-                    int layout, void* __restrict__ out, int64_t* __restrict__ tgt_out, const int* __restrict__ cursor,
-                    int nbatch) {
-  if (cursor) {
-    const int k = *cursor;
-    idx += (size_t)(k % nbatch) * B;
-    seed += (uint64_t)k;
-  }
-  augment_rows32(images, labels, idx, B, C, H, pad, seed, train, layout, out, tgt_out);
-}
-
 // cursor (optional): device-side step counter k (read only).  The batch is rows [k % nbatch * B, +B) of
 // the epoch's index permutation `idx` and the augmentation seed is seed + k (DeviceLoader.batch_seed(k)),
 // so a captured training step draws a new batch on every replay with no host work.  The counter is
@@ -233,12 +168,6 @@ DDPX_API int ddpx_augment(const void* images, const int64_t* labels, const int64
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
                      layout == OUT_NHWC4_F32);
   if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
-  if (!nhwc && W == 32 && !((uintptr_t)images & 15) && !((uintptr_t)out & 15)) {
-    const int nr = B * C * H;
-    hipLaunchKernelGGL(augment_rows_kernel, dim3((nr + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
-                       idx, B, C, H, pad, seed, train, layout, out, tgt_out, (const int*)nullptr, 1);
-    return (int)hipGetLastError();
-  }
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx, B, C, H, W, pad, seed, train, layout, out, tgt_out, (const int*)nullptr, 1);
@@ -256,12 +185,6 @@ DDPX_API int ddpx_augment_cursor(const void* images, const int64_t* labels, cons
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
                      layout == OUT_NHWC4_F32);
   if ((layout == OUT_NHWC8_BF16 && C > 8) || (layout == OUT_NHWC4_F32 && C > 4)) return -2;
-  if (!nhwc && W == 32 && !((uintptr_t)images & 15) && !((uintptr_t)out & 15)) {
-    const int nr = B * C * H;
-    hipLaunchKernelGGL(augment_rows_kernel, dim3((nr + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
-                       idx_all, B, C, H, pad, seed, train, layout, out, tgt_out, cursor, nbatch);
-    return (int)hipGetLastError();
-  }
   const int n = nhwc ? B * H * W : B * C * H * (W / 8);
   hipLaunchKernelGGL(augment_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const uint8_t*)images, labels,
                      idx_all, B, C, H, W, pad, seed, train, layout, out, tgt_out, cursor, nbatch);
