@@ -56,12 +56,12 @@ def main():
         xt = x[..., :Ci].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         wt = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         row["miopen_fwd"] = round(timeit(lambda: F.conv2d(xt, wt, padding=1)), 1)
-        for cfg in range(14):
+        for cfg in range(16):
             row[f"fwd{cfg}"] = round(timeit(lambda: K.conv_fwd(x, wf, Co, stats=True, tile=cfg)), 1)
             row[f"dgrad{cfg}"] = round(timeit(lambda: K.conv_dgrad(dy, wd, N, H, H, Cp, Co, tile=cfg)), 1)
             row[f"wgrad{cfg}"] = round(timeit(lambda: K.conv_wgrad(dy, x, Co, Ci, out=dw, tile=cfg)), 1)
         for kind in ("fwd", "dgrad", "wgrad"):
-            best = min(range(14), key=lambda c: row[f"{kind}{c}"])
+            best = min(range(16), key=lambda c: row[f"{kind}{c}"])
             row[f"best_{kind}"] = best
             row[f"best_{kind}_tflops"] = round(flop / row[f"{kind}{best}"] / 1e6, 1)
         res.append(row)
