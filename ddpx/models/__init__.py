@@ -13,18 +13,16 @@ __all__ = ["VGG", "DeepNN", "MLP", "build_model", "native_kernels_for"]
 def native_kernels_for(name: str, dtype: str, kernels: str = "auto") -> bool:
     """Whether ``build_model`` puts ``name`` on the hand-written kernels for ``kernels`` = auto|native|torch.
 
-    auto = native everywhere except DeepNN at fp32: there MIOpen's fp32 convolutions (Winograd F(2,3) for the
-    forward / data gradient, 4.30 ms per step) still beat the exact-f32 MFMA implicit-GEMM path (4.81 ms), so that
-    model's convolutions run on torch/MIOpen under the ddpx engine (flat store, fused flat SGD, native DDP);
-    ``--kernels native`` selects the exact-f32 kernels.  VGG at fp32 (the reference's own recipe) runs native:
-    19.07 ms vs MIOpen's 19.43 ms per step on the same box (profiles/r4_f32)."""
+    auto = native everywhere (measured faster than the stock libraries on every model and precision, including the
+    reference's fp32 recipe: VGG 18.79 vs MIOpen 19.46 ms, DeepNN 3.83 vs 4.29 ms per step, profiles/r4_f32);
+    ``--kernels torch`` runs the torch/MIOpen ops under the ddpx engine (flat store, fused flat SGD, native DDP)."""
     if kernels == "torch":
         return False
     if kernels == "native":
         return True
-    # measured (profiles/r4_f32): VGG fp32 native 19.07 ms vs MIOpen 19.43 ms per step (same box) -> native;
-    # DeepNN fp32 native 4.81 ms vs stock 4.30 ms (MIOpen's Winograd convolutions) -> torch until native wins
-    return not (name == "deepnn" and dtype == "fp32")
+    # measured (profiles/r4_f32): at fp32 the native kernels beat MIOpen on both CNNs (VGG 18.79 vs 19.46 ms,
+    # DeepNN 3.83 vs 4.29 ms per step, same boxes), so auto is native everywhere
+    return True
 
 
 def build_model(name: str, hidden=None, layers: int = 3, dtype: str = "auto", device=None, kernels: str = "auto",
