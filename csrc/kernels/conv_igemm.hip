@@ -120,16 +120,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // profiles/r1_fdiv/conv_sweep_fdiv.json): the 8-wave 256x256 tile (cfg 13) wins every >= 128-channel
 // layer at 16x16 and 8x8 (fwd 512->512@8: 151 vs 198 us for 256x128); the 32x32 layers keep 256x128
 // (cfg 8); 4x4 layers (P = 8192) want 64x128; <= 64-channel outputs stay on 64x64.
-// (round-4 sweep of every VGG layer x tile config, profiles/r4_final/conv_sweep.json)
 static int pick_fwd(int P, int Co) {
   if (Co <= 64) return 7;     // conv0 (3->64 @32), DeepNN's 64/32-channel layers: 64x64, 3 stages
-  if (P <= 8192) return 15;   // 4x4 layers: 128x128, 8 waves, 4 stages (58 vs 59 us)
+  if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
   if (P >= 524288) return 8;  // 32x32 layers: 256x128, 8 waves
   return 13;                  // 256x256, 8 waves
 }
 static int pick_dgrad(int P, int C, int Co) {
-  if (C <= 64) return 7;      // dx of a 64-channel input (VGG conv1 @32): 64x64, 3 stages (163 vs 168 us)
-  if (P <= 8192) return 15;   // 4x4 layers: 128x128, 8 waves, 4 stages (66 vs 73 us)
+  if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32): 128x64, 3 stages
+  if (P <= 8192) return 5;
   if (Co <= 64 || Co > C) return 8;  // widening layers (dx narrower than dy) and thin DeepNN layers
   return 13;
 }
@@ -218,7 +217,7 @@ static int pick_wgrad(int P, int C, int Co) {
   // M = Co <= 64 (DeepNN's 128->64, 64->64, 64->32 layers): a 256-row tile would be 3/4 empty;
   // 64x64 / 3 stages measured 2.6x faster on 128->64@32 (profiles/r1_deepnn/conv_sweep_deepnn.json)
   if (Co <= 64) return 7;
-  if (C <= 64) return 15;     // VGG conv1 (64->128 @32): 128x128, 8 waves, 4 stages (156 vs 181 us for 64x64)
+  if (C <= 64) return 7;      // VGG conv1 (64->128 @32): 64x64 (259 vs 280 us for 128x128)
   return 13;                  // 256x256, 8 waves (283 vs 393 us for 256x128 on 256->256@16)
 }
 
