@@ -36,11 +36,14 @@ constexpr int VPT = BM * BN / 4 / 256;  // f32x4 vectors per stream thread per t
 //   4 stages: one more 24 KiB stage in flight (the math side's K-steps are L2->LDS latency bound with
 //             only 4 DMA-issuing waves), which fits the 160 KiB LDS only with unpadded rows (4-way
 //             conflicts on the once-per-tile accumulator store).
-template <int STAGES, int XTRA = 0>
+//   SB (single hand-off buffer): the stream waves read each gradient vector one K-step ahead, so they never touch
+//             the buffer in the K-step the math waves refill it: one fp32 tile buffer instead of two, which leaves
+//             room for a 4-stage ring with padded rows (DDPX_WSGD_SB=1, 4 stream waves).
+template <int STAGES, int XTRA = 0, bool SB = false>
 struct Cfg {
-  static constexpr int ALD = STAGES >= 4 ? BN : BN + 4;
+  static constexpr int ALD = (STAGES >= 4 && !SB) ? BN : BN + 4;
   static constexpr int ACC_BYTES = BM * ALD * 4;
-  static constexpr int LDS_BYTES = STAGES * SLOT + 2 * ACC_BYTES + (XTRA >= 2 ? SLOT : 0);
+  static constexpr int LDS_BYTES = STAGES * SLOT + (SB ? 1 : 2) * ACC_BYTES + (XTRA >= 2 ? SLOT : 0);
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
@@ -50,10 +53,11 @@ struct Cfg {
 // XTRA (measurement only, DDPX_WSGD_XTRA): 1 = every K-step runs its MFMAs twice (the second set into a
 // dead accumulator kept live), 2 = also a second operand stage of LDS-DMA per K-step into a dummy ring — the
 // math and L2->LDS load a fused data-gradient GEMM would add beside the weight-gradient tiles.
-template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0>
+template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false>
 __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
-  constexpr int ALD = Cfg<STAGES, XTRA>::ALD, ACC_BYTES = Cfg<STAGES, XTRA>::ACC_BYTES;
-  constexpr int LDS_BYTES = Cfg<STAGES, XTRA>::LDS_BYTES;
+  constexpr int ALD = Cfg<STAGES, XTRA, SB>::ALD, ACC_BYTES = Cfg<STAGES, XTRA, SB>::ACC_BYTES;
+  constexpr int LDS_BYTES = Cfg<STAGES, XTRA, SB>::LDS_BYTES;
+  static_assert(!SB || NSW == 4, "single hand-off buffer: one update per K-step");
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -171,7 +175,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
             for (int b = 0; b < FN; ++b) asm volatile("" ::"v"(acc2[a][b]));
         }
         // accumulators -> tile buffer i&1 (C/D map: row 4*(lane>>4)+r, col lane&15 of each 16x16 block)
-        float* T = accb + (i & 1) * (ACC_BYTES / 4);
+        float* T = accb + (SB ? 0 : (i & 1) * (ACC_BYTES / 4));
         const int mr = wm * 32 + 4 * (lane >> 4), nc = wn * 64 + (lane & 15);
 #pragma unroll
         for (int a = 0; a < FM; ++a)
@@ -229,11 +233,13 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? P1 : P0) + off));
       mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? M1 : M0) + off));
     };
-    // update vector v of tile j from the gradient tile T, then refill the slot with the vector DIST ahead
-    auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
+    auto grad_vec = [&](const float* T, int v) -> f32x4 {
+      return *reinterpret_cast<const f32x4*>(T + (row0 + RSTEP * v) * ALD + col);
+    };
+    // update vector v of tile j with gradient g, then refill the slot with the vector DIST ahead
+    auto update_vec_g = [&](int j, int v, const f32x4 g, f32x4& pv, f32x4& mv) {
       int sel;
       const size_t off = vec_off(j, v, sel);
-      const f32x4 g = *reinterpret_cast<const f32x4*>(T + (row0 + RSTEP * v) * ALD + col);
       f32x4 po, bo;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // sgd_apply's fma sequence
@@ -260,6 +266,10 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       const int vn = v + DIST;
       const bool same = vn < SV, next = !same && j + 1 < nt;
       load_vec(same ? j : (next ? j + 1 : j), same ? vn : (next ? vn - SV : v), pv, mv);
+    };
+    // update vector v of tile j from the gradient tile T
+    auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
+      update_vec_g(j, v, grad_vec(T, v), pv, mv);
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
 #pragma unroll
@@ -289,9 +299,37 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
         __builtin_amdgcn_s_barrier();
       }
     };
-    trip(0);
+    if constexpr (SB) {
+      // single hand-off buffer: vector v's gradient is read in the K-step before its update (vector 0 right after
+      // the hand-off barrier), so the last K-step of an iteration — when the math waves overwrite the buffer with
+      // the next tile — reads nothing; every read has landed before the next barrier (lgkmcnt(0))
+      f32x4 gq = grad_vec(accb, 0);
+      auto trip_sb = [&](int r) {
+        const int i = 1 + r / TPI, t = (r % TPI) * DIST;
+#pragma unroll
+        for (int u = 0; u < DIST; ++u) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          const f32x4 g = gq;
+          if (t + u + 1 < SV) gq = grad_vec(accb, t + u + 1);
+          update_vec_g(i - 1, t + u, g, rp[u], rm[u]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier, then the next tile's vector 0
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          gq = grad_vec(accb, 0);
+        }
+      };
+      trip_sb(0);
 #pragma unroll 1
-    for (int r = 1; r < TPI * nt; ++r) trip(r);
+      for (int r = 1; r < TPI * nt; ++r) trip_sb(r);
+    } else {
+      trip(0);
+#pragma unroll 1
+      for (int r = 1; r < TPI * nt; ++r) trip(r);
+    }
   }
 }
 
@@ -335,6 +373,15 @@ static inline bool n_order() {
   return v;
 }
 
+// DDPX_WSGD_SB=1: single hand-off buffer + 4-stage padded ring (4 stream waves, no MX-FP8 copy)
+static inline bool single_buffer() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_WSGD_SB");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 static inline int xtra() {
   static const int v = [] {
     const char* e = getenv("DDPX_WSGD_XTRA");
@@ -352,6 +399,12 @@ static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0,
     const int x = xtra();
     if (x == 1) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 1>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
     if (x == 2) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 2>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
+  }
+  if constexpr (!FP8) {
+    if (nsw == 4 && no && single_buffer()) {
+      hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false, 4, true, 0, true>), grid, dim3(512), 0, s, p0, p1, nt1);
+      return;
+    }
   }
   if (nsw == 8) {
     if (no) hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 8, true>), grid, dim3(768), 0, s, p0, p1, nt1);
