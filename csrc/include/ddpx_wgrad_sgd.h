@@ -139,7 +139,8 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
           const int ahead = min(STAGES - 2, G - 1 - g);
           constexpr int LW = XTRA >= 2 ? 2 * LPW : LPW;
           // stage g landed: everything but the (up to STAGES - 2) younger stages' DMAs
-          if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LW>();
+          if (STAGES >= 5 && ahead >= 3) pipe::wait_vmcnt<3 * LW>();
+          else if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LW>();
           else if (ahead >= 1) pipe::wait_vmcnt<LW>();
           else pipe::wait_vmcnt<0>();
           __builtin_amdgcn_s_barrier();
@@ -373,11 +374,12 @@ static inline bool n_order() {
   return v;
 }
 
-// DDPX_WSGD_SB=1: single hand-off buffer + 4-stage padded ring (4 stream waves, no MX-FP8 copy)
-static inline bool single_buffer() {
-  static const bool v = [] {
+// DDPX_WSGD_SB=1|5: single hand-off buffer + 4-stage (1) or 5-stage (5) padded ring (4 stream waves, no MX-FP8
+// copy); 0 = off
+static inline int single_buffer() {
+  static const int v = [] {
     const char* e = getenv("DDPX_WSGD_SB");
-    return e && e[0] == '1';
+    return (e && e[0] == '1') ? 4 : (e && e[0] == '5') ? 5 : 0;
   }();
   return v;
 }
@@ -401,8 +403,12 @@ static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0,
     if (x == 2) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 2>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
   }
   if constexpr (!FP8) {
-    if (nsw == 4 && no && single_buffer()) {
+    if (nsw == 4 && no && single_buffer() == 4) {
       hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false, 4, true, 0, true>), grid, dim3(512), 0, s, p0, p1, nt1);
+      return;
+    }
+    if (nsw == 4 && no && single_buffer() == 5) {
+      hipLaunchKernelGGL((wgrad_sgd_ws_kernel<5, false, 4, true, 0, true>), grid, dim3(512), 0, s, p0, p1, nt1);
       return;
     }
   }
