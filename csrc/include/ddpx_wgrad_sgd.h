@@ -57,7 +57,6 @@ template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = fals
 __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
   constexpr int ALD = Cfg<STAGES, XTRA, SB>::ALD, ACC_BYTES = Cfg<STAGES, XTRA, SB>::ACC_BYTES;
   constexpr int LDS_BYTES = Cfg<STAGES, XTRA, SB>::LDS_BYTES;
-  static_assert(!SB || NSW == 4, "single hand-off buffer: one update per K-step");
   constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
   constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -316,6 +315,11 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
           if (t + u + 1 < SV) gq = grad_vec(accb, t + u + 1);
           update_vec_g(i - 1, t + u, g, rp[u], rm[u]);
           __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 1; k < KPU; ++k) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+          }
         }
         if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier, then the next tile's vector 0
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -374,8 +378,7 @@ static inline bool n_order() {
   return v;
 }
 
-// DDPX_WSGD_SB=1|5: single hand-off buffer + 4-stage (1) or 5-stage (5) padded ring (4 stream waves, no MX-FP8
-// copy); 0 = off
+// DDPX_WSGD_SB=1|5: single hand-off buffer + 4-stage (1) or 5-stage (5) padded ring (no MX-FP8 copy); 0 = off
 static inline int single_buffer() {
   static const int v = [] {
     const char* e = getenv("DDPX_WSGD_SB");
@@ -403,12 +406,21 @@ static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0,
     if (x == 2) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<2, false, 4, true, 2>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
   }
   if constexpr (!FP8) {
-    if (nsw == 4 && no && single_buffer() == 4) {
+    const int sb = no ? single_buffer() : 0;
+    if (sb == 4 && nsw == 4) {
       hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false, 4, true, 0, true>), grid, dim3(512), 0, s, p0, p1, nt1);
       return;
     }
-    if (nsw == 4 && no && single_buffer() == 5) {
+    if (sb == 5 && nsw == 4) {
       hipLaunchKernelGGL((wgrad_sgd_ws_kernel<5, false, 4, true, 0, true>), grid, dim3(512), 0, s, p0, p1, nt1);
+      return;
+    }
+    if (sb == 4 && nsw == 8) {
+      hipLaunchKernelGGL((wgrad_sgd_ws_kernel<4, false, 8, true, 0, true>), grid, dim3(768), 0, s, p0, p1, nt1);
+      return;
+    }
+    if (sb == 5 && nsw == 8) {
+      hipLaunchKernelGGL((wgrad_sgd_ws_kernel<5, false, 8, true, 0, true>), grid, dim3(768), 0, s, p0, p1, nt1);
       return;
     }
   }
