@@ -133,3 +133,17 @@ def test_bench_batch_prefetch_trains_identically(gpu, tmp_path, model):
     assert a["config"]["graph"] and b["config"]["graph"]
     assert a["config"]["final_loss"] == b["config"]["final_loss"]
     assert a["config"]["master_digest"] == b["config"]["master_digest"] is not None
+
+
+def test_multigpu_reference_command_fp32_native_calibrated(gpu, tmp_path):
+    """``python multigpu.py E S`` with the reference's defaults (VGG, fp32, batch 512) on the GPU, one rank: the
+    native fp32 kernels under DDP over the native RCCL communicator, with the bucket plan calibrated by training
+    steps, HIP graphs and per-bucket optimizer overlap — the tuned path behind the reference's own entry point."""
+    out = _run([os.path.join(ROOT, "multigpu.py"), "1", "1", "--nprocs", "1", "--data", "synthetic", "--train_size",
+                "2048", "--test_size", "512"], tmp_path,
+               extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port())})
+    assert "[GPU0] Epoch 0 | Batchsize: 512 | Steps: 4" in out
+    assert "fp32 model has size=35.20 MiB" in out
+    assert "bucket plan: calibrated" in out, out
+    sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
+    assert all(v.dtype in (torch.float32, torch.int64) for v in sd.values())
