@@ -463,7 +463,7 @@ static int g_f32_block = -1;
 static int f32_block() {
   if (g_f32_block < 0) {
     const char* e = getenv("DDPX_F32_BLOCK");
-    g_f32_block = (e && e[0] == '1') ? 1 : (e && e[0] == '2') ? 2 : 4;
+    g_f32_block = (e && e[0] == '1') ? 1 : (e && e[0] == '2') ? 2 : (e && e[0] == '8') ? 8 : 4;
   }
   return g_f32_block;
 }
@@ -488,6 +488,9 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
                          B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     else if (f32_block() == 4)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 4>), dim3(nwg), dim3(NT), 0, s, A,
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+    else if (f32_block() == 8)
+      hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 8>), dim3(nwg), dim3(NT), 0, s, A,
                          B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
     else
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,
@@ -1462,7 +1465,7 @@ DDPX_API int ddpx_f32_nchw_flatten(const float* x, int N, int S, int C, int back
 // Summation block (1, 2 or 4 K-steps of 16) of the LDS-DMA core; returns the previous setting.
 DDPX_API int ddpx_f32_set_block(int kb) {
   const int prev = f32_block();
-  g_f32_block = (kb == 1 || kb == 2) ? kb : 4;
+  g_f32_block = (kb == 1 || kb == 2 || kb == 8) ? kb : 4;
   return prev;
 }
 
