@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Spread of the bf16 VGG training trajectory (tests/test_gpu_parity.py's setup) across runs that differ only in
+summation order: torch fp32 (twice), torch bf16 autocast (twice), and the native bf16 path under each BatchNorm
+merge order (ddpx_bn_set_merge: legacy / split / bwd).  Prints one JSON line per run: last-20 mean loss and
+test accuracy.
+
+    python benchmarks/vgg_parity_probe.py [--steps 100] [--batch 128]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=128)
+    a = ap.parse_args()
+    import ddpx
+    from ddpx.data.datasets import synthetic_cifar
+    from ddpx.data.loader import DeviceLoader
+    from ddpx.models import VGG
+    from ddpx.optim.schedule import OneCycleLambda
+    from ddpx.optim.sgd import SGD
+    from ddpx.runtime import native
+    from test_gpu_parity import _accuracy, _train
+    gpu = torch.device("cuda", 0)
+    steps, B = a.steps, a.batch
+    torch.manual_seed(0)
+    ref = VGG().to(gpu)
+    init = {k: v.clone() for k, v in ref.state_dict().items()}
+    train = synthetic_cifar(8192, seed=0, noise=230.0)
+    test = synthetic_cifar(2048, seed=0, noise=230.0, split_seed_offset=7)
+    lam = OneCycleLambda(steps_per_epoch=steps // 20, num_epochs=20)
+
+    def torch_run(amp):
+        ref.load_state_dict(init)
+        o = torch.optim.SGD(ref.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
+        s = torch.optim.lr_scheduler.LambdaLR(o, lam)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            loss = _train(ref, DeviceLoader(train, B, gpu, layout="nchw_f32", seed=0), o, s, steps, False)
+        return loss, _accuracy(ref, DeviceLoader(test, B, gpu, train=False, layout="nchw_f32"))
+
+    def native_run(merge):
+        if merge is not None:
+            native.kernels().ddpx_bn_set_merge(merge)
+        nat = VGG()
+        nat.load_state_dict(init)
+        nat.use_native = True
+        ddpx.prepare_model(nat, gpu)
+        o = SGD(nat.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, fused_backward=True)
+        s = torch.optim.lr_scheduler.LambdaLR(o, lam)
+        loss = _train(nat, DeviceLoader(train, B, gpu, layout="nhwc8_bf16", seed=0), o, s, steps, True)
+        return loss, _accuracy(nat, DeviceLoader(test, B, gpu, train=False, layout="nhwc8_bf16"))
+
+    runs = [("torch_fp32", lambda: torch_run(False)), ("torch_fp32", lambda: torch_run(False)),
+            ("torch_bf16_autocast", lambda: torch_run(True)), ("torch_bf16_autocast", lambda: torch_run(True))]
+    for name, m in (("native_bf16_merge_legacy", 1), ("native_bf16_merge_split", 0), ("native_bf16_merge_bwd", 2)):
+        runs.append((name, lambda m=m: native_run(m)))
+    for name, fn in runs:
+        loss, acc = fn()
+        print(json.dumps({"run": name, "tail20": round(loss[-20:].mean().item(), 4),
+                          "head10": round(loss[:10].mean().item(), 4), "test_acc": round(acc, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
