@@ -64,18 +64,35 @@ def sgd_flat_(param: torch.Tensor, momentum_buf: torch.Tensor, grad: torch.Tenso
         raise ValueError("sgd_flat: buffers must have equal numel")
     if not param.is_cuda:
         lr_v = float(lr) if not torch.is_tensor(lr) else float(lr.item())
-        d = grad.float() * grad_scale
-        if weight_decay:
-            d = d.add(param, alpha=weight_decay)
-        if momentum:
-            if first:
-                momentum_buf.copy_(d)
-            else:
-                momentum_buf.mul_(momentum).add_(d)
-            d = d.add(momentum_buf, alpha=momentum) if nesterov else momentum_buf
-        param.add_(d, alpha=-lr_v)
-        if shadow is not None:
-            shadow.copy_(param)
+        # one cache-blocked sweep: each 256K-element block goes through every pass while it is still in
+        # L2 (whole-buffer passes with full-size temporaries cost ~3.7x on the 29M-parameter MLP); the
+        # per-element arithmetic and its rounding order are torch.optim.SGD's
+        blk = 1 << 18
+        tmp = torch.empty(min(n, blk), dtype=torch.float32)
+        pf, bf, gf = param.view(-1), momentum_buf.view(-1), grad.view(-1)
+        sf = shadow.view(-1) if shadow is not None else None
+        for s in range(0, n, blk):
+            e = min(n, s + blk)
+            p, g = pf[s:e], gf[s:e]
+            d = tmp[:e - s]
+            d.copy_(g)
+            if grad_scale != 1.0:
+                d.mul_(grad_scale)
+            if weight_decay:
+                d.add_(p, alpha=weight_decay)
+            if momentum:
+                b = bf[s:e]
+                if first:
+                    b.copy_(d)
+                else:
+                    b.mul_(momentum).add_(d)
+                if nesterov:
+                    d.add_(b, alpha=momentum)
+                else:
+                    d = b
+            p.add_(d, alpha=-lr_v)
+            if sf is not None:
+                sf[s:e].copy_(p)
         return param
     lib = native.kernels()
     lr_dev = lr.data_ptr() if torch.is_tensor(lr) else None
