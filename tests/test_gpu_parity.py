@@ -51,7 +51,20 @@ def _accuracy(model, loader):
     return 100.0 * hit / n
 
 
+SEEDS = (0, 1, 2, 3)
+
+
 def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
+    """Outcome parity over an ensemble of initialisations / batch orders, not one trajectory.
+
+    In this regime (lr 0.4 one-cycle, 100 steps, heavy-noise data) a single trajectory is chaotic: the
+    native bf16 run from one init moved from 0.53 to 0.71 last-20 loss with nothing but the summation order of
+    the BatchNorm statistics, and torch fp32 itself is not reproducible run to run
+    (``profiles/r4_final/NOTES.md``).  So each seed trains both engines from the same weights on the same
+    batches, and the bar is on the ensemble means: last-20 loss within 25 % of the fp32 mean, test accuracy
+    within 4 points (averaging 4 seeds halves the single-trajectory spread the old one-seed bar had to absorb)."""
+    import math
+
     import ddpx
     from ddpx.data.datasets import synthetic_cifar
     from ddpx.data.loader import DeviceLoader
@@ -60,14 +73,6 @@ def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     from ddpx.optim.sgd import SGD
 
     steps, B = 100, 128
-    torch.manual_seed(0)
-    ref = VGG().to(gpu)
-    nat = VGG()
-    nat.load_state_dict(ref.state_dict())
-    nat.use_native = True
-    ddpx.prepare_model(nat, gpu)
-    assert nat.input_layout(gpu) == "nhwc8_bf16"
-
     # heavy pixel noise and a short run: the default set (noise 60) is separated perfectly within a few
     # epochs (loss 1e-4 after 300 steps), which would make any two trainers agree; this stops mid-way
     train = synthetic_cifar(8192, seed=0, noise=230.0)
@@ -75,34 +80,49 @@ def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     # one-cycle over the whole run: 20 "epochs" of steps/20 batches
     lam = OneCycleLambda(steps_per_epoch=steps // 20, num_epochs=20)
 
-    # the stock fp32 reference is not bitwise reproducible on the GPU (MIOpen / hipBLASLt algorithm choice and
-    # reduction order): two runs from the same weights measured tail losses 0.47-0.56 and test accuracies
-    # 86.5-90.1 % (profiles/r3_bn/NOTES.md).  The reference band below is widened by the spread of two runs.
-    init = {k: v.clone() for k, v in ref.state_dict().items()}
-    refs = []
-    for _ in range(2):
-        ref.load_state_dict(init)
+    rows = []
+    for seed in SEEDS:
+        torch.manual_seed(seed)
+        ref = VGG().to(gpu)
+        nat = VGG()
+        nat.load_state_dict(ref.state_dict())
+        nat.use_native = True
+        ddpx.prepare_model(nat, gpu)
+        assert nat.input_layout(gpu) == "nhwc8_bf16"
+
         o_ref = torch.optim.SGD(ref.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4)
         s_ref = torch.optim.lr_scheduler.LambdaLR(o_ref, lam)
-        l_ref = _train(ref, DeviceLoader(train, B, gpu, layout="nchw_f32", seed=0), o_ref, s_ref, steps, False)
-        refs.append((l_ref, _accuracy(ref, DeviceLoader(test, B, gpu, train=False, layout="nchw_f32"))))
+        l_ref = _train(ref, DeviceLoader(train, B, gpu, layout="nchw_f32", seed=seed), o_ref, s_ref, steps, False)
+        a_ref = _accuracy(ref, DeviceLoader(test, B, gpu, train=False, layout="nchw_f32"))
 
-    o_nat = SGD(nat.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, fused_backward=True)
-    s_nat = torch.optim.lr_scheduler.LambdaLR(o_nat, lam)
-    l_nat = _train(nat, DeviceLoader(train, B, gpu, layout="nhwc8_bf16", seed=0), o_nat, s_nat, steps, True)
-    torch.cuda.synchronize()
+        o_nat = SGD(nat.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4, fused_backward=True)
+        s_nat = torch.optim.lr_scheduler.LambdaLR(o_nat, lam)
+        l_nat = _train(nat, DeviceLoader(train, B, gpu, layout="nhwc8_bf16", seed=seed), o_nat, s_nat, steps, True)
+        a_nat = _accuracy(nat, DeviceLoader(test, B, gpu, train=False, layout="nhwc8_bf16"))
+        torch.cuda.synchronize()
 
-    assert torch.isfinite(l_nat).all() and all(torch.isfinite(lr_).all() for lr_, _ in refs)
-    tails = [lr_[-20:].mean().item() for lr_, _ in refs]
-    accs = [a for _, a in refs]
-    tail_ref, acc_ref = sum(tails) / 2, sum(accs) / 2
-    tail_nat = l_nat[-20:].mean().item()
-    acc_nat = _accuracy(nat, DeviceLoader(test, B, gpu, train=False, layout="nhwc8_bf16"))
-    print(f"\nloss last-20 ref {tails[0]:.4f} / {tails[1]:.4f} native {tail_nat:.4f}; test accuracy ref "
-          f"{accs[0]:.2f}% / {accs[1]:.2f}% native {acc_nat:.2f}%")
-    # both learn the task ...
-    for lr_, a in refs:
-        assert lr_[-20:].mean().item() < 0.8 * lr_[:10].mean().item() and a > 30.0
-    # ... and end in the same place: bf16 compute vs fp32 changes the trajectory, not the outcome
-    assert abs(tail_nat - tail_ref) < max(0.05, 0.25 * tail_ref) + abs(tails[0] - tails[1]), (tail_nat, tails)
-    assert abs(acc_nat - acc_ref) < 5.0 + abs(accs[0] - accs[1]), (acc_nat, accs)
+        assert torch.isfinite(l_nat).all() and torch.isfinite(l_ref).all()
+        # both learn the task on every seed
+        assert l_ref[-20:].mean().item() < 0.8 * l_ref[:10].mean().item() and a_ref > 30.0, (seed, l_ref, a_ref)
+        assert l_nat[-20:].mean().item() < 0.8 * l_nat[:10].mean().item() and a_nat > 30.0, (seed, l_nat, a_nat)
+        rows.append((l_ref[-20:].mean().item(), l_nat[-20:].mean().item(), a_ref, a_nat))
+        print(f"\nseed {seed}: loss last-20 fp32 {rows[-1][0]:.4f} native {rows[-1][1]:.4f}; "
+              f"test accuracy fp32 {a_ref:.2f}% native {a_nat:.2f}%")
+
+    n = len(rows)
+
+    def mean_sd(v):
+        m = sum(v) / len(v)
+        return m, math.sqrt(sum((x - m) ** 2 for x in v) / (len(v) - 1))
+
+    tail_ref, _ = mean_sd([r[0] for r in rows])
+    tail_nat, _ = mean_sd([r[1] for r in rows])
+    acc_ref, _ = mean_sd([r[2] for r in rows])
+    acc_nat, _ = mean_sd([r[3] for r in rows])
+    _, sd_dt = mean_sd([r[1] - r[0] for r in rows])
+    _, sd_da = mean_sd([r[3] - r[2] for r in rows])
+    print(f"\nmean over {n} seeds: loss fp32 {tail_ref:.4f} native {tail_nat:.4f} (paired sd {sd_dt:.4f}); "
+          f"accuracy fp32 {acc_ref:.2f}% native {acc_nat:.2f}% (paired sd {sd_da:.2f})")
+    # the same outcome: bf16 compute vs fp32 changes each trajectory, not where the ensemble ends
+    assert abs(tail_nat - tail_ref) < max(0.05, 0.25 * tail_ref), rows
+    assert abs(acc_nat - acc_ref) < 4.0, rows
