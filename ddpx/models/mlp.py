@@ -54,6 +54,13 @@ class MLP(nn.Module):
         fc0 = self.fc0
         return getattr(fc0.weight, "_ddpx_shadow", None) is not None and not x.requires_grad
 
+    def _cpu_fused_ok(self, x):
+        """CPU training step on a FlatParams store: one autograd node writing the flat gradients (ops/mlp_cpu)."""
+        if not self.use_native or x.is_cuda:
+            return False
+        from ..ops import mlp_cpu
+        return mlp_cpu.eligible(self, x)
+
     def _flatten(self, x):
         return x.reshape(x.shape[0], -1)
 
@@ -77,6 +84,9 @@ class MLP(nn.Module):
         if self._native_ok(x):
             from ..ops import mlp as mlp_ops
             return mlp_ops.mlp_logits(self, self._flatten(x))
+        if self._cpu_fused_ok(x):
+            from ..ops import mlp_cpu
+            return mlp_cpu.mlp_logits(self, self._flatten(x).float())
         return self._torch_forward(x)
 
     def forward_loss(self, x: torch.Tensor, targets: torch.Tensor):
@@ -87,7 +97,7 @@ class MLP(nn.Module):
         if self._native_ok(x):
             from ..ops import mlp as mlp_ops
             return mlp_ops.mlp_loss(self, self._flatten(x), targets), None
-        logits = self._torch_forward(x)
+        logits = self.forward(x)
         return F.cross_entropy(logits, targets), logits
 
     # ---- ddpx engine protocol -------------------------------------------------

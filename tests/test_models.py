@@ -110,3 +110,32 @@ def test_mlp_cpu_forward_loss():
     loss, logits = m.forward_loss(x, t)
     assert logits.shape == (16, 10)
     assert torch.allclose(loss, torch.nn.functional.cross_entropy(m(x), t))
+
+
+def test_mlp_cpu_one_node_backward_matches_torch():
+    """ops/mlp_cpu: the CPU training step writes the flat gradients directly (no per-parameter .grad), in
+    grad-ready order, equal to torch autograd's, including accumulation over two backwards."""
+    import copy
+
+    import ddpx
+    torch.manual_seed(0)
+    m = MLP(in_features=3072, hidden=96, layers=4)
+    ref = copy.deepcopy(m)
+    ddpx.prepare_model(m, "cpu")
+    flat = m.fc0.weight._ddpx_flat
+    order = []
+    orig = flat.grad_done
+    pos = {id(p): i for i, p in enumerate(m.parameters())}  # fc0.w, fc0.b, ..., fc3.w, fc3.b
+    flat.grad_done = lambda p, chunk=None: (order.append(pos[id(p)] // 2), orig(p, chunk))[1]
+    x = torch.rand(24, 3, 32, 32)
+    t = torch.randint(0, 10, (24,))
+    for _ in range(2):
+        loss, logits = m.forward_loss(x, t)
+        loss.backward()
+        l_ref = torch.nn.functional.cross_entropy(ref(x), t)
+        l_ref.backward()
+        assert torch.allclose(loss, l_ref, atol=1e-6)
+    assert order[:8] == [3, 3, 2, 2, 1, 1, 0, 0]  # classifier first (gradient-ready order)
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert p.grad is None
+        assert torch.allclose(p.main_grad, q.grad, atol=1e-6)
