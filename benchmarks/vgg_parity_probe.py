@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--seeds", type=int, default=1)
+    ap.add_argument("--noise", type=float, default=230.0)
+    ap.add_argument("--merges", default="legacy,split,bwd", help="native BN merge orders to run")
     a = ap.parse_args()
     import ddpx
     from ddpx.data.datasets import synthetic_cifar
@@ -35,8 +37,8 @@ def main():
     gpu = torch.device("cuda", 0)
     steps, B = a.steps, a.batch
     ref = VGG().to(gpu)
-    train = synthetic_cifar(8192, seed=0, noise=230.0)
-    test = synthetic_cifar(2048, seed=0, noise=230.0, split_seed_offset=7)
+    train = synthetic_cifar(8192, seed=0, noise=a.noise)
+    test = synthetic_cifar(2048, seed=0, noise=a.noise, split_seed_offset=7)
     lam = OneCycleLambda(steps_per_epoch=steps // 20, num_epochs=20)
 
     def torch_run(amp, init, seed):
@@ -68,13 +70,14 @@ def main():
                     ("torch_bf16_autocast", lambda: torch_run(True, init, seed))]
         else:
             runs = [("torch_fp32", lambda: torch_run(False, init, seed))]
-        for name, m in (("native_bf16_merge_legacy", 1), ("native_bf16_merge_split", 0), ("native_bf16_merge_bwd", 2)):
-            runs.append((name, lambda m=m: native_run(m, init, seed)))
+        for name, m in (("legacy", 1), ("split", 0), ("bwd", 2)):
+            if name in a.merges.split(","):
+                runs.append(("native_bf16_merge_" + name, lambda m=m: native_run(m, init, seed)))
         for name, fn in runs:
             loss, acc = fn()
-            print(json.dumps({"run": name, "seed": seed, "tail20": round(loss[-20:].mean().item(), 4),
+            print(json.dumps({"run": name, "seed": seed, "batch": B, "noise": a.noise, "steps": steps, "tail20": round(loss[-20:].mean().item(), 4),
                               "head10": round(loss[:10].mean().item(), 4), "test_acc": round(acc, 2)}), flush=True)
-        native.kernels().ddpx_bn_set_merge(1)
+        native.kernels().ddpx_bn_set_merge(-1)
 
 
 if __name__ == "__main__":

@@ -123,17 +123,19 @@ finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, co
 // merges the S partials in split order: deterministic, and the hand-off is MI355X_MICROARCH "Valid forms" row 1
 // (sc1 stores drained by vmcnt(0) before the ticket, sc1 loads after it).  Tickets reset by their last arriver.
 constexpr int kMergeMaxC = 1024, kFinMaxS = 32, kBwdMaxS = 32;
-// Which merges use the two-level kernels: 0 both, 1 neither (the per-channel kernels above; default), 2 the
-// backward sums only.  Split, the forward statistics merge measured no faster (86.8 vs 87 us per VGG step) and
-// the backward one 83 -> 61 us; both match fp64 like the per-channel ones (tests/test_gpu_vgg.py), but the
-// changed summation order moves the deterministic bf16 VGG trajectory of tests/test_gpu_parity.py from a tail
-// loss of 0.53 (per-channel) to 0.65-0.71 against torch fp32's 0.47-0.56 (profiles/r3_bn/NOTES.md), so the
-// per-channel merges stay the default.  DDPX_BN_MERGE=split|legacy|bwd, or ddpx_bn_set_merge(mode).
+// Which merges use the two-level kernels: 0 both, 1 neither (the per-channel kernels above), 2 the backward sums
+// only (default).  Split, the forward statistics merge measured no faster (86.8 vs 87 us per VGG step) and the
+// backward one 83 -> 61 us; both match fp64 like the per-channel ones (tests/test_gpu_vgg.py).  A changed
+// summation order moves any single deterministic bf16 VGG trajectory (0.53 -> 0.71 tail loss on one seed,
+// profiles/r3_bn), but over an ensemble of seeds at the reference's batch size the three orders end in the same
+// place as torch fp32 (profiles/r4_parity: mean last-20 loss fp32 0.415, per-channel 0.320, split 0.329, backward
+// split 0.430), which is what tests/test_gpu_parity.py now checks.  DDPX_BN_MERGE=split|legacy|bwd, or
+// ddpx_bn_set_merge(mode) (mode < 0: back to the environment / default).
 static int g_merge_mode = -1;
 static inline int merge_mode() {
   if (g_merge_mode < 0) {
     const char* e = getenv("DDPX_BN_MERGE");
-    g_merge_mode = !e ? 1 : (e[0] == 's' ? 0 : (e[0] == 'b' ? 2 : 1));
+    g_merge_mode = !e ? 2 : (e[0] == 's' ? 0 : (e[0] == 'l' ? 1 : 2));
   }
   return g_merge_mode;
 }
@@ -677,7 +679,7 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const unsigned short* 
 
 using namespace ddpx;
 
-DDPX_API void ddpx_bn_set_merge(int mode) { bn::g_merge_mode = mode < 0 || mode > 2 ? 1 : mode; }
+DDPX_API void ddpx_bn_set_merge(int mode) { bn::g_merge_mode = mode < 0 || mode > 2 ? -1 : mode; }
 
 DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,

@@ -126,9 +126,12 @@ static int pick_fwd(int P, int Co) {
   if (P >= 524288) return 8;  // 32x32 layers: 256x128, 8 waves
   return 13;                  // 256x256, 8 waves
 }
+// Data-gradient picks do not change any result bit (every tile sums K in the same order, no statistics), so
+// they follow the round-4 sweep directly (profiles/r4_final/conv_sweep.json): VGG conv1's dx 64x64 (163 vs
+// 168 us), the 4x4 layers 8-wave 128x128 / 4 stages (66 vs 73 us).
 static int pick_dgrad(int P, int C, int Co) {
-  if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32): 128x64, 3 stages
-  if (P <= 8192) return 5;
+  if (C <= 64) return Co >= 128 ? 7 : 6;  // dx of a 64-channel input: 64x64 (VGG conv1 @32) / 128x64 (DeepNN)
+  if (P <= 8192) return 15;
   if (Co <= 64 || Co > C) return 8;  // widening layers (dx narrower than dy) and thin DeepNN layers
   return 13;
 }
@@ -217,7 +220,10 @@ static int pick_wgrad(int P, int C, int Co) {
   // M = Co <= 64 (DeepNN's 128->64, 64->64, 64->32 layers): a 256-row tile would be 3/4 empty;
   // 64x64 / 3 stages measured 2.6x faster on 128->64@32 (profiles/r1_deepnn/conv_sweep_deepnn.json)
   if (Co <= 64) return 7;
-  if (C <= 64) return 7;      // VGG conv1 (64->128 @32): 64x64 (259 vs 280 us for 128x128)
+  // VGG conv1 (64->128 @32): 8-wave 128x128 / 4 stages (156 vs 181 us for 64x64 in the round-4 sweep,
+  // profiles/r4_final/conv_sweep.json; a different split-K summation order, judged by the multi-seed
+  // tests/test_gpu_parity.py)
+  if (C <= 64) return 15;
   return 13;                  // 256x256, 8 waves (283 vs 393 us for 256x128 on 256->256@16)
 }
 

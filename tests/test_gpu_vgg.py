@@ -210,8 +210,9 @@ def test_native_sync_batchnorm_kernels_match_local_bn(gpu):
 @pytest.mark.parametrize("N,H,Ci,Co", [(512, 32, 8, 64), (512, 8, 256, 256), (64, 4, 512, 512), (5, 6, 16, 24)])
 def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
     """BatchNorm statistics from the conv epilogue's tile partials: the two-level channel-coalesced merges
-    (mode 0, DDPX_BN_MERGE=split) and the per-channel ones (mode 1, the default) both match an fp64 reduction of the stored bf16 outputs (batch mean / biased variance /
-    running stats), and so do the backward sums (c1, c2, dgamma, dbeta)."""
+    (mode 0, DDPX_BN_MERGE=split) and the per-channel ones (mode 1) both match an fp64 reduction of the stored
+    bf16 outputs (batch mean / biased variance / running stats), and so do the backward sums (c1, c2, dgamma,
+    dbeta); the default (mode 2) pairs the per-channel forward merge with the split backward one."""
     from ddpx.ops import conv as K
     from ddpx.runtime import native
     torch.manual_seed(3)
@@ -236,7 +237,7 @@ def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
             torch.cuda.synchronize()
             outs[legacy] = (mean.clone(), rstd.clone(), bn.running_var.clone(), dgam, dbet, dy.float())
     finally:
-        lib.ddpx_bn_set_merge(1)
+        lib.ddpx_bn_set_merge(-1)
     rstd64 = (var64 + 1e-5).rsqrt()
     xhat64 = (y64 - mean64) * rstd64
     gz64 = xhat64.gt(0).double() * g.double()  # gamma 1, beta 0: ReLU mask of xhat (a rare fp32 flip at 0 is
