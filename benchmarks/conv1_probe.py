@@ -32,7 +32,29 @@ def timed(fn, reps=20):
     return round(ts[len(ts) // 2], 1)
 
 
+def ksweep():
+    """Per-tile fixed cost vs per-K-step cost at the 32x32 geometry: the 256x128 forward tile over input channel
+    counts C = 64..512 (K = 9 C, 9..72 K-steps per tile), Co = 128."""
+    from ddpx.ops import conv as K
+    dev = torch.device("cuda", 0)
+    N, H, W, Co = 512, 32, 32, 128
+    for C in (64, 128, 256, 512):
+        x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+        w = torch.randn(Co, C, 3, 3, device=dev) * 0.05
+        wf = torch.empty(Co * 9 * C, dtype=torch.bfloat16, device=dev)
+        wd = torch.empty_like(wf)
+        K.weight_prep(w, wf, wd)
+        fl = 2.0 * N * H * W * Co * 9 * C
+        for stats in (False, True):
+            us = timed(lambda: K.conv_fwd(x, wf, Co, stats=stats, tile=8))
+            print(json.dumps({"case": f"ksweep_C{C}_stats{int(stats)}", "ksteps": 9 * C // 64, "us": us,
+                              "tflops": round(fl / us / 1e6, 1)}), flush=True)
+        del x, w, wf, wd
+
+
 def main():
+    if "--ksweep" in sys.argv:
+        return ksweep()
     from ddpx.ops import conv as K
     from ddpx.ops import gemm as G
     dev = torch.device("cuda", 0)
