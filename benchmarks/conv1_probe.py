@@ -52,9 +52,27 @@ def ksweep():
         del x, w, wf, wd
 
 
+def pmc_case(C):
+    """Five launches of the 256x128 forward (statistics epilogue) at C input channels, 32x32, Co 128: the
+    kernel a rocprofv3 --pmc pass reads."""
+    from ddpx.ops import conv as K
+    dev = torch.device("cuda", 0)
+    N, H, W, Co = 512, 32, 32, 128
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(Co, C, 3, 3, device=dev) * 0.05
+    wf = torch.empty(Co * 9 * C, dtype=torch.bfloat16, device=dev)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w, wf, wd)
+    for _ in range(5):
+        K.conv_fwd(x, wf, Co, stats=True, tile=8)
+    torch.cuda.synchronize()
+
+
 def main():
     if "--ksweep" in sys.argv:
         return ksweep()
+    if "--pmc" in sys.argv:
+        return pmc_case(int(sys.argv[sys.argv.index("--pmc") + 1]))
     from ddpx.ops import conv as K
     from ddpx.ops import gemm as G
     dev = torch.device("cuda", 0)

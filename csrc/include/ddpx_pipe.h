@@ -114,6 +114,7 @@ struct Params {
   void* cs_out;
   int cs_flags;
   int* cs_tcnt;
+  int im_slow;             // 1: im2col A operands use the per-chunk src_off path (A/B checks of ImRows)
 };
 
 constexpr unsigned kOOB = 0x80000000u;
@@ -185,6 +186,52 @@ __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t rs, char* slot
 #pragma unroll
   for (int j = 0; j < NI; ++j)
     dma16(rs, slot + (j * NW + wave) * 1024, tile_voff<ROWS, KC, MODE, NW>(g, ld, row0, nrows, k0, kend, wave, lane, j));
+}
+
+// im2col A operand (K-contig rows = output pixels) with C % 64 == 0: every 64-wide K-step lies inside ONE tap,
+// so the tap, its pixel shift and the channel base are wave-uniform (scalar) per K-step, and everything that
+// depends on the row — the pixel's (h, w) and its byte base — is computed once per tile.  The per-chunk work
+// drops from two fast divisions, the tap divide and ~35 VALU (the 256x128 forward's K-step spent ~100 VALU on
+// operand addresses between its barrier and its first MFMA, profiles/r4_vgg) to a bounds test and an add.
+// Offsets are exactly src_off's (same bytes, same zero fill).
+template <int ROWS, int NW>
+struct ImRows {
+  static constexpr int NI = ROWS / (8 * NW);
+  int hw[NI];         // (h << 16) | w of the row's pixel; h = 0x4000 for rows past nrows (always out of bounds)
+  unsigned base[NI];  // byte offset of (pixel, first channel of this lane's chunk) in the NHWC tensor
+};
+
+template <int ROWS, int NW>
+__device__ __forceinline__ void im_rows_init(ImRows<ROWS, NW>& ir, const ConvGeom& g, int row0, int nrows, int wave,
+                                             int lane) {
+#pragma unroll
+  for (int j = 0; j < ImRows<ROWS, NW>::NI; ++j) {
+    const int r = (j * NW + wave) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int p = row0 + r;
+    const int pw = fdiv(p, g.dW);
+    const int w = p - pw * g.W;
+    const int h = pw - fdiv(pw, g.dH) * g.H;
+    ir.hw[j] = p < nrows ? ((h << 16) | w) : (0x4000 << 16);
+    ir.base[j] = (unsigned)((p * g.C + c * 8) * 2);
+  }
+}
+
+template <int ROWS, int MODE, int NW>
+__device__ __forceinline__ void stage_tile_im(__amdgpu_buffer_rsrc_t rs, char* slot, const ConvGeom& g,
+                                              const ImRows<ROWS, NW>& ir, int k0, int wave) {
+  // wave-uniform per K-step: tap, channel base, pixel shift
+  const int tap = fdiv(k0, g.dC), c0 = k0 - tap * g.C;
+  const int ky = (tap * 11) >> 5, kx = tap - ky * 3;
+  int dy = ky - 1, dx = kx - 1;
+  if constexpr (MODE == MODE_IM2COL_BWD) { dy = -dy; dx = -dx; }
+  const int shift = ((dy * g.W + dx) * g.C + c0) * 2;
+#pragma unroll
+  for (int j = 0; j < ImRows<ROWS, NW>::NI; ++j) {
+    const int hh = (ir.hw[j] >> 16) + dy, ww = (ir.hw[j] & 0xffff) + dx;
+    const bool ok = (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+    dma16(rs, slot + (j * NW + wave) * 1024, ok ? ir.base[j] + (unsigned)shift : kOOB);
+  }
 }
 
 // K-contig fragment (ds_read_b128 of the swizzled [row][64] image): an ordinary LDS load the compiler's
@@ -496,12 +543,25 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
 
   const int nk = (kend - kbeg + BK - 1) / BK;
 
+  // im2col A operand with whole taps per K-step: row addressing cached for the tile (ImRows)
+  constexpr bool A_IM = AK && (AMODE == MODE_IM2COL_FWD || AMODE == MODE_IM2COL_BWD);
+  ImRows<A_IM ? BM : 8 * NW, NW> arow;
+  const bool a_fast = A_IM && !p.im_slow && (p.conv.C & 63) == 0;
+  if constexpr (A_IM) {
+    if (a_fast) im_rows_init<BM, NW>(arow, p.conv, m0, p.M, wave, lane);
+  }
+
   auto issue = [&](int t) {
     char* slot = smem + (t % STAGES) * SLOT;
 #pragma unroll
     for (int u = 0; u < KSUB; ++u) {
       const int k0 = kbeg + t * BK + u * 64;
-      stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+      if constexpr (A_IM) {
+        if (a_fast) stage_tile_im<BM, AMODE, NW>(ra, slot + u * A_SUB, p.conv, arow, k0, wave);
+        else stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+      } else {
+        stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
+      }
       stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
     }
   };

@@ -127,10 +127,11 @@ static int pick_fwd(int P, int Co) {
   return 13;                  // 256x256, 8 waves
 }
 // Data-gradient picks do not change any result bit (every tile sums K in the same order, no statistics), so
-// they follow the round-4 sweep directly (profiles/r4_final/conv_sweep.json): VGG conv1's dx 64x64 (163 vs
-// 168 us), the 4x4 layers 8-wave 128x128 / 4 stages (66 vs 73 us).
+// they follow the round-4 measurements directly: VGG conv1's dx 128x64 with the cached im2col rows (141 vs
+// 153 us for 64x64, profiles/r4_vgg/probe_*.jsonl), the 4x4 layers 8-wave 128x128 / 4 stages (66 vs 73 us,
+// profiles/r4_final/conv_sweep.json).
 static int pick_dgrad(int P, int C, int Co) {
-  if (C <= 64) return Co >= 128 ? 7 : 6;  // dx of a 64-channel input: 64x64 (VGG conv1 @32) / 128x64 (DeepNN)
+  if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32, DeepNN): 128x64, 3 stages
   if (P <= 8192) return 15;
   if (Co <= 64 || Co > C) return 8;  // widening layers (dx narrower than dy) and thin DeepNN layers
   return 13;
@@ -143,6 +144,19 @@ using namespace ddpx;
 using namespace ddpx::pipe;
 
 static bool chk16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// DDPX_IM2COL_ROWCACHE=0: per-chunk im2col addressing for the forward / data-gradient A operand (A/B checks)
+static int g_im_slow = -1;
+static int im_slow() {
+  if (g_im_slow < 0) {
+    const char* e = getenv("DDPX_IM2COL_ROWCACHE");
+    g_im_slow = (e && e[0] == '0') ? 1 : 0;
+  }
+  return g_im_slow;
+}
+// 1: cached row addressing (default), 0: per-chunk addressing, < 0: back to the environment / default
+DDPX_API void ddpx_conv_set_rowcache(int on) { g_im_slow = on < 0 ? -1 : (on ? 0 : 1); }
+
 
 DDPX_API int ddpx_conv_weight_prep(const float* w, int Co, int Cr, int Cp, void* wf, void* wd, hipStream_t s) {
   if (Cp % 8 || Cp < Cr) return -1;
@@ -183,6 +197,7 @@ DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats,
   p.lda = C; p.ldb = K; p.ldc = Co;
   p.epi = stats ? EPI_BNSTAT_BF16 : EPI_BF16;
   p.alpha = 1.f;
+  p.im_slow = im_slow();
   const size_t ab = (size_t)P * C * 2, bb = (size_t)Co * K * 2;
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
@@ -206,6 +221,7 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   p.lda = Co; p.ldb = C; p.ldc = C;
   p.epi = EPI_BF16;
   p.alpha = 1.f;
+  p.im_slow = im_slow();
   const size_t ab = (size_t)P * Co * 2, bb = (size_t)K * C * 2;
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;

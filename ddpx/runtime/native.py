@@ -69,6 +69,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_augment_cursor", I, P, P, P, I, I, I, I, I, I, c_uint64, I, I, P, P, P, P)
     _sig(lib, "ddpx_conv_weight_prep", I, P, I, I, I, P, P, P)
     _sig(lib, "ddpx_bn_set_merge", None, I)
+    _sig(lib, "ddpx_conv_set_rowcache", None, I)
     _sig(lib, "ddpx_conv_fwd_tiles_m", I, I, I, I)
     _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I)
     _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)

@@ -251,3 +251,34 @@ def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
     # the two merges differ only by fp32 rounding of the merge order
     assert _rel(outs[0][0], outs[1][0]) < 1e-5 and _rel(outs[0][1], outs[1][1]) < 1e-5
     assert _rel(outs[0][5], outs[1][5]) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,Co,tile", [(8, 32, 64, 128, -1), (4, 32, 64, 128, 7), (3, 16, 128, 256, -1),
+                                            (2, 8, 256, 512, -1), (5, 4, 512, 512, -1), (3, 6, 64, 64, 5),
+                                            (2, 32, 8, 64, -1)])
+def test_im2col_row_cache_bitwise(gpu, N, H, C, Co, tile):
+    """The cached im2col row addressing (ImRows, csrc/include/ddpx_pipe.h; C % 64 == 0) loads exactly the
+    bytes the per-chunk path does: forward output, its BatchNorm tile statistics and the data gradient are
+    bitwise equal with ddpx_conv_set_rowcache(0) (ragged tiles and the C = 8 fallback included)."""
+    from ddpx.ops import conv as K
+    from ddpx.runtime import native
+    lib = native.kernels()
+    torch.manual_seed(5)
+    xn = torch.randn(N, H, H, C, device=gpu).to(torch.bfloat16).contiguous()
+    w = torch.randn(Co, C, 3, 3, device=gpu) * (1.0 / (C * 9) ** 0.5)
+    wf = torch.empty(Co * 9 * C, dtype=torch.bfloat16, device=gpu)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w, wf, wd)
+    dy = torch.randn(N * H * H, Co, device=gpu).to(torch.bfloat16).contiguous()
+    outs = []
+    try:
+        for on in (1, 0):
+            lib.ddpx_conv_set_rowcache(on)
+            y, st, T, BM = K.conv_fwd(xn, wf, Co, tile=tile)
+            dx = K.conv_dgrad(dy, wd, N, H, H, C, Co, tile=tile)
+            torch.cuda.synchronize()
+            outs.append((y, st, dx))
+    finally:
+        lib.ddpx_conv_set_rowcache(-1)
+    (y1, s1, d1), (y0, s0, d0) = outs
+    assert torch.equal(y1, y0) and torch.equal(s1, s0) and torch.equal(d1, d0)
