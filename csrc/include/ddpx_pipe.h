@@ -234,6 +234,58 @@ __device__ __forceinline__ void stage_tile_im(__amdgpu_buffer_rsrc_t rs, char* s
   }
 }
 
+// im2col N-contig operand of the weight gradient (k-rows = pixels, columns = (tap, channel)) when the image
+// width divides 64: a lane's column, hence its tap shift, channel and column bounds, is fixed for the tile,
+// and so is its pixel's w (k0 is a multiple of 64, so of W); per K-step only h = (k0 / W + kr / W) mod H and
+// the K-tail test remain.  Two registers per wave-instruction: the byte offset relative to pixel k0, and
+// kr | (kr / W) << 8 | (dy + 1) << 16 | column-valid << 24.  Offsets are exactly src_off's.
+template <int ROWS, int NW>
+struct ColRows {
+  static constexpr int NI = ROWS / (8 * NW);
+  unsigned base[NI];
+  unsigned kv[NI];
+};
+
+template <int ROWS, int NW>
+__device__ __forceinline__ void col_rows_init(ColRows<ROWS, NW>& cr, const ConvGeom& g, int col0, int ncols, int wave,
+                                              int lane) {
+  constexpr int ROWB = ROWS * 2;
+  constexpr int CPR = ROWB / 16;
+#pragma unroll
+  for (int j = 0; j < ColRows<ROWS, NW>::NI; ++j) {
+    const int inst = j * NW + wave;
+    const int kr = inst * (1024 / ROWB) + lane / CPR;
+    const int q = lane % CPR;
+    const int L = (q >> 1) ^ tr_swz<ROWB>(kr);
+    const int gr = col0 + L * 16 + (q & 1) * 8;
+    const int tap = fdiv(gr, g.dC), c = gr - tap * g.C;
+    const int ky = (tap * 11) >> 5, kx = tap - ky * 3;
+    const int dy = ky - 1, dx = kx - 1;
+    const int v = fdiv(kr, g.dW), w = kr - v * g.W;
+    const bool ok = gr < ncols && tap < 9 && (unsigned)(w + dx) < (unsigned)g.W;
+    cr.base[j] = (unsigned)(((kr + dy * g.W + dx) * g.C + c) * 2);
+    cr.kv[j] = (unsigned)kr | ((unsigned)v << 8) | ((unsigned)(dy + 1) << 16) | ((unsigned)ok << 24);
+  }
+}
+
+template <int ROWS, int NW>
+__device__ __forceinline__ void stage_tile_col(__amdgpu_buffer_rsrc_t rs, char* slot, const ConvGeom& g,
+                                               const ColRows<ROWS, NW>& cr, int k0, int kend, int wave) {
+  const int pw0 = fdiv(k0, g.dW);                  // exact: W divides k0
+  const int sH = pw0 - fdiv(pw0, g.dH) * g.H;      // h of pixel k0
+  const unsigned kb = (unsigned)k0 * (unsigned)g.C * 2u;
+  const int krem = kend - k0;
+#pragma unroll
+  for (int j = 0; j < ColRows<ROWS, NW>::NI; ++j) {
+    const unsigned kv = cr.kv[j];
+    const int t = sH + (int)((kv >> 8) & 0xffu);
+    const int h = t - fdiv(t, g.dH) * g.H;
+    const int hh = h + (int)((kv >> 16) & 3u) - 1;
+    const bool ok = (kv >> 24) && (int)(kv & 0xffu) < krem && (unsigned)hh < (unsigned)g.H;
+    dma16(rs, slot + (j * NW + wave) * 1024, ok ? kb + cr.base[j] : kOOB);
+  }
+}
+
 // K-contig fragment (ds_read_b128 of the swizzled [row][64] image): an ordinary LDS load the compiler's
 // waitcnt pass tracks.
 template <int ROWS>
@@ -550,6 +602,13 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   if constexpr (A_IM) {
     if (a_fast) im_rows_init<BM, NW>(arow, p.conv, m0, p.M, wave, lane);
   }
+  // weight-gradient im2col B operand with an image width dividing 64: column addressing cached (ColRows)
+  constexpr bool B_COL = !BKc && BMODE == MODE_IM2COL_COL;
+  ColRows<B_COL ? BN : 8 * NW, NW> bcol;
+  const bool b_fast = B_COL && !p.im_slow && (64 % p.conv.W) == 0;
+  if constexpr (B_COL) {
+    if (b_fast) col_rows_init<BN, NW>(bcol, p.conv, n0, p.N, wave, lane);
+  }
 
   auto issue = [&](int t) {
     char* slot = smem + (t % STAGES) * SLOT;
@@ -562,7 +621,12 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
       } else {
         stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
       }
-      stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+      if constexpr (B_COL) {
+        if (b_fast) stage_tile_col<BN, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, bcol, k0, kend, wave);
+        else stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+      } else {
+        stage_tile<BN, BKc, BMODE, NW>(rb, slot + A_BYTES + u * B_SUB, p.conv, p.ldb, n0, p.N, k0, kend, wave, lane);
+      }
     }
   };
 

@@ -295,6 +295,7 @@ DDPX_API int ddpx_conv_wgrad(const void* dy, const void* x, float* part, int S, 
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = make_geom(H, W, C, P);
+  p.im_slow = im_slow();
   p.klen = ((P + S - 1) / S + 63) / 64 * 64;
   p.split_stride = (long long)Co * 9 * C;
   const int Sreal = (P + p.klen - 1) / p.klen;

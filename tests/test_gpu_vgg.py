@@ -257,9 +257,11 @@ def test_bn_merges_match_fp64(gpu, N, H, Ci, Co):
                                             (2, 8, 256, 512, -1), (5, 4, 512, 512, -1), (3, 6, 64, 64, 5),
                                             (2, 32, 8, 64, -1)])
 def test_im2col_row_cache_bitwise(gpu, N, H, C, Co, tile):
-    """The cached im2col row addressing (ImRows, csrc/include/ddpx_pipe.h; C % 64 == 0) loads exactly the
-    bytes the per-chunk path does: forward output, its BatchNorm tile statistics and the data gradient are
-    bitwise equal with ddpx_conv_set_rowcache(0) (ragged tiles and the C = 8 fallback included)."""
+    """The cached im2col addressing (ImRows for the forward / data-gradient A operand when C % 64 == 0,
+    ColRows for the weight-gradient B operand when W divides 64; csrc/include/ddpx_pipe.h) loads exactly the
+    bytes the per-chunk path does: forward output, its BatchNorm tile statistics, the data gradient and the
+    weight gradient are bitwise equal with ddpx_conv_set_rowcache(0) (ragged tiles, W = 6 and the C = 8
+    fallbacks included)."""
     from ddpx.ops import conv as K
     from ddpx.runtime import native
     lib = native.kernels()
@@ -276,9 +278,11 @@ def test_im2col_row_cache_bitwise(gpu, N, H, C, Co, tile):
             lib.ddpx_conv_set_rowcache(on)
             y, st, T, BM = K.conv_fwd(xn, wf, Co, tile=tile)
             dx = K.conv_dgrad(dy, wd, N, H, H, C, Co, tile=tile)
+            dw = torch.empty(Co, C, 3, 3, device=gpu)
+            K.conv_wgrad(dy, xn, Co, C, out=dw, tile=tile)
             torch.cuda.synchronize()
-            outs.append((y, st, dx))
+            outs.append((y, st, dx, dw))
     finally:
         lib.ddpx_conv_set_rowcache(-1)
-    (y1, s1, d1), (y0, s0, d0) = outs
-    assert torch.equal(y1, y0) and torch.equal(s1, s0) and torch.equal(d1, d0)
+    (y1, s1, d1, w1), (y0, s0, d0, w0) = outs
+    assert torch.equal(y1, y0) and torch.equal(s1, s0) and torch.equal(d1, d0) and torch.equal(w1, w0)
