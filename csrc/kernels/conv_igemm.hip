@@ -101,17 +101,24 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     const size_t i = base + q;
     if (sgd.p) {
       const float pn = sgd_apply(sgd, i, v, *sgd.lr);
-      if (wf) {  // the forward / dgrad GEMM layouts of the updated weight (weight_prep's output)
-        const unsigned short h = f2bf(pn);
-        wf[((size_t)o * 9 + t) * Cp + c0 + cc] = h;
-        wd[((size_t)t * Co + o) * Cp + c0 + cc] = h;
-      }
+      if (wf) red[t][cc] = pn;  // (this thread's own element) -> the layout writes below
     } else if (out_bf16) {
       unsigned short* d = reinterpret_cast<unsigned short*>(out) + i;
       *d = f2bf(accumulate ? v + bf2f(*d) : v);
     } else {
       float* d = reinterpret_cast<float*>(out) + i;
       *d = accumulate ? v + *d : v;
+    }
+  }
+  if (sgd.p && wf) {
+    // the forward / dgrad GEMM layouts of the updated weight (weight_prep's output), channel-fastest: a wave
+    // writes 128 contiguous bytes of each [.][tap][channel] row instead of 2-byte stores 9 taps apart
+    __syncthreads();
+    for (int q = threadIdx.x; q < nc * 9; q += 256) {
+      const int t = q / nc, cc = q - t * nc;
+      const unsigned short h = f2bf(red[t][cc]);
+      wf[((size_t)o * 9 + t) * Cp + c0 + cc] = h;
+      wd[((size_t)t * Co + o) * Cp + c0 + cc] = h;
     }
   }
 }

@@ -286,3 +286,35 @@ def test_im2col_row_cache_bitwise(gpu, N, H, C, Co, tile):
         lib.ddpx_conv_set_rowcache(-1)
     (y1, s1, d1, w1), (y0, s0, d0, w0) = outs
     assert torch.equal(y1, y0) and torch.equal(s1, s0) and torch.equal(d1, d0) and torch.equal(w1, w0)
+
+
+@pytest.mark.parametrize("N,H,C,Co", [(4, 8, 256, 512), (2, 16, 64, 128), (3, 4, 512, 512), (2, 32, 8, 64)])
+def test_wgrad_fused_sgd_writes_prepared_layouts(gpu, N, H, C, Co):
+    """conv_wgrad(sgd=..., prepared=(wf, wd)): the fused update's reduce also writes the bf16 forward / dgrad
+    GEMM layouts of the UPDATED weight; they equal weight_prep of the new master bitwise (the forward after a
+    fused step skips weight_prep), and the master / momentum equal an unfused step."""
+    from ddpx.ops import conv as K
+    torch.manual_seed(11)
+    Cr = 3 if C == 8 else C
+    x = torch.randn(N, H, H, C, device=gpu)
+    if Cr < C:
+        x[..., Cr:] = 0
+    xn = x.to(torch.bfloat16).contiguous()
+    dy = torch.randn(N * H * H, Co, device=gpu).to(torch.bfloat16).contiguous()
+    w0 = torch.randn(Co, Cr, 3, 3, device=gpu) * 0.05
+    buf0 = torch.randn_like(w0) * 0.01
+    lr = torch.tensor(0.1, device=gpu)
+    p, buf = w0.clone(), buf0.clone()
+    wf = torch.zeros(Co * 9 * C, dtype=torch.bfloat16, device=gpu)
+    wd = torch.zeros_like(wf)
+    K.weight_prep(w0, wf, wd)  # the padded channels' zeros the update must keep
+    K.conv_wgrad(dy, xn, Co, Cr, sgd=(p, buf, None, lr, 0.9, 5e-4), prepared=(wf, wd))
+    g = torch.empty_like(w0)
+    K.conv_wgrad(dy, xn, Co, Cr, out=g)
+    buf_ref = buf0 * 0.9 + (g + 5e-4 * w0)
+    p_ref = w0 - 0.1 * buf_ref
+    wf_ref, wd_ref = torch.zeros_like(wf), torch.zeros_like(wd)
+    K.weight_prep(p, wf_ref, wd_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(wf, wf_ref) and torch.equal(wd, wd_ref)
+    assert torch.allclose(p, p_ref, rtol=1e-6, atol=1e-6) and torch.allclose(buf, buf_ref, rtol=1e-5, atol=1e-6)
