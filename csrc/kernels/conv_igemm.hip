@@ -63,7 +63,40 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   // output, each summing every TS-th slab, then a fixed-order combine (deterministic)
   int TS = 1;
   while (TS < 16 && items * TS * 2 <= 256) TS *= 2;
-  for (int j0 = 0; j0 < items; j0 += 256 / TS) {
+  if (TS == 1) {
+    // one thread per output, up to 3 outputs per thread (9 x 64 items): the loads of 8 slabs for ALL of a
+    // thread's outputs go out together (24 in flight instead of 4: the reduce was latency-bound at ~2 TB/s),
+    // then each output adds its slabs in slab order (the same sum, bit for bit, as one slab at a time)
+    constexpr int MI = (9 * CT + 255) / 256;
+    float acc[MI];
+    const float* src[MI];
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii) {
+      acc[ii] = 0.f;
+      const int j = threadIdx.x + ii * 256;
+      const int jj = j < items ? j : 0;
+      src[ii] = part + (size_t)o * 9 * Cp + (size_t)(jj / nc) * Cp + c0 + jj % nc;
+    }
+    for (int k0 = 0; k0 < S; k0 += 8) {
+      float v[MI][8];
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          v[ii][q] = (k0 + q < S && threadIdx.x + ii * 256 < items) ? src[ii][(size_t)(k0 + q) * slab] : 0.f;
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (k0 + q < S) acc[ii] += v[ii][q];
+    }
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii) {
+      const int j = threadIdx.x + ii * 256;
+      if (j < items) red[j / nc][j % nc] = acc[ii];
+    }
+  }
+  for (int j0 = 0; TS > 1 && j0 < items; j0 += 256 / TS) {
     const int j = j0 + threadIdx.x / TS, sub = threadIdx.x % TS;
     float s = 0.f;
     if (j < items && threadIdx.x / TS < 256 / TS) {
