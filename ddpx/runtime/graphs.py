@@ -218,6 +218,12 @@ class GraphedSteps:
             graphs = self.make_graphs()
         except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager steps
             ok, err = False, f"{type(e).__name__}: {e}"
+            import os
+            if os.environ.get("DDPX_DEBUG_CAPTURE") == "1":
+                import sys
+                import traceback
+                print(f"[ddpx] graph capture failed: {err}", file=sys.stderr, flush=True)
+                traceback.print_exc()
         all_ok = self.agree(ok) if self.agree is not None else ok
         if all_ok:
             self.graphs = graphs
