@@ -65,10 +65,13 @@ def parse(argv=None):
                    help="1: MX-FP8 hidden-layer forward / weight-gradient GEMMs (MLP models; default 0)")
     p.add_argument("--torch_amp", action="store_true", help="--impl torch: bf16 autocast (+channels_last for VGG)")
     p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
-                   help="compute precision of the ddpx engine on the GPU: bf16 (default) or fp32, the reference's "
-                        "recipe on the exact-f32 MFMA kernels (the stock reference then runs without autocast)")
+                   help="compute precision of the ddpx engine on the GPU: bf16 (default here: BASELINE.json's headline "
+                        "config is the bf16 toy MLP) or fp32, the reference's recipe on the exact-f32 MFMA kernels (the "
+                        "stock reference then runs without autocast; singlegpu.py / multigpu.py default to fp32 like "
+                        "the reference)")
     p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
-                   help="ddpx engine ops: auto = hand-written kernels except VGG at fp32 (MIOpen convolutions)")
+                   help="ddpx engine ops: auto / native = the hand-written HIP kernels for every model and precision; "
+                        "torch = torch ops (MIOpen / hipBLASLt) under the ddpx engine")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--prefetch_batch", type=int, default=0,
                    help="1 (N = 1, graphs): step k's kernels read a batch augmented during step k-1 on a side stream "
@@ -693,9 +696,8 @@ def main(argv=None):
     from ddpx.models import native_kernels_for
     if args.impl == "ddpx" and not native_kernels_for(args.model, "fp32" if args.dtype == "fp32" else "bf16",
                                                       args.kernels):
-        # torch ops under the ddpx engine (VGG at fp32: MIOpen convolutions) run eagerly: capturing torch's
-        # autograd with AccumulateGrad nodes made by the eager warm-up steps crashed the process (exit -11);
-        # a ~20 ms step does not need the graph's launch savings
+        # torch ops under the ddpx engine (--kernels torch: MIOpen / hipBLASLt) run eagerly: capturing torch's
+        # autograd with AccumulateGrad nodes made by the eager warm-up steps crashed the process (exit -11)
         args.no_graph = True
     device = torch.device("cpu") if cpu else torch.device("cuda", local)
     loader = make_data(args, device, rank, world)
@@ -711,6 +713,9 @@ def main(argv=None):
     comm = make_comm(args, device, world)
     if getattr(args, "calibrate", False):
         calibrate_plan(args, device, world, loader, idx_all, full, comm)
+    if not cpu:
+        from ddpx.runtime.graphs import assert_no_capture
+        assert_no_capture("before building the timed engine")
     eng = make_runner(args, device, world, loader, idx_all, full, comm)
     model, net, opt, sched, run, runner = eng.model, eng.net, eng.opt, eng.sched, eng.run, eng.runner
 

@@ -219,7 +219,14 @@ __device__ __forceinline__ void im_rows_init(ImRows<ROWS, NW>& ir, const ConvGeo
 
 template <int ROWS, int MODE, int NW>
 __device__ __forceinline__ void stage_tile_im(__amdgpu_buffer_rsrc_t rs, char* slot, const ConvGeom& g,
-                                              const ImRows<ROWS, NW>& ir, int k0, int wave) {
+                                              const ImRows<ROWS, NW>& ir, int k0, int kend, int wave) {
+  // K tail (k0 >= K = 9*C): zero fill like src_off's tap >= 9 (a wave-uniform scalar test); without it a
+  // tap index of 9 would load real shifted pixels, and 0 * Inf in the product would turn into NaN
+  if (k0 >= kend) {
+#pragma unroll
+    for (int j = 0; j < ImRows<ROWS, NW>::NI; ++j) dma16(rs, slot + (j * NW + wave) * 1024, kOOB);
+    return;
+  }
   // wave-uniform per K-step: tap, channel base, pixel shift
   const int tap = fdiv(k0, g.dC), c0 = k0 - tap * g.C;
   const int ky = (tap * 11) >> 5, kx = tap - ky * 3;
@@ -616,7 +623,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     for (int u = 0; u < KSUB; ++u) {
       const int k0 = kbeg + t * BK + u * 64;
       if constexpr (A_IM) {
-        if (a_fast) stage_tile_im<BM, AMODE, NW>(ra, slot + u * A_SUB, p.conv, arow, k0, wave);
+        if (a_fast) stage_tile_im<BM, AMODE, NW>(ra, slot + u * A_SUB, p.conv, arow, k0, kend, wave);
         else stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);
       } else {
         stage_tile<BM, AK, AMODE, NW>(ra, slot + u * A_SUB, p.conv, p.lda, m0, p.M, k0, kend, wave, lane);

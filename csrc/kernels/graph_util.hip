@@ -10,3 +10,33 @@ DDPX_API int ddpx_graph_upload(void* exec, hipStream_t s) {
   if (!exec) return -1;
   return (int)hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), s);
 }
+
+// Capture bookkeeping for ddpx.runtime.graphs.capture_step (profiles/r5_capture/NOTES.md): the capture status
+// of ANY stream (torch only answers for the current one) and a hard end of a capture that torch's capture_end
+// could not end.  On ROCm 7 an unjoined capture (a forked side stream not joined back) makes
+// hipStreamEndCapture fail while BOTH streams stay "active", and a stream whose capture was invalidated keeps
+// reporting "invalidated" afterwards: every later synchronous copy on it fails (torch's memcpy_and_sync
+// requires the status "none").
+// status: 0 none, 1 active, 2 invalidated; id: the capture's id (0 when none).
+DDPX_API int ddpx_stream_capture_info(hipStream_t s, int* status, unsigned long long* id) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  hipError_t e = hipStreamGetCaptureInfo(s, &st, &cid);
+  *status = (int)st;
+  *id = st == hipStreamCaptureStatusNone ? 0 : cid;
+  return (int)e;
+}
+
+// End the capture running on `s` (from the thread that began it) and destroy whatever graph it produced.
+// Returns the hipStreamEndCapture code (the capture is over either way unless the code is a wrong-thread /
+// unmatched error).
+DDPX_API int ddpx_stream_end_capture_discard(hipStream_t s) {
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(s, &g);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  (void)hipStreamGetCaptureInfo(s, &st, nullptr);
+  // an unjoined end hands back the graph while the capture stays active (it still owns it): keep it then
+  if (g && st != hipStreamCaptureStatusActive) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();  // do not leave the code behind for torch's next launch check
+  return (int)e;
+}

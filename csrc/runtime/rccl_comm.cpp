@@ -62,6 +62,8 @@ struct Comm {
   std::atomic<bool> aborted{false};
   int rank = 0, nranks = 1, device = 0;
   hipStream_t stream = nullptr;  // dedicated comm stream (high priority)
+  int priority = 0;
+  std::vector<hipStream_t> retired;  // streams a failed HIP-graph capture left unusable (ddpx_comm_renew_stream)
   // watchdog
   std::mutex mu;  // guards pending / free_events
   std::deque<Pending> pending;
@@ -265,7 +267,8 @@ DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int devic
   c->device = device;
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
-  he = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high_priority ? hi : lo);
+  c->priority = high_priority ? hi : lo;
+  he = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->priority);
   if (he != hipSuccess) {
     *err = (int)he;
     delete c;
@@ -310,6 +313,22 @@ DDPX_API int ddpx_comm_set_timeout(void* h, double timeout_s, int action) {
 }
 
 DDPX_API void* ddpx_comm_stream(void* h) { return static_cast<Comm*>(h)->stream; }
+
+// Replace the comm stream by a fresh one (same priority).  A HIP-graph capture that failed after forking onto
+// the comm stream can leave it in the capture status "invalidated" on ROCm 7, and RCCL refuses to enqueue on such
+// a stream (profiles/r5_capture/NOTES.md).  RCCL communicators are not bound to a stream, so swapping it is safe
+// once the caller synchronised the device; the old stream is kept (never destroyed while it may still be
+// referenced by a graph) and released at destroy.
+DDPX_API int ddpx_comm_renew_stream(void* h) {
+  Comm* c = static_cast<Comm*>(h);
+  std::lock_guard<std::mutex> g(c->issue_mu);
+  hipStream_t s = nullptr;
+  hipError_t he = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, c->priority);
+  if (he != hipSuccess) return (int)he;
+  c->retired.push_back(c->stream);
+  c->stream = s;
+  return 0;
+}
 DDPX_API int ddpx_comm_error(void* h) { return static_cast<Comm*>(h)->error.load(); }
 
 DDPX_API int ddpx_comm_destroy(void* h, int abort) {
@@ -333,6 +352,7 @@ DDPX_API int ddpx_comm_destroy(void* h, int abort) {
   for (auto& p : c->pending) hipEventDestroy(p.ev);
   for (auto ev : c->free_events) hipEventDestroy(ev);
   hipStreamDestroy(c->stream);
+  for (auto s : c->retired) (void)hipStreamDestroy(s);
   delete c;
   return e;
 }

@@ -33,8 +33,8 @@ def build_argv(argv):
     rest = argv[i:]
     joined = " ".join(opts)
     if "--nproc-per-node" not in joined and "--nproc_per_node" not in joined:
-        import torch
-        n = torch.cuda.device_count() or 1
+        from .utils.devices import visible_gpu_count
+        n = visible_gpu_count() or 1
         opts = ["--nproc-per-node", str(n)] + opts
     if "--nnodes" not in joined:
         opts = ["--nnodes", "1"] + opts

@@ -17,8 +17,11 @@ import torch
 
 def eligible(model, x) -> bool:
     w = model.fc0.weight
+    flat = getattr(w, "_ddpx_flat", None)
+    # the backward writes fp32 GEMM results straight into the flat gradient buffer (``out=``): a bf16 gradient
+    # buffer (--grad_dtype bf16) takes the generic autograd path, which casts on accumulation
     return (not x.is_cuda and torch.is_grad_enabled() and not x.requires_grad and w.dtype == torch.float32
-            and getattr(w, "_ddpx_flat", None) is not None)
+            and flat is not None and flat.grad is not None and flat.grad.dtype == torch.float32)
 
 
 class _MLPCPU(torch.autograd.Function):

@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from ..runtime.flat_params import ALIGN
+from ..runtime.graphs import assert_no_capture
 from .ddp import plan_buckets
 
 _CANDIDATE_CAPS = [(1.0, 25.0), (1.0, 8.0), (4.0, 16.0), (16.0, 64.0)]
@@ -152,6 +153,9 @@ def calibrate_by_step(plans, make_trial, sync=lambda: None, warm=3, reps=5, roun
             local.append(time_trial(step, sync, warm=warm, reps=reps, rounds=rounds))
         finally:
             close()
+        # a trial's graph capture must leave no stream capturing: the next trial (or the timed engine) would
+        # otherwise have its work recorded instead of run (profiles/r5_capture/NOTES.md)
+        assert_no_capture(f"after calibration trial {p.get('name', '?')}")
     if not plans:
         raise ValueError("calibrate_by_step: no candidate plans")
     ms = _max_over_ranks(local)

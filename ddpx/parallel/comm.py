@@ -221,6 +221,16 @@ class RcclComm(Comm):
             raise RuntimeError(f"ncclCommInitRank failed (code {err.value})")
         self._rt = rt
         self.stream = torch.cuda.ExternalStream(rt.ddpx_comm_stream(self.handle), device=self.device)
+        # captured steps fork onto this stream: a failed capture joins it back / renews it, and the capture-leak
+        # check covers it (ddpx.runtime.graphs)
+        from ..runtime.graphs import register_side_stream
+        self._side_name = f"RCCL comm stream #{id(self)}"
+        register_side_stream(self, self._side_name, renew=RcclComm.renew_stream, attr="stream")
+
+    def renew_stream(self):
+        """Swap in a fresh communicator stream (the old one was left unusable by a failed capture)."""
+        native.check(self._rt.ddpx_comm_renew_stream(self.handle), "ddpx_comm_renew_stream")
+        self.stream = torch.cuda.ExternalStream(self._rt.ddpx_comm_stream(self.handle), device=self.device)
 
     def _s(self, stream):
         return native.stream_handle(stream) if stream is not None else native.stream_handle()
@@ -283,6 +293,8 @@ class RcclComm(Comm):
 
     def close(self, abort=False):
         if getattr(self, "handle", None):
+            from ..runtime.graphs import unregister_side_stream
+            unregister_side_stream(self._side_name)
             self._rt.ddpx_comm_destroy(self.handle, int(abort))
             self.handle = None
 

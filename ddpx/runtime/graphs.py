@@ -15,10 +15,198 @@ Rules this relies on (all ddpx ops follow them):
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 
 _UPLOAD_SIG = False
+_CAPTURE_SIG = False
+
+
+class CaptureLeak(RuntimeError):
+    """A stream is still capturing (or stuck "invalidated") after a capture ended: any later synchronous copy
+    on it would fail with hipErrorStreamCaptureUnsupported, and kernels issued on it would be recorded instead
+    of executed.  Raised instead of continuing silently (profiles/r5_capture/NOTES.md)."""
+
+
+# ---------------------------------------------------------------- capture status of arbitrary streams
+_STATUS = {0: "none", 1: "active", 2: "invalidated"}
+
+
+def _capture_native():
+    global _CAPTURE_SIG
+    from . import native
+    if not _CAPTURE_SIG:
+        native.register_kernel_sig("ddpx_stream_capture_info", native.c_int, native.c_void_p,
+                                   native.ctypes.POINTER(native.c_int), native.ctypes.POINTER(native.c_uint64))
+        native.register_kernel_sig("ddpx_stream_end_capture_discard", native.c_int, native.c_void_p)
+        _CAPTURE_SIG = True
+    return native
+
+
+def stream_capture_info(stream) -> tuple[str, int]:
+    """(status, capture id) of ``stream`` (a torch stream): status none / active / invalidated."""
+    native = _capture_native()
+    st, cid = native.c_int(0), native.c_uint64(0)
+    rc = native.kernels().ddpx_stream_capture_info(stream.cuda_stream, native.ctypes.byref(st),
+                                                    native.ctypes.byref(cid))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamGetCaptureInfo failed with code {rc}")
+    return _STATUS.get(st.value, str(st.value)), int(cid.value)
+
+
+def stream_capture_status(stream) -> str:
+    return stream_capture_info(stream)[0]
+
+
+# Side streams a captured step may fork onto (the RCCL communicator's stream, a prefetch stream): the capture
+# joins them back if a failure left them forked, and the leak check covers them.  name -> (getter, renew):
+# getter() returns the stream now (None once its owner is gone); renew() replaces a stream that a failed capture
+# left unusable, or is None.
+_SIDE: dict = {}
+
+
+def register_side_stream(stream_or_owner, name: str, renew=None, attr: str | None = None):
+    """Register a side stream by object, or by (owner, attribute) so a renewed stream is followed; the owner
+    is held weakly."""
+    if attr is None:
+        s = stream_or_owner
+        _SIDE[name] = (lambda: s, renew)
+    else:
+        ref = weakref.ref(stream_or_owner)
+
+        def get():
+            o = ref()
+            return getattr(o, attr, None) if o is not None else None
+
+        def ren():
+            o = ref()
+            if o is not None and renew is not None:
+                renew(o)
+        _SIDE[name] = (get, ren if renew is not None else None)
+
+
+def unregister_side_stream(name: str):
+    _SIDE.pop(name, None)
+
+
+def _side_streams():
+    out = []
+    for name, (get, renew) in list(_SIDE.items()):
+        s = get()
+        if s is None:
+            _SIDE.pop(name, None)
+            continue
+        out.append((name, s, renew))
+    return out
+
+
+_CAP_STREAM = None
+
+
+def _capture_stream():
+    global _CAP_STREAM
+    if _CAP_STREAM is None:
+        _CAP_STREAM = torch.cuda.Stream()
+    return _CAP_STREAM
+
+
+def _join_into(cap, cid):
+    """Join every registered side stream that is part of capture ``cid`` back into ``cap`` (what the body did
+    not get to, e.g. because it raised between a fork and its join)."""
+    joined = []
+    for name, s, _ in _side_streams():
+        if s == cap:
+            continue
+        st, sid = stream_capture_info(s)
+        if st == "active" and sid == cid:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            cap.wait_event(ev)
+            joined.append(name)
+    return joined
+
+
+def _abort_capture(graph, cap):
+    """End a capture whose body or end failed, leaving no stream capturing; retire streams it left unusable."""
+    global _CAP_STREAM
+    native = _capture_native()
+    st, cid = stream_capture_info(cap)
+    ended = False
+    if st == "active":
+        _join_into(cap, cid)
+        try:
+            graph.capture_end()  # also ends torch's allocation routing into the graph's private pool
+            ended = True
+        except Exception:  # noqa: BLE001 - invalidated: ended below
+            pass
+    if not ended:
+        try:  # capture_end raised before it stopped routing this stream's allocations into the graph's pool
+            torch._C._cuda_endAllocateToPool(cap.device.index, graph.pool())
+        except Exception:  # noqa: BLE001
+            pass
+        if stream_capture_status(cap) != "none":
+            native.kernels().ddpx_stream_end_capture_discard(cap.cuda_stream)
+    try:
+        graph.reset()
+    except Exception:  # noqa: BLE001
+        pass
+    if stream_capture_status(cap) != "none":
+        _CAP_STREAM = None  # never capture on it again: the next capture gets a fresh stream
+    for name, s, renew in _side_streams():
+        if stream_capture_status(s) != "none" and renew is not None:
+            torch.cuda.synchronize()
+            renew()
+
+
+def capture_step(graph, fn):
+    """Capture ``fn()`` into ``graph`` (thread-local mode) and return its result; the replacement of
+    ``with torch.cuda.graph(graph)`` for every captured training step.
+
+    torch's context manager does not end a capture cleanly on failure: when ``capture_end`` raises (an unjoined
+    side stream, an invalidated capture) it skips restoring the current stream, so the thread keeps issuing work
+    to a stream that is still capturing (ROCm 7 leaves an unjoined capture active on both streams), and an
+    "eager" fallback step is silently recorded instead of run, until the next synchronous copy fails with
+    hipErrorStreamCaptureUnsupported (profiles/r4_flaky, profiles/r5_capture/NOTES.md).  Here, on any
+    failure: forked side streams are joined back, the capture is ended and discarded, streams left unusable are
+    retired / renewed, the current stream is always restored, and the failure is re-raised."""
+    cap = _capture_stream()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    with torch.cuda.stream(cap):
+        graph.capture_begin(capture_error_mode="thread_local")
+        try:
+            out = fn()
+        except BaseException:
+            _abort_capture(graph, cap)
+            raise
+        try:
+            graph.capture_end()
+        except BaseException:
+            _abort_capture(graph, cap)
+            raise
+    return out
+
+
+def assert_no_capture(where: str, extra=()):
+    """Raise :class:`CaptureLeak` if the current stream, the capture stream or any registered side stream is
+    not in the capture status "none" (call between calibration trials, before building a timed engine, and
+    after a capture fallback)."""
+    if not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    streams = [("current stream", torch.cuda.current_stream(), None)]
+    if _CAP_STREAM is not None:
+        streams.append(("capture stream", _CAP_STREAM, None))
+    streams += _side_streams()
+    streams += [(n, s, None) for n, s in extra]
+    bad = []
+    for name, s, _ in streams:
+        st = stream_capture_status(s)
+        if st != "none":
+            bad.append(f"{name} (0x{s.cuda_stream:x}) is {st}")
+    if bad:
+        raise CaptureLeak(f"{where}: " + "; ".join(bad))
 
 
 def _upload(graph):
@@ -71,8 +259,7 @@ class CapturedStep:
         self.graph = torch.cuda.CUDAGraph()
         if pre_replay is not None:
             pre_replay()
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.static_loss = self.fn(self.static_x, self.static_y)
+        self.static_loss = capture_step(self.graph, lambda: self.fn(self.static_x, self.static_y))
         _upload(self.graph)
         torch.cuda.synchronize()
 
@@ -106,10 +293,17 @@ class CapturedCycle:
         sig0 = signature() if signature is not None else None
         first = CapturedStep(fn, example_x, example_y, use_inputs_as_static=use_inputs_as_static, comm=comm)
         self.graphs = [first]
+        # host-visible state after each version (its capture advanced the host bookkeeping exactly as a replay
+        # advances the device): every replay puts the host back in step with the device, so an eager step after
+        # an odd number of replays reads the bf16 copy the last replay wrote
+        self.post = [signature() if signature is not None else None]
         while signature is not None and signature() != sig0:
             if len(self.graphs) >= max_period:
                 raise RuntimeError(f"training-step state does not return to its start within {max_period} steps")
             self.graphs.append(CapturedStep(fn, first.static_x, first.static_y, use_inputs_as_static=True, comm=comm))
+            self.post.append(signature())
+        owner = getattr(signature, "__self__", None)
+        self._set_sig = getattr(owner, "set_pingpong_signature", None) if len(self.graphs) > 1 else None
         self.static_x, self.static_y = first.static_x, first.static_y
         self.k = 0
 
@@ -123,9 +317,12 @@ class CapturedCycle:
     def __call__(self, x=None, y=None):
         if x is not None:
             self.load(x, y)
-        g = self.graphs[self.k % len(self.graphs)]
+        i = self.k % len(self.graphs)
         self.k += 1
-        return g()
+        out = self.graphs[i]()
+        if self._set_sig is not None:
+            self._set_sig(self.post[i])
+        return out
 
 
 def pingpong_signature_of(opt):
@@ -182,6 +379,7 @@ def try_capture(fn, x, y, net, opt, comm=None, agree=agree_all_ranks):
     if agree(g is not None):
         return g, None
     restore_after_failed_capture(net, opt, snap)
+    assert_no_capture("after a failed step capture")
     return None, err or "graph capture failed on another rank"
 
 
@@ -233,6 +431,8 @@ class GraphedSteps:
         self.graph_error = err or "graph capture failed on another rank"
         if self.on_fallback is not None:
             self.on_fallback()
+        # the eager steps that follow must run, not be recorded into a capture the failure left open
+        assert_no_capture("after a failed step capture")
 
     def run(self, k: int, n: int):
         """Steps k .. k+n-1; returns the last step's loss."""

@@ -55,7 +55,9 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                         "trains without autocast) or bf16 (MFMA bf16 with fp32 master weights; auto = bf16 on a GPU)")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     p.add_argument("--kernels", default="auto", choices=["auto", "native", "torch"],
-                   help="auto: hand-written kernels, except VGG at fp32 (MIOpen convolutions are faster there)")
+                   help="auto / native: the hand-written HIP kernels for every model and precision (measured faster "
+                        "than MIOpen / hipBLASLt, profiles/r4_f32); torch: torch ops (MIOpen / hipBLASLt) under the "
+                        "ddpx engine (flat store, fused SGD, native DDP)")
     p.add_argument("--bucket_cap_mb", type=float, default=None,
                    help="DDP bucket cap (default: calibrated on the node at start-up, see --bucket_plan)")
     p.add_argument("--first_bucket_mb", type=float, default=None)
@@ -228,7 +230,7 @@ def build_model_and_optimizer(args, device, distributed: bool = False, comm=None
                 model.use_native = False  # fp32 SyncBatchNorm: torch-op BatchNorm on the merged statistics
             model = convert_sync_batchnorm(model, comm)
     if args.graph and device.type == "cuda" and not getattr(model, "use_native", True):
-        # torch-op models (e.g. VGG at fp32 on MIOpen convolutions) step eagerly: capturing torch's autograd with
+        # torch-op models (--kernels torch: MIOpen / hipBLASLt ops) step eagerly: capturing torch's autograd with
         # AccumulateGrad nodes created by the eager warm-up steps is not supported (it crashed in bench.py)
         if getattr(args, "graph_explicit", True):
             print("note: --graph ignored for the torch-op model path", flush=True)

@@ -47,9 +47,14 @@ if __name__ == "__main__":
         if args.nprocs:
             world_size = args.nprocs
         else:
-            # device_count() does not initialise HIP in this process: the spawned children are
-            # forked+exec'd, which must not happen from a process that touched the GPU
-            n = 0 if args.device == "cpu" else torch.cuda.device_count()
+            # the reference's world_size = torch.cuda.device_count() (multigpu.py:262), counted without
+            # initialising HIP here (environment / KFD topology, ddpx.utils.devices): the ranks are fork+exec'd,
+            # which must not happen from a process that touched the GPU
+            from ddpx.utils.devices import visible_gpu_count
+            n = 0 if args.device == "cpu" else visible_gpu_count()
             world_size = n if n > 0 else 2
+        if args.device != "cpu":
+            from ddpx.utils.devices import assert_hip_uninitialised
+            assert_hip_uninitialised("multigpu.py: mp.spawn")
         mp.spawn(main, args=(world_size, args.save_every, args.total_epochs, args.batch_size, args),
                  nprocs=world_size)

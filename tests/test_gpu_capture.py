@@ -1,0 +1,144 @@
+"""A failed HIP-graph capture must leave no stream capturing (profiles/r5_capture/NOTES.md).
+
+Round 4 saw ``bench.py --ddp_single --shard_optimizer 1`` die in the timed model's ``model.to(device)`` with
+hipErrorStreamCaptureUnsupported right after the graph-captured calibration trials (profiles/r4_flaky): torch's
+``torch.cuda.graph`` skips restoring the current stream when ``capture_end`` raises, and ROCm 7 leaves an
+unjoined capture active, so the thread kept issuing "eager" work into a dead capture.  These tests drive the
+failure paths deterministically through :func:`ddpx.runtime.graphs.capture_step` and the bench engine
+(ZeRO-1 + comm-side optimizer + deferred gathers + optimizer overlap, on the real RCCL communicator), then do an
+H2D copy right away.
+"""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests._dist_util import free_port
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pg(gpu):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+def _h2d_works(dev):
+    t = torch.arange(16, dtype=torch.float32).to(dev)  # memcpy_and_sync: checks the current stream's capture status
+    torch.cuda.synchronize()
+    return float(t.sum()) == 120.0
+
+
+@pytest.mark.parametrize("mode", ["raise_after_fork", "unjoined", "invalidated"])
+def test_failed_capture_leaves_no_stream_capturing(gpu, mode):
+    from ddpx.runtime.graphs import (CaptureLeak, assert_no_capture, capture_step, register_side_stream,
+                                     stream_capture_status, unregister_side_stream)
+    default = torch.cuda.current_stream()
+    side = torch.cuda.Stream(gpu)
+    register_side_stream(side, "test side stream")
+    x = torch.zeros(4096, device=gpu)
+    y = torch.zeros(4, device=gpu)
+    torch.cuda.synchronize()
+
+    def body():
+        x.add_(1)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            x.mul_(2)
+        if mode == "raise_after_fork":
+            raise RuntimeError("injected failure between a fork and its join")
+        if mode == "invalidated":  # an unsafe call on the capturing thread (torch raises, HIP invalidates)
+            with torch.cuda.stream(torch.cuda.Stream(gpu)):
+                y.copy_(torch.ones(4), non_blocking=False)
+        if mode != "unjoined":
+            torch.cuda.current_stream().wait_stream(side)
+
+    g = torch.cuda.CUDAGraph()
+    try:
+        with pytest.raises(Exception) as ei:
+            capture_step(g, body)
+        assert not isinstance(ei.value, CaptureLeak), ei.value
+        assert torch.cuda.current_stream() == default
+        assert stream_capture_status(default) == "none"
+        assert stream_capture_status(side) == "none"
+        assert_no_capture(f"after a {mode} capture")
+        assert _h2d_works(gpu)
+        # eager work runs again (a leaked capture would record it instead)
+        x.zero_()
+        x.add_(3)
+        torch.cuda.synchronize()
+        assert float(x[0]) == 3.0
+        # and the next capture works
+        g2 = torch.cuda.CUDAGraph()
+        capture_step(g2, lambda: x.add_(1))
+        g2.replay()
+        torch.cuda.synchronize()
+        assert float(x[0]) == 4.0
+    finally:
+        unregister_side_stream("test side stream")
+
+
+def _bench_engine(gpu, inject, monkeypatch):
+    import bench
+    from ddpx.parallel.ddp import DistributedDataParallel
+    args = bench.parse(["--gpus", "1", "--ddp_single", "--shard_optimizer", "1", "--bucket_plan", "default",
+                        "--steps", "6", "--warmup", "0", "--train_size", "4096", "--graph_steps", "1"])
+    bench.resolve_defaults(args, 1)
+    # the round-4 failing configuration
+    assert args.shard_optimizer and args.comm_side_optimizer and args.defer_gather and args.overlap_optimizer
+    loader = bench.make_data(args, gpu, 0, 1)
+    idx_all = loader._epoch_indices()
+    full = [i for i in range(len(loader)) if (i + 1) * args.batch_size <= idx_all.numel()]
+    comm = bench.make_comm(args, gpu, 1)
+    hits = {"n": 0}
+    if inject:
+        orig = DistributedDataParallel.gather_bucket
+
+        def failing_gather(self, b):
+            # inside the optimizer's comm-stream block of the CAPTURED step: the comm stream is forked, its join
+            # not yet recorded, the reduce-scatters / shard updates already captured
+            if torch.cuda.is_current_stream_capturing():
+                hits["n"] += 1
+                raise RuntimeError("injected mid-capture failure (ZeRO-1 comm-side gather)")
+            return orig(self, b)
+        monkeypatch.setattr(DistributedDataParallel, "gather_bucket", failing_gather)
+    eng = bench.make_runner(args, gpu, 1, loader, idx_all, full, comm)
+    return eng, comm, hits
+
+
+@pytest.mark.parametrize("inject", [False, True])
+def test_zero1_comm_side_defer_trial_teardown_then_h2d(gpu, pg, inject, monkeypatch):
+    from ddpx.models import build_model
+    from ddpx.runtime.flat_params import flat_of
+    from ddpx.runtime.graphs import assert_no_capture
+    from ddpx.runtime.setup import prepare_model
+    eng, comm, hits = _bench_engine(gpu, inject, monkeypatch)
+    try:
+        eng.run(0, 3)  # two eager steps, then the capture (+ one replay, or the eager fallback)
+        torch.cuda.synchronize()
+        if inject:
+            assert hits["n"] == 1
+            assert not eng.runner.use_graph and "injected" in eng.runner.graph_error
+        else:
+            assert eng.runner.use_graph and eng.runner.graph_error is None
+        # the steps after the capture really run: the fp32 master weights move
+        f = flat_of(eng.model)
+        before = f.master.clone()
+        eng.run(3, 2)
+        torch.cuda.synchronize()
+        assert not torch.equal(before, f.master)
+        assert torch.isfinite(f.master).all()
+    finally:
+        eng.close()
+        torch.cuda.synchronize()
+    assert_no_capture("after the trial's teardown")
+    # what the timed engine does next: build a model on the host and copy it to the device
+    m = build_model("mlp", hidden=512, device=gpu)
+    prepare_model(m, gpu)
+    assert _h2d_works(gpu)
+    comm.close()

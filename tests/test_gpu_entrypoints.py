@@ -147,3 +147,20 @@ def test_multigpu_reference_command_fp32_native_calibrated(gpu, tmp_path):
     assert "bucket plan: calibrated" in out, out
     sd = torch.load(tmp_path / "checkpoint.pt", weights_only=True)
     assert all(v.dtype in (torch.float32, torch.int64) for v in sd.values())
+
+
+def test_multigpu_reference_launch_without_nprocs(gpu, tmp_path):
+    """``python multigpu.py E S`` exactly as the reference launches it (no --nprocs: world size = the node's GPU
+    count, /root/reference/multigpu.py:262-263), counted without initialising HIP in the launcher
+    (ddpx.utils.devices), which then mp.spawns the ranks."""
+    from ddpx.utils.devices import visible_gpu_count
+    n = visible_gpu_count()
+    assert n == torch.cuda.device_count(), (n, torch.cuda.device_count())
+    if n != 1:
+        pytest.skip("the one-rank launch check needs a one-GPU box")
+    out = _run([os.path.join(ROOT, "multigpu.py"), "1", "1", "--data", "synthetic", "--train_size", "2048",
+                "--test_size", "512"], tmp_path, extra_env={"MASTER_ADDR": "127.0.0.1",
+                                                              "MASTER_PORT": str(free_port())})
+    assert "[GPU0] Epoch 0 | Batchsize: 512 | Steps: 4" in out
+    assert "fp32 model has accuracy=" in out
+    assert "[GPU1]" not in out

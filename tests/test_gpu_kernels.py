@@ -522,7 +522,10 @@ def _fused_dgrad_step(gpu, graph, ddpx, MLP, SGD, CapturedCycle, pingpong_signat
     if graph:
         g = CapturedCycle(body, xs[1], ts[1], signature=pingpong_signature_of(oa))
         assert g.period == 2
-        la += [g(xs[i], ts[i]).item() for i in range(1, 5)]
+        # an ODD number of replays, then an eager step: the host's ping-pong parity must follow the replays
+        # (the eager step reads the bf16 copy the last replay wrote)
+        la += [g(xs[i], ts[i]).item() for i in range(1, 4)]
+        la.append(body(xs[4], ts[4]).item())
     else:
         la += [body(xs[i], ts[i]).item() for i in range(1, 5)]
     lb = []
