@@ -5,6 +5,8 @@
 // uploaded right after capture, so their first replay costs what every later replay costs.
 #include "ddpx_common.h"
 
+#include <thread>
+
 // exec: the hipGraphExec_t of a captured graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()).
 DDPX_API int ddpx_graph_upload(void* exec, hipStream_t s) {
   if (!exec) return -1;
@@ -33,10 +35,41 @@ DDPX_API int ddpx_stream_capture_info(hipStream_t s, int* status, unsigned long 
 DDPX_API int ddpx_stream_end_capture_discard(hipStream_t s) {
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(s, &g);
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  (void)hipStreamGetCaptureInfo(s, &st, nullptr);
-  // an unjoined end hands back the graph while the capture stays active (it still owns it): keep it then
-  if (g && st != hipStreamCaptureStatusActive) (void)hipGraphDestroy(g);
+  // an unjoined end hands back the graph while the capture stays active (it still owns it): only a clean end
+  // transfers it
+  if (g && e == hipSuccess) (void)hipGraphDestroy(g);
   (void)hipGetLastError();  // do not leave the code behind for torch's next launch check
   return (int)e;
+}
+
+static hipStreamCaptureStatus capture_status(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  (void)hipStreamGetCaptureInfo(s, &st, nullptr);
+  return st;
+}
+
+static void end_and_drop(hipStream_t s) {
+  hipGraph_t g = nullptr;
+  // only a clean end hands over the graph: after an unmatched / unjoined end it may still belong to the origin
+  if (hipStreamEndCapture(s, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+}
+
+// Bring a stream that a failed capture left behind back to the capture status "none" (measured on ROCm 7,
+// benchmarks/capture_probe.hip): a side stream still "active" after its origin's capture ended is ended on its
+// own (hipErrorStreamCaptureUnmatched, after which it reads "invalidated"); an "invalidated" stream returns to
+// "none" after one empty capture.  An origin stream whose unjoined end failed refuses a second end on its own
+// thread (hipErrorStreamCaptureWrongThread); that end is retried from a helper thread.  Returns the final status.
+DDPX_API int ddpx_stream_force_reset(hipStream_t s) {
+  if (capture_status(s) == hipStreamCaptureStatusActive) {
+    end_and_drop(s);
+    if (capture_status(s) == hipStreamCaptureStatusActive) {
+      std::thread t([s] { end_and_drop(s); });
+      t.join();
+    }
+  }
+  if (capture_status(s) == hipStreamCaptureStatusInvalidated) {
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) end_and_drop(s);
+  }
+  (void)hipGetLastError();
+  return (int)capture_status(s);
 }

@@ -41,6 +41,7 @@ def _capture_native():
         native.register_kernel_sig("ddpx_stream_capture_info", native.c_int, native.c_void_p,
                                    native.ctypes.POINTER(native.c_int), native.ctypes.POINTER(native.c_uint64))
         native.register_kernel_sig("ddpx_stream_end_capture_discard", native.c_int, native.c_void_p)
+        native.register_kernel_sig("ddpx_stream_force_reset", native.c_int, native.c_void_p)
         _CAPTURE_SIG = True
     return native
 
@@ -153,8 +154,14 @@ def _abort_capture(graph, cap):
     except Exception:  # noqa: BLE001
         pass
     if stream_capture_status(cap) != "none":
-        _CAP_STREAM = None  # never capture on it again: the next capture gets a fresh stream
+        native.kernels().ddpx_stream_force_reset(cap.cuda_stream)
+        if stream_capture_status(cap) != "none":
+            _CAP_STREAM = None  # never capture on it again: the next capture gets a fresh stream
     for name, s, renew in _side_streams():
+        # a side stream of an invalidated capture stays "active" after the origin's end; one of an aborted
+        # capture may read "invalidated": both are brought back to "none", or the stream is replaced
+        if stream_capture_status(s) != "none":
+            native.kernels().ddpx_stream_force_reset(s.cuda_stream)
         if stream_capture_status(s) != "none" and renew is not None:
             torch.cuda.synchronize()
             renew()
@@ -182,11 +189,26 @@ def capture_step(graph, fn):
             _abort_capture(graph, cap)
             raise
         try:
+            # a side stream the body forked and never joined back would make the end fail AND leave both
+            # streams capturing for good (ROCm 7: a second end is refused, WrongThread): join it first
+            late = _join_into(cap, stream_capture_info(cap)[1])
+            if late:
+                _warn_once(f"capture_step: joined side stream(s) the captured body left forked: {late}")
             graph.capture_end()
         except BaseException:
             _abort_capture(graph, cap)
             raise
     return out
+
+
+_WARNED = set()
+
+
+def _warn_once(msg):
+    if msg not in _WARNED:
+        _WARNED.add(msg)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def assert_no_capture(where: str, extra=()):

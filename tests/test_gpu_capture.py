@@ -60,9 +60,17 @@ def test_failed_capture_leaves_no_stream_capturing(gpu, mode):
 
     g = torch.cuda.CUDAGraph()
     try:
-        with pytest.raises(Exception) as ei:
-            capture_step(g, body)
-        assert not isinstance(ei.value, CaptureLeak), ei.value
+        if mode == "unjoined":  # joined back before the end (a failed unjoined end cannot be repaired on ROCm 7)
+            with pytest.warns(RuntimeWarning, match="left forked"):
+                capture_step(g, body)
+            g.replay()
+            torch.cuda.synchronize()
+            assert float(x[0]) == 2.0
+            g.reset()
+        else:
+            with pytest.raises(Exception) as ei:
+                capture_step(g, body)
+            assert not isinstance(ei.value, CaptureLeak), ei.value
         assert torch.cuda.current_stream() == default
         assert stream_capture_status(default) == "none"
         assert stream_capture_status(side) == "none"
