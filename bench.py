@@ -437,6 +437,8 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
             # buffer from its own device cursor (batch index = augments issued so far)
             bufs = [(static_x, static_y), (torch.empty_like(static_x), torch.empty_like(static_y))]
             side = torch.cuda.Stream(device)
+            from ddpx.runtime.graphs import register_side_stream
+            register_side_stream(side, f"prefetch stream #{id(side)}")  # joined back / reset by a failed capture
             data_ctr = counter.clone()
             loader.cursor_batch(idx_dev, nfull, *bufs[0], counter=data_ctr)  # batch of the first step
             data_ctr.add_(1)
