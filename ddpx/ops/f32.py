@@ -243,9 +243,15 @@ def conv_wgrad(dy, x, Co, Ci, out, accumulate=False):
     _call("ddpx_f32_conv_wgrad_reduce", part.data_ptr(), S, Co, Ci, Cp, out.data_ptr(), int(accumulate))
 
 
-def bn_forward(y, N, H, W, C, bn, training, pool, stats=None):
+def bn_forward(y, N, H, W, C, bn, training, pool, stats=None, comm=None):
     """(x_next, a, b, mean, rstd): statistics + running-stat update + [pool](relu(a*(y-mean)+b)), a = gamma*rstd,
-    b = beta.  ``stats`` = (part, T, R): chunk statistics already made (the conv GEMM epilogue)."""
+    b = beta.  ``stats`` = (part, T, R): chunk statistics already made (the conv GEMM epilogue).
+
+    ``comm`` (SyncBatchNorm, ``--sync_bn`` under DDP; /root/reference/multigpu.py:127): this rank's (mean, M2) is
+    merged from its chunk statistics (``ddpx_bn_local_stats``), all-gathered ([world][2][C], one collective on the
+    current stream: graph-capturable on RCCL), and the finalize merges the ranks in rank order as equal chunks
+    of P rows each, so the batch statistics and the running-stat update (unbiased with the global count, as
+    torch's SyncBatchNorm) are the global ones.  Every rank holds the same P (equal DistributedSampler shards)."""
     dev = y.device
     P = N * H * W
     a = torch.empty(C, dtype=torch.float32, device=dev)
@@ -258,8 +264,17 @@ def bn_forward(y, N, H, W, C, bn, training, pool, stats=None):
         part = torch.empty((T, 2, C), dtype=torch.float32, device=dev) if training else a
         if training:
             _call("ddpx_f32_bn_stats", y.data_ptr(), P, C, R, part.data_ptr())
+    Ptot = P
+    if training and comm is not None:
+        local = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        native.check(native.kernels().ddpx_bn_local_stats(part.data_ptr(), T, R, P, C, local.data_ptr(),
+                                                          native.stream_handle()), "ddpx_bn_local_stats")
+        ws = comm.world_size
+        part = torch.empty(ws * 2 * C, dtype=torch.float32, device=dev)
+        comm.allgather(part, local)
+        T, R, Ptot = ws, P, ws * P
     nbt = bn.num_batches_tracked if (training and bn.num_batches_tracked is not None) else None
-    _call("ddpx_f32_bn_finalize", part.data_ptr(), T, R, P, C, bn.weight.data_ptr(), bn.bias.data_ptr(),
+    _call("ddpx_f32_bn_finalize", part.data_ptr(), T, R, Ptot, C, bn.weight.data_ptr(), bn.bias.data_ptr(),
           bn.running_mean.data_ptr(), bn.running_var.data_ptr(), native.ptr(nbt), float(bn.momentum),
           float(bn.eps), int(training), a.data_ptr(), b.data_ptr(), mean.data_ptr(), rstd.data_ptr())
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)
@@ -269,8 +284,12 @@ def bn_forward(y, N, H, W, C, bn, training, pool, stats=None):
     return out, a, b, mean, rstd
 
 
-def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumulate=False):
-    """dy [P, C] of BatchNorm+ReLU(+MaxPool) given the block output gradient g; dgamma/dbeta (+)= ..."""
+def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumulate=False, comm=None):
+    """dy [P, C] of BatchNorm+ReLU(+MaxPool) given the block output gradient g; dgamma/dbeta (+)= ...
+
+    ``comm`` (SyncBatchNorm): the per-channel means c1 = mean(dy), c2 = mean(dy * xhat) are summed over the ranks
+    (one all-reduce of [2][C]) and divided by the world size — the global means, every rank holding P rows — before
+    the apply; dgamma / dbeta stay this rank's sums (DDP averages them), as in torch's SyncBatchNorm."""
     _f32(g, "g")
     P = N * H * W
     R = bn_chunk_rows(P, C)
@@ -278,9 +297,14 @@ def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumul
     part = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
     _call("ddpx_f32_bn_bwd_sums", g.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
           rstd.data_ptr(), N, H, W, C, int(pool), R, part.data_ptr())
-    c1, c2 = torch.empty_like(a), torch.empty_like(a)
+    cc = torch.empty(2 * C, dtype=torch.float32, device=y.device)
+    c1, c2 = cc[:C], cc[C:]
     _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), native.ptr(dgamma),
           native.ptr(dbeta), int(accumulate))
+    if comm is not None:
+        comm.allreduce_(cc, op="sum")
+        native.check(native.kernels().ddpx_scale_f32(cc.data_ptr(), 2 * C, 1.0 / comm.world_size,
+                                                     native.stream_handle()), "ddpx_scale_f32")
     dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
     _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
           rstd.data_ptr(), c1.data_ptr(), c2.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
@@ -353,9 +377,16 @@ def prep_vgg_input(x):
     raise ValueError(f"unsupported VGG input {tuple(x.shape)} {x.dtype}")
 
 
+def _sync_comm(model, training):
+    """SyncBatchNorm communicator (``--sync_bn`` under DDP at world size > 1), else None."""
+    comm = getattr(model, "sync_bn_comm", None)
+    return comm if (training and comm is not None and comm.world_size > 1) else None
+
+
 def _vgg_forward(model, x, targets, training):
     plan = _vgg_plan(model)
     saved = []
+    comm = _sync_comm(model, training)
     N, H, W, C = x.shape
     for bi, (conv, bn, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
@@ -364,7 +395,7 @@ def _vgg_forward(model, x, targets, training):
             y, st = conv_fwd_stats(x, plan.wf[bi], Co)
         else:
             y, st = conv_fwd(x, plan.wf[bi], Co), None
-        xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool, stats=st)
+        xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool, stats=st, comm=comm)
         saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co
@@ -385,12 +416,13 @@ def _vgg_backward(model, saved, last, dl, grad_out):
     flat.grad_done(cls.weight)
     flat.grad_done(cls.bias)
     g = avgpool_backward(dfeat, *xshape)
+    comm = _sync_comm(model, True)
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, bn, pool = plan.blocks[bi]
         x, y, a, b, mean, rstd, (N, H, W, C, Co), _ = saved[bi]
         dgam, accg = flat.grad_target(bn.weight)
         dbet, _ = flat.grad_target(bn.bias)
-        dy = bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgam, dbet, accumulate=accg)
+        dy = bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgam, dbet, accumulate=accg, comm=comm)
         flat.grad_done(bn.weight)
         flat.grad_done(bn.bias)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))

@@ -221,13 +221,11 @@ def build_model_and_optimizer(args, device, distributed: bool = False, comm=None
     model = build_model(args.model, hidden=args.hidden, layers=args.layers, dtype=args.dtype, device=device,
                         kernels=args.kernels, fp8=getattr(args, "fp8", False))
     if getattr(args, "sync_bn", False) and distributed:
-        if (getattr(model, "use_native", False) and device.type == "cuda"
-                and getattr(model, "native_dtype", "bf16") != "fp32"):
-            # native path: the BN kernels merge statistics across ranks themselves (ops/vgg_native.py)
+        if getattr(model, "use_native", False) and device.type == "cuda":
+            # native path, bf16 and fp32: the BN kernels merge statistics across ranks themselves
+            # (ops/vgg_native.py, ops/f32.py bn_forward / bn_backward with comm)
             model.sync_bn_comm = comm
         else:
-            if getattr(model, "native_dtype", "bf16") == "fp32":
-                model.use_native = False  # fp32 SyncBatchNorm: torch-op BatchNorm on the merged statistics
             model = convert_sync_batchnorm(model, comm)
     if args.graph and device.type == "cuda" and not getattr(model, "use_native", True):
         # torch-op models (--kernels torch: MIOpen / hipBLASLt ops) step eagerly: capturing torch's autograd with

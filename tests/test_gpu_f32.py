@@ -511,3 +511,58 @@ def test_conv_fwd_stats_epilogue(gpu, N, H, C, Co):
     finally:
         Fk.set_staging(prev)
     assert st3 is None and torch.equal(y3, y4)
+
+
+class _MirrorComm:
+    """A 2-rank communicator whose other rank holds exactly this rank's batch."""
+    world_size = 2
+    rank = 0
+
+    def allgather(self, out, inp, stream=None):
+        out.view(2, -1).copy_(inp.view(1, -1).expand(2, -1))
+
+    def allreduce_(self, t, op="sum", stream=None, async_op=False):
+        assert op == "sum"
+        t.mul_(2.0)
+
+
+def test_native_fp32_sync_batchnorm_matches_doubled_batch(gpu):
+    """Native fp32 SyncBatchNorm (``--sync_bn`` at the reference's precision, /root/reference/multigpu.py:127):
+    over a mirror communicator (the other rank holds the same batch) the statistics, running stats (unbiased with
+    the GLOBAL count) and every gradient equal those of torch BatchNorm on the doubled batch [x, x] (fp64 arbiter)."""
+    import copy
+
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.ops import f32 as Fk
+    torch.manual_seed(9)
+    native = build_model("vgg", dtype="fp32", device=gpu, kernels="native")
+    ref = copy.deepcopy(native).cpu().double()
+    ref.use_native = False
+    ref.compute_dtype = torch.float64
+    flat = ddpx.prepare_model(native, gpu)
+    native.sync_bn_comm = _MirrorComm()
+    assert Fk._sync_comm(native, True) is not None
+    x = torch.rand(32, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (32,), device=gpu)
+    flat.zero_grad()
+    loss, logits = native.forward_loss(x, y)
+    assert logits is None  # the native fp32 path ran
+    loss.backward()
+    x2, y2 = torch.cat([x, x]).cpu().double(), torch.cat([y, y]).cpu()
+    rl = F.cross_entropy(ref(x2), y2)
+    rl.backward()
+    assert abs(loss.item() - rl.item()) < 1e-5, (loss.item(), rl.item())
+    for (n, b), (_, rb) in zip(native.named_buffers(), ref.named_buffers()):
+        if b.is_floating_point():
+            assert torch.allclose(b.cpu().double(), rb, rtol=1e-5, atol=1e-6), n
+        else:
+            assert int(b) == int(rb), n
+    rp = dict(ref.named_parameters())
+    bad = []
+    for n, p in native.named_parameters():
+        e = _rel(p.main_grad.cpu(), rp[n].grad)
+        top = n.startswith(("classifier", "backbone.bn7"))
+        if not e < (1e-5 if top else 5e-3):  # pooling-decision flips below bn7 (test above)
+            bad.append((n, e))
+    assert not bad, bad

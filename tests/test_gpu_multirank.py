@@ -180,6 +180,8 @@ def _syncbn_worker(rank, ws, port, mode, errq):
     mode "dup": both ranks hold the same half (SyncBN == local BN);  "nosync": plain BN, reference = the
     two half batches run one after the other with loss / ws (DDP semantics)."""
     import torch.distributed as dist
+    f32 = mode.endswith("_f32")  # the reference's precision: the native exact-f32 kernels (ops/f32.py)
+    mode = mode[:-4] if f32 else mode
     try:
         import ddpx
         from ddpx.models import VGG
@@ -195,6 +197,7 @@ def _syncbn_worker(rank, ws, port, mode, errq):
         comm = HostStagedComm()
         for m in (ours, ref):
             m.use_native = True
+            m.native_dtype = "fp32" if f32 else "bf16"
         if mode != "nosync":
             ours.sync_bn_comm = comm
         ddpx.prepare_model(ours, dev)
@@ -206,9 +209,9 @@ def _syncbn_worker(rank, ws, port, mode, errq):
         B = 32
         for s in range(2):
             g = torch.Generator(device="cpu").manual_seed(500 + s)
-            xg = torch.rand(ws * B, 32, 32, 8, generator=g)
+            xg = torch.rand(ws * B, 32, 32, 4 if f32 else 8, generator=g)
             xg[..., 3:] = 0
-            xg = xg.to(dev).to(torch.bfloat16)
+            xg = xg.to(dev) if f32 else xg.to(dev).to(torch.bfloat16)
             tg = torch.randint(0, 10, (ws * B,), generator=g).to(dev)
             if mode == "dup":
                 xg, tg = xg[:B].repeat(ws, 1, 1, 1), tg[:B].repeat(ws)
@@ -246,7 +249,8 @@ def _syncbn_worker(rank, ws, port, mode, errq):
                 # test_native_sync_batchnorm_ops_two_ranks (kernels, 2 ranks) and
                 # test_native_sync_batchnorm_kernels_match_local_bn (whole VGG, mirror communicator);
                 # here: wiring (collective order, replica consistency) and the forward statistics.
-                tol = 0.2 if mode == "sync" else 2e-2
+                # fp32: no bf16 activation noise to magnify; what remains are max-pool routing flips
+                tol = (2e-2 if f32 else 0.2) if mode == "sync" else 2e-2
                 bad = []
                 for (n, p), q in zip(ours.named_parameters(), ref.parameters()):
                     rel = ((p.main_grad - q.main_grad).norm() / q.main_grad.norm().clamp_min(1e-12)).item()
@@ -272,7 +276,7 @@ def _syncbn_worker(rank, ws, port, mode, errq):
         raise
 
 
-@pytest.mark.parametrize("mode", ["nosync", "dup", "sync"])
+@pytest.mark.parametrize("mode", ["nosync", "dup", "sync", "dup_f32", "sync_f32"])
 def test_native_sync_batchnorm_two_ranks_one_gpu(gpu, mode):
     """``--sync_bn`` on the native VGG: statistics all-gathered / gradient sums all-reduced between the
     native BN kernels; two half-batch ranks track one full-batch process."""
