@@ -89,6 +89,14 @@ def main():
         cases[f"fwd0_t{tile}"] = lambda tile=tile: G.linear_fwd(x, w0, b0, relu=True, out=h1, tile=tile)
         cases[f"fwd1_t{tile}"] = lambda tile=tile: G.linear_fwd(h1, w1, b1, relu=True, out=h2, tile=tile)
         cases[f"dgrad1_t{tile}"] = lambda tile=tile: G.linear_dgrad(d2, w1, relu_mask_of=h1, out=d1, tile=tile)
+    # warp-specialised split-K tiles (cfg 16: 256x128 8 math + 4 loader waves; 17: 128x128 4 + 4)
+    for tile, sp in ((16, 4), (16, 2), (17, 2), (17, 4), (14, 2)):
+        cases[f"fwd0_t{tile}s{sp}"] = lambda tile=tile, sp=sp: G.linear_fwd(x, w0, b0, relu=True, out=h1, tile=tile,
+                                                                             splits=sp)
+        cases[f"fwd1_t{tile}s{sp}"] = lambda tile=tile, sp=sp: G.linear_fwd(h1, w1, b1, relu=True, out=h2, tile=tile,
+                                                                             splits=sp)
+        cases[f"dgrad1_t{tile}s{sp}"] = lambda tile=tile, sp=sp: G.linear_dgrad(d2, w1, relu_mask_of=h1, out=d1,
+                                                                                tile=tile, splits=sp)
     for tile in (-1, 13, 5, 1, 0):
         cases[f"wgrad1_t{tile}"] = lambda tile=tile: G.linear_wgrad(d2, h1, dW1, tile=tile)
         cases[f"wgrad0_t{tile}"] = lambda tile=tile: G.linear_wgrad(d1, x, dW0, tile=tile)

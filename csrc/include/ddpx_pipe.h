@@ -115,7 +115,15 @@ struct Params {
   int cs_flags;
   int* cs_tcnt;
   int im_slow;             // 1: im2col A operands use the per-chunk src_off path (A/B checks of ImRows)
+  // diagnostics (ddpx_gemm_set_stamps): per-workgroup s_memrealtime stamps (100 MHz) at kernel start, main loop
+  // end, split-K ticket taken, combine done, epilogue done: [workgroup][8] int64; nullptr = off
+  long long* stamp;
 };
+
+__device__ __forceinline__ void stamp_at(const Params& p, int tid, int k) {
+  if (p.stamp && tid == 0)
+    p.stamp[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
 
 constexpr unsigned kOOB = 0x80000000u;
 
@@ -370,6 +378,23 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Ring hand-off words of the warp-specialised pipeline (LW loader waves): monotone per-slot counters in the
+// kernel's one LDS array.  A poll is a relaxed workgroup-scope load in an s_sleep loop, bounded so that a
+// broken hand-off ends the kernel (wrong results, caught by the tests) instead of spinning forever
+// (~2^20 polls x 64 clocks ~ 30 ms; a healthy wait is well under 100 us).
+__device__ __forceinline__ void lds_wait_ge(int* c, int target) {
+  for (int it = 0; it < (1 << 20); ++it) {
+    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // no LDS read of the slot moves above the poll
+}
+
+__device__ __forceinline__ void lds_signal(int* c, int lane) {
+  asm volatile("" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // ---------------------------------------------------------------- epilogue
 // The accumulator tile is staged through LDS as fp32 [BM][BN+4]; every thread
 // then owns one 4-column quad (BN/4 quads, 256 % (BN/4) == 0) for rows
@@ -543,9 +568,16 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 // KSUB: 64-wide K sub-tiles per stage (one barrier per 64*KSUB of K).
 // SGDPF (fused-SGD wgrad only): the tile's fp32 master / momentum rows are LDS-DMA'd into a side
 // buffer during the main loop, so the optimizer epilogue only streams writes.
+// LW > 0: warp-specialised ring.  LW extra LOADER waves (the last ones of the workgroup) issue every K-step's
+// LDS-DMA and publish it (counted vmcnt, then a FULL counter per slot); the NW MATH waves wait on FULL, read
+// their fragments, release the slot (FREE counter) and run the MFMAs.  No workgroup barrier in the main loop:
+// the math waves never wait for each other, and the loaders run up to STAGES - 1 K-steps ahead of the slowest
+// math wave (the barrier-coupled ring lets 8 waves meet at every K-step: 52 vs 77 GB/s of L2 -> LDS per CU on
+// the 128x128 tile, profiles/r2_splitk).  The loaders end after the last publish; the math waves then run the
+// combine and epilogue (an s_barrier waits only for waves that have not ended).
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
-          bool SGDPF = false, bool SK = false>
-__global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
+          bool SGDPF = false, bool SK = false, int LW = 0>
+__global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
   constexpr int BK = 64 * KSUB;
@@ -559,12 +591,18 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
   constexpr int PF_PER_WAVE = SGDPF ? (BM / PF_RPI) / NW : 0;  // per array
   constexpr int PFW = 2 * PF_PER_WAVE;                        // prefetch DMA ops per wave
   static_assert(!SGDPF || (BM % (PF_RPI * NW) == 0 && 64 % PF_CPR == 0), "prefetch geometry");
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT + PF_BYTES];
+  static_assert(LW == 0 || (!SGDPF && KSUB == 1 && AMODE == MODE_PLAIN && BMODE == MODE_PLAIN && STAGES <= 8),
+                "warp-specialised ring: plain operands, one 64-deep K sub-tile per slot");
+  constexpr int FLAG_BYTES = LW ? 64 : 0;  // FULL[8], FREE[8]
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT + PF_BYTES + FLAG_BYTES];
+  int* const ring_full = reinterpret_cast<int*>(smem + STAGES * SLOT + PF_BYTES);
+  int* const ring_free = ring_full + 8;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // wm in [0, WGM)
+  stamp_at(p, tid, 0);
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -675,6 +713,40 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     }
   };
 
+  if constexpr (LW > 0) {
+    if (tid < 16) ring_full[tid] = 0;  // FULL[0..7], FREE[0..7]
+    __syncthreads();
+    if (wave >= NW) {
+      // ------------------------------------------------------------ loader waves
+      const int lw = wave - NW;
+      constexpr int LPL = (BM + BN) / (8 * LW);  // LDS-DMA instructions per loader wave per K-step
+      for (int t = 0; t < nk; ++t) {
+        const int sl = t % STAGES;
+        if (t >= STAGES) lds_wait_ge(ring_free + sl, (t / STAGES) * NW);  // every math wave read step t - STAGES
+        char* slot = smem + sl * SLOT;
+        const int k0 = kbeg + t * 64;
+        stage_tile<BM, AK, AMODE, LW>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, lw, lane);
+        stage_tile<BN, BKc, BMODE, LW>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, lw, lane);
+        if (t >= 1) {  // this wave's share of step t - 1 has landed: publish it
+          wait_vmcnt<LPL>();
+          lds_signal(ring_full + (t - 1) % STAGES, lane);
+        }
+      }
+      if (nk >= 1) {
+        wait_vmcnt<0>();
+        lds_signal(ring_full + (nk - 1) % STAGES, lane);
+      }
+      return;
+    }
+    // --------------------------------------------------------------- math waves
+    for (int t = 0; t < nk; ++t) {
+      const int sl = t % STAGES;
+      lds_wait_ge(ring_full + sl, (t / STAGES + 1) * LW);
+      mma_slot(t);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+      lds_signal(ring_free + sl, lane);
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s);
@@ -692,7 +764,9 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     if (t == 0) prefetch_sgd();
     mma_slot(t);
   }
+  }
 
+  stamp_at(p, tid, 1);
   // ---- in-launch split-K combine (cdna_hip_programming §5 "Projection GEMM" item 2, sc1 form) ----
   if constexpr (SK) {
     constexpr int NF = FM * FN;
@@ -713,25 +787,26 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) *flag = __hip_atomic_fetch_add(p.tcnt + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    stamp_at(p, tid, 2);
     if (*flag != S - 1) return;  // not the last split of this tile
     if (tid == 0) __hip_atomic_store(p.tcnt + wg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // sum in split order (own partial from registers): the same bits whichever split arrives last
-    f32x4 tot[FM][FN];
+    // sum in split order, every partial (this split's too) read back from its slab: the same bits whichever split
+    // arrives last, and the accumulators are the running sum (no second tile of registers: the 8-wave tiles
+    // would spill); one split's fragments are in flight together
     for (int sp = 0; sp < S; ++sp) {
+      f32x4 v[FM][FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const f32x4 v = sp == split ? acc[i][j]
-                                      : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                      rsl, slab_off(sp, i * FN + j), 0, 16 /* sc1 */));
-          tot[i][j] = sp == 0 ? v : tot[i][j] + v;
-        }
+        for (int j = 0; j < FN; ++j)
+          v[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl, slab_off(sp, i * FN + j), 0,
+                                                                                    16 /* sc1 */));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = sp == 0 ? v[i][j] : acc[i][j] + v[i][j];
     }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = tot[i][j];
+    stamp_at(p, tid, 3);
   }
 
   // ---- stage the accumulator tile through LDS (all DMA has landed: last wait was vmcnt(0)) ----
@@ -816,13 +891,15 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
       }
     }
   }
+  stamp_at(p, tid, 4);
   if (!p.colsum || p.epi == EPI_BNSTAT_BF16) return;
 
   // ---- per-tile column sums (bias gradient) ----
   __syncthreads();
   quad_colsum<BN, NT>(red, cs, tid, colres);
-  if (NW != 4 || !p.cs_tcnt) {  // (the in-launch finish is built for the 4-wave tiles only: it adds
-                                // spills to the register-bound 8-wave ones, which no dgrad picks)
+  if ((NW != 4 && LW == 0) || !p.cs_tcnt) {  // (the in-launch finish is built for the 4-wave tiles and the
+                                            // warp-specialised ones: it adds spills to the register-bound
+                                            // barrier-coupled 8-wave ones, which no dgrad picks)
     if (tid < BN && n0 + tid < p.N) p.colsum[(size_t)tm * p.N + n0 + tid] = colres[tid];
     return;
   }
@@ -864,15 +941,16 @@ __global__ void __launch_bounds__(NW * 64) gemm_pipe_kernel(Params p) {
 }
 
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
-          bool SGDPF = false, bool SK = false>
+          bool SGDPF = false, bool SK = false, int LW = 0>
 static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB, SGDPF, SK>),
-                     dim3(tiles, splits), dim3(NW * 64), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, STAGES, AK, BKc, AMODE, BMODE, NW, KSUB, SGDPF, SK, LW>),
+                     dim3(tiles, splits), dim3((NW + LW) * 64), 0, s, p);
   return hipGetLastError();
 }
 
-constexpr int kNumCfgs = 16;
+// cfg 16 / 17: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products, in-launch split-K
+constexpr int kNumCfgs = 18;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
 static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
 
@@ -882,7 +960,7 @@ static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
 static inline void tile_of(int cfg, int* bm, int* bn) {
   static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
                                      {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
-                                     {128, 128}, {128, 128}};
+                                     {128, 128}, {128, 128}, {256, 128}, {128, 128}};
   const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
@@ -899,6 +977,14 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 13: return launch<256, 256, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 64x128 each, 128 KiB
     case 14: return launch<128, 128, 3, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 96 KiB
     case 15: return launch<128, 128, 4, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 128 KiB
+    case 16:  // warp-specialised (plain operands only)
+      if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
+        return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8, 1, false, false, 4>(p, splits, s);
+      return hipErrorInvalidValue;
+    case 17:
+      if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
+        return launch<128, 128, 4, AK, BKc, AMODE, BMODE, 4, 1, false, false, 4>(p, splits, s);
+      return hipErrorInvalidValue;
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
     case 2: return launch<128, 64, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB
@@ -921,6 +1007,9 @@ static hipError_t dispatch_sk(const Params& p, int cfg, int splits, hipStream_t 
     case 8: return launch<256, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
     case 14: return launch<128, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
     case 15: return launch<128, 128, 4, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true>(p, splits, s);
+    // warp-specialised: 8 math waves (64x64 each) + 4 loaders, 3 x 48 KiB ring / 4 math waves + 4 loaders
+    case 16: return launch<256, 128, 3, AK, BKc, MODE_PLAIN, MODE_PLAIN, 8, 1, false, true, 4>(p, splits, s);
+    case 17: return launch<128, 128, 4, AK, BKc, MODE_PLAIN, MODE_PLAIN, 4, 1, false, true, 4>(p, splits, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -93,6 +93,12 @@ static int plan(int M, int N, int K, bool ak, bool bk, int epi, int* cfg) {
 
 using namespace ddpx;
 
+static long long* g_stamp = nullptr;
+
+// Diagnostics: every following ddpx_gemm_pipe launch writes per-workgroup timestamps into buf
+// ([workgroups][8] int64, s_memrealtime); nullptr turns it off (benchmarks/gemm_stamps.py).
+DDPX_API void ddpx_gemm_set_stamps(long long* buf) { g_stamp = buf; }
+
 // Number of row tiles (M direction) the kernel will use for cfg (for sizing colsum partials).
 DDPX_API int ddpx_gemm_pipe_tiles_m(int M, int N, int K, int a_kcontig, int b_kcontig, int tile_cfg) {
   int cfg = tile_cfg;
@@ -134,6 +140,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
                  M, N, K, lda, ldb, ldc, ldaux, epi, accumulate, alpha, (unsigned)a_bytes, (unsigned)b_bytes,
                  SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd},
                  pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr, cs_out, cs_flags, cs_tcnt};
+  p.stamp = g_stamp;
   if (cs_tcnt && (!colsum || epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || (!cs_out && !sgd_p) ||
                   (sgd_p && !sgd_lr)))
     return -10;
