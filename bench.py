@@ -386,6 +386,15 @@ def torch_runner(args, device, world, loader, idx_all, full, group=None):
     return model, net, opt, sched, run
 
 
+def graph_sizes(S: int, ramp: bool = True):
+    """Training steps per captured graph: S, and (``ramp``) the sizes a replay window opens with, each launch
+    covered by the GPU work of the one before (ddpx.runtime.graphs.GraphedSteps.schedule): 1, 4, S - 5, S."""
+    out = {1, S}
+    if ramp and S >= 8:
+        out |= {4, S - 5}
+    return sorted(out)
+
+
 def make_runner(args, device, world, loader, idx_all, full, comm=None):
     """The engine under test and ``run(k, n)`` for its steps k .. k+n-1 (returns the last loss).
 
@@ -470,9 +479,9 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
                 pstate["k"] += 1
                 return loss
 
-        def multi_body(x, y):
+        def multi_body(x, y, m):
             loss = None
-            for _ in range(S):
+            for _ in range(m):
                 loss = step_body(x, y)
             return loss
 
@@ -495,11 +504,14 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
             sig = pingpong_signature_of(opt)
             g = {1: CapturedCycle(step_body, static_x, static_y, signature=sig, use_inputs_as_static=True,
                                   comm=comm_obj)}
-            if S > 1:
-                g[S] = CapturedCycle(multi_body, static_x, static_y, signature=sig, use_inputs_as_static=True,
-                                     comm=comm_obj)
-                if g[S].period > 1 or g[1].period > 1 and S % g[1].period:
-                    g.pop(S)  # S-step graphs only when they leave the copies where the 1-step cycle expects them
+            # multi-step graphs: S, plus the ramp sizes a timed window starts with (GraphedSteps.schedule)
+            for m in graph_sizes(S, ramp=os.environ.get("DDPX_GRAPH_RAMP", "1") != "0"):
+                if m == 1:
+                    continue
+                g[m] = CapturedCycle(lambda x, y, m=m: multi_body(x, y, m), static_x, static_y, signature=sig,
+                                     use_inputs_as_static=True, comm=comm_obj)
+                if g[m].period > 1 or g[1].period > 1 and m % g[1].period:
+                    g.pop(m)  # m-step graphs only when they leave the copies where the 1-step cycle expects them
             return g
 
         def fallback():
@@ -809,6 +821,8 @@ def main(argv=None):
                    "comm": (args.comm if ddpx_ddp else None),
                    "graph": bool(runner is not None and runner.use_graph),
                    "graph_steps": (args.graph_steps if (runner is not None and runner.use_graph) else None),
+                   "graph_schedule": (runner.schedule(args.steps) if (runner is not None and runner.use_graph)
+                                      else None),
                    "prefetch_batch": bool(getattr(args, "prefetch_batch", 0)),
                    "graph_error": (runner.graph_error if runner is not None else None),
                    "optimizer": "sgd(lr=0.4 one-cycle, m=0.9, wd=5e-4)" + (

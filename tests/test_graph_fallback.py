@@ -49,7 +49,21 @@ def test_capture_success_replays_multi_step_graphs():
     steps = []
     r = GraphedSteps(eager, make_graphs, steps_per_graph=4, after=steps.append)
     r.run(0, 11)
-    assert seen == ["e", "e", "g4", "g4", "g1"] and sum(steps) == 11 and r.graph_error is None
+    # the replay window opens with the smallest graph (its launch is the only one not covered by queued GPU work)
+    assert seen == ["e", "e", "g1", "g4", "g4"] and sum(steps) == 11 and r.graph_error is None
+
+
+def test_replay_schedule_ramps_then_uses_the_largest_graph():
+    r = GraphedSteps(lambda: None, lambda: {}, steps_per_graph=20)
+    r.graphs = {1: None, 4: None, 15: None, 20: None}
+    assert r.schedule(20) == [1, 4, 15]
+    assert r.schedule(200) == [1, 4, 15] + [20] * 9
+    assert r.schedule(3) == [1, 1, 1]
+    assert r.schedule(26) == [1, 4, 15, 4, 1, 1]
+    for n in range(1, 90):
+        assert sum(r.schedule(n)) == n
+    r.graphs = {1: None}
+    assert r.schedule(5) == [1] * 5
 
 
 def _rank(rank, world, port, q):
