@@ -107,6 +107,9 @@ def parse(argv=None):
                         "slice of the weight gradient is written (opt-in; default off)")
     p.add_argument("--defer_gather", type=int, default=None,
                    help="ZeRO-1 only: all-gathers issued at the start of the next step, waited per chunk")
+    p.add_argument("--side_optimizer", type=int, default=None,
+                   help="replicated plan with optimizer overlap: each bucket's SGD update on a side stream behind its "
+                        "all-reduce and its weights' last read in backward, one join per step (default 1)")
     p.add_argument("--comm_side_optimizer", type=int, default=None,
                    help="ZeRO-1 only: shard updates on the RCCL stream behind each reduce-scatter")
     p.add_argument("--first_bucket_mb", type=float, default=None)
@@ -282,6 +285,8 @@ def resolve_zero_defaults(args):
         return
     if args.comm_side_optimizer is None:
         args.comm_side_optimizer = int(bool(args.shard_optimizer))
+    if getattr(args, "side_optimizer", None) is None:
+        args.side_optimizer = int(os.environ.get("DDPX_SIDE_OPTIMIZER", "1") != "0")
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 
@@ -322,7 +327,8 @@ def build_ddpx(args, device, world, comm=None):
                                       overlap_optimizer=bool(args.overlap_optimizer),
                                       shard_optimizer=bool(args.shard_optimizer), chunk_mb=args.chunk_mb or None,
                                       defer_gather=bool(args.defer_gather),
-                                      comm_side_optimizer=bool(args.comm_side_optimizer))
+                                      comm_side_optimizer=bool(args.comm_side_optimizer),
+                                      side_stream_optimizer=bool(getattr(args, "side_optimizer", 0)))
         if args.overlap_optimizer or args.shard_optimizer:
             net.attach_optimizer(opt)
     sched = one_cycle(opt, resolve_steps_per_epoch("compat", 0, world > 1))
@@ -606,6 +612,7 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
         a.bucket_cap_mb = plan["bucket_cap_mb"]
         a.first_bucket_mb = plan["first_bucket_mb"]
         a.comm_side_optimizer = args.comm_side_optimizer
+        a.side_optimizer = getattr(args, "side_optimizer", None)
         a.defer_gather = args.defer_gather
         if not args.chunk_explicit:
             a.chunk_mb = plan.get("chunk_mb") or 0.0
@@ -841,6 +848,8 @@ def main(argv=None):
                    "comm_side_optimizer": (bool(args.comm_side_optimizer)
                                            if (ddpx_ddp and args.shard_optimizer) else None),
                    "overlap_optimizer": bool(args.overlap_optimizer) if multi else None,
+                   "side_stream_optimizer": (bool(getattr(args, "side_optimizer", 0))
+                                             if (ddpx_ddp and not args.shard_optimizer) else None),
                    "final_loss": round(final_loss, 4), "ddp": bool(multi),
                    "replicas_consistent": consistent,
                    "master_digest": digest,

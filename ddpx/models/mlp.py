@@ -107,10 +107,14 @@ class MLP(nn.Module):
 
     def ddpx_spec(self, device):
         """Flat-store layout request: bf16 compute shadow + all params written by native kernels."""
+        # hidden weights W_l (l >= 1) are read by the data-gradient GEMM after their gradient is produced: a
+        # side-stream optimizer may update them only after the model's flat.release (ddpx.parallel.ddp)
+        late = [lin.weight for lin in self.linears()[1:-1]]
         if torch.device(device).type == "cuda" and self.use_native and self.compute_dtype == torch.float32:
             from ..runtime import native
             native.kernels()
-            return {"native_params": list(self.parameters())}  # fp32: kernels read the masters
+            # fp32: kernels read the masters
+            return {"native_params": list(self.parameters()), "late_read_params": late}
         if self.native_active(device):
             from ..runtime import native
             native.kernels()  # fail loudly if the extension is missing on a GPU
@@ -119,7 +123,7 @@ class MLP(nn.Module):
             # offset / 32) is 16-B / 4-B aligned for the MX GEMM's operand loads
             return {"shadow_dtype": torch.bfloat16, "native_params": list(self.parameters()),
                     "shadow_only_params": [m.weight for m in self.modules() if isinstance(m, nn.Linear)],
-                    "align": 128 if getattr(self, "fp8", False) else 64}
+                    "align": 128 if getattr(self, "fp8", False) else 64, "late_read_params": late}
         return {}
 
     def input_layout(self, device) -> str:

@@ -626,6 +626,7 @@ def _mlp_backward(model, hs, dl, grad_out):
         _grad_write(flat, lin.bias, lambda o, ac: colsum(dz, o, ac))
         if i > 0:
             dz = linear_dgrad(dz, lin.weight, mask=hs[i])
+            flat.release(lin.weight)  # last read of W_i in this backward
 
 
 class _MLPLossF32(torch.autograd.Function):

@@ -200,6 +200,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             # ReLU backward + bias gradient of layer l-1 fused into the dgrad epilogue
             dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_grad=dbl,
                                    bias_grad_accumulate=accl)
+            flat.release(w)  # W_l's last read: a side-stream update of its bucket may start now
             flat.grad_done(bp)
             dpre = dnext
 

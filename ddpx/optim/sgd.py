@@ -252,9 +252,25 @@ class SGD(Optimizer):
                 self._update(*f.span(i, j), g)
                 i = j + 1
         elif src is not None and src.overlap_active():
-            for (start, end) in src.bucket_ranges_in_completion_order():
-                src.wait_range(start, end)
-                self._update(start, end, g)
+            side = src.update_side_stream() if hasattr(src, "update_side_stream") else None
+            if side is None:
+                for (start, end) in src.bucket_ranges_in_completion_order():
+                    src.wait_range(start, end)
+                    self._update(start, end, g)
+            else:
+                # each bucket's update on the side stream behind its all-reduce and its weights' release, in
+                # completion order (no wait for the end of backward); one join into the compute stream.  A pending
+                # LR advance (none when the head kernel took it) is launched on the side stream before the first
+                # update reads the LR.
+                cur = torch.cuda.current_stream()
+                for (start, end) in src.bucket_ranges_in_completion_order():
+                    b = src.bucket_ranges.index((start, end))
+                    src.side_wait_bucket(b, side)
+                    with torch.cuda.stream(side):
+                        self._update(start, end, g)
+                done = torch.cuda.Event()
+                done.record(side)
+                cur.wait_event(done)
             src.optimizer_done()
         else:
             self._update(0, self.flat.total, g)

@@ -271,7 +271,7 @@ class DistributedDataParallel(nn.Module):
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
                  reduce_single: bool = False, shard_optimizer: bool = False, chunk_mb: float | None = None,
                  defer_gather: bool = False, comm_side_optimizer: bool = False,
-                 find_unused_parameters: bool = False):
+                 find_unused_parameters: bool = False, side_stream_optimizer: bool = False):
         super().__init__()
         # torch DDP semantics: False (default) -> a parameter without gradient on some rank is an error at
         # world size > 1 (its bucket would otherwise be issued in a different order on different ranks);
@@ -394,6 +394,27 @@ class DistributedDataParallel(nn.Module):
                     raise RuntimeError(f"DDP: bucket layout differs between rank {self.rank} and rank {r}")
         self.debug = os.environ.get("DDPX_DEBUG", "0") == "1"
         self.flat.sink = self
+        # replicated plan, optimizer overlap: every bucket's SGD update runs on a side stream as soon as (a) its
+        # all-reduce has landed and (b) nothing later in this backward reads its weights — the bucket's ready
+        # point, or for a parameter the model declares read after its gradient (flat.late_read: the MLP's data
+        # gradient reads W_l after W_l's gradient was produced) the model's release (flat.release, recorded on
+        # the compute stream right after that last read), or the end of backward if the release never came.
+        # One join of the side stream per step instead of one wait per bucket on the compute stream, and the
+        # updates overlap the rest of backward (at N > 1: the later buckets' collectives)
+        self._opt_stream = None
+        if (side_stream_optimizer and active and not self.sharded and overlap_optimizer
+                and isinstance(comm, RcclComm) and dev.type == "cuda"):
+            self._opt_stream = torch.cuda.Stream(dev)
+            from ..runtime.graphs import register_side_stream
+            self._side_name = f"DDP optimizer stream #{id(self)}"
+            register_side_stream(self._opt_stream, self._side_name)
+        late = getattr(self.flat, "late_read", None)
+        # late-read parameters per bucket; unknown read pattern (late = None): every bucket waits for backward's end
+        self._late = [(sum(1 for i in self.bucket_params[b] if id(self.flat.params[i]) in late) if late is not None
+                       else 1 << 30) for b in range(len(self.bucket_ranges))]
+        self._released = [0] * len(self.bucket_ranges)
+        self._rel_ev = [None] * len(self.bucket_ranges)
+        self._bwd_end_ev = None
         self._completion_order = []
         self._marks = [0] * len(self.bucket_ranges)
         # deferred all-gather (ZeRO-1 shadow gathers): the optimizer leaves the gathers of the updated
@@ -561,6 +582,9 @@ class DistributedDataParallel(nn.Module):
             self.reducer.prepare()
             self._completion_order = []
             self._marks = [0] * len(self.bucket_ranges)
+            self._released = [0] * len(self.bucket_ranges)
+            self._rel_ev = [None] * len(self.bucket_ranges)
+            self._bwd_end_ev = None
         self._queued = False
         if self.module.training:
             self._sync_buffers()
@@ -599,6 +623,19 @@ class DistributedDataParallel(nn.Module):
                 self.reducer.mark_ready(b, 1)
             if self._marks[b] == self.bucket_expected[b]:
                 self._completion_order.append(b)
+
+    def param_released(self, i: int):
+        """The model's last read of parameter i in this backward has been issued (flat.release): once every
+        late-read parameter of its bucket is released, the side-stream update of that bucket may start."""
+        if self._opt_stream is None or not self._sync_enabled:
+            return
+        bs = self.chunk_bucket[i] if i in self.chunk_bucket else [self.bucket_of[i]]
+        for b in bs:
+            self._released[b] += 1
+            if self._released[b] == self._late[b]:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+                self._rel_ev[b] = ev
 
     def reducer_launched(self, b):
         return self._marks_complete(b)
@@ -652,6 +689,10 @@ class DistributedDataParallel(nn.Module):
             for i in skip:
                 self.flat.updated[i] = True
             return
+        if self._opt_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self._bwd_end_ev = ev  # release point of buckets whose model never released their late reads
         if self.overlap_optimizer:
             self._overlap_pending = True
             # launch stragglers but do not join: the optimizer waits per bucket
@@ -680,6 +721,18 @@ class DistributedDataParallel(nn.Module):
     def wait_range(self, start, end):
         b = self.bucket_ranges.index((start, end))
         self.reducer.wait_bucket(b)
+
+    def update_side_stream(self):
+        """Replicated plan: the stream the per-bucket SGD updates run on (side_stream_optimizer), else None."""
+        return self._opt_stream if self.overlap_active() else None
+
+    def side_wait_bucket(self, b, stream):
+        """Make ``stream`` wait for bucket b's all-reduce and for the release of its weights."""
+        self.reducer.wait_bucket(b, stream)
+        if self._late[b]:
+            ev = self._rel_ev[b] if self._released[b] >= self._late[b] else self._bwd_end_ev
+            if ev is not None:
+                stream.wait_event(ev)
 
     def optimizer_stream(self):
         """The stream the ZeRO-1 shard updates run on when ``comm_side_optimizer`` is set (the native
@@ -734,5 +787,9 @@ class DistributedDataParallel(nn.Module):
         return super().state_dict(*args, **kwargs)
 
     def close(self):
+        if self._opt_stream is not None:
+            from ..runtime.graphs import unregister_side_stream
+            unregister_side_stream(self._side_name)
+            self._opt_stream = None
         if self.reducer is not None and hasattr(self.reducer, "close"):
             self.reducer.close()

@@ -90,6 +90,9 @@ class FlatParams:
         self.updated = [False] * len(self.params)  # parameter already stepped by a fused-optimizer epilogue
         self.fused_opt = None  # set by ddpx.optim.SGD(fused_backward=True)
         self.sink = None
+        # parameters the model reads in backward AFTER producing their gradient (announced through release()):
+        # a side-stream optimizer must not rewrite them before that read (ddpx.parallel.ddp)
+        self.late_read = None
         self.optimizer = None  # the ddpx SGD that owns this store (set by SGD)
         # device LR-schedule advance of that optimizer not launched yet: (table, counter, lr) until a kernel
         # (the classifier head's forward) carries it or the optimizer launches it itself (ddpx.optim.sgd)
@@ -346,6 +349,11 @@ class FlatParams:
 
     def chunks_of(self, p):
         return self.chunk_rows.get(self.index[id(p)])
+
+    def release(self, p):
+        """The model's last read of p in this backward has been issued (p in ``late_read``)."""
+        if self.sink is not None and hasattr(self.sink, "param_released"):
+            self.sink.param_released(self.index[id(p)])
 
     def before_read(self, p, chunk=None):
         """Called by native ops right before they read p (or its row chunk) in a forward: a sharded

@@ -83,6 +83,9 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this (MB of gradient) into row-chunk DDP buckets")
+    p.add_argument("--side_optimizer", type=int, default=1,
+                   help="DDP with optimizer overlap, replicated optimizer: each bucket's SGD update on a side stream "
+                        "behind its all-reduce and its weights' last read in backward (0: on the compute stream)")
     p.add_argument("--comm_side_optimizer", action="store_true",
                    help="with --shard_optimizer on the RCCL path: shard updates on the communicator stream behind "
                         "each reduce-scatter (one join per step instead of one per bucket)")
@@ -263,7 +266,8 @@ def make_ddp(args, model, optimizer, comm):
                                   overlap_optimizer=args.overlap_optimizer,
                                   shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
                                   defer_gather=args.defer_gather,
-                                  comm_side_optimizer=args.comm_side_optimizer)
+                                  comm_side_optimizer=args.comm_side_optimizer,
+                                  side_stream_optimizer=bool(getattr(args, "side_optimizer", 1)))
     if args.overlap_optimizer or args.shard_optimizer:
         net.attach_optimizer(optimizer)
     return net
