@@ -286,7 +286,7 @@ def resolve_zero_defaults(args):
     if args.comm_side_optimizer is None:
         args.comm_side_optimizer = int(bool(args.shard_optimizer))
     if getattr(args, "side_optimizer", None) is None:
-        args.side_optimizer = int(os.environ.get("DDPX_SIDE_OPTIMIZER", "1") != "0")
+        args.side_optimizer = int(os.environ.get("DDPX_SIDE_OPTIMIZER", "0") == "1")
     if args.defer_gather is None:
         args.defer_gather = int(bool(args.shard_optimizer) and args.model.startswith("mlp"))
 
@@ -395,6 +395,9 @@ def torch_runner(args, device, world, loader, idx_all, full, group=None):
 def graph_sizes(S: int, ramp: bool = True):
     """Training steps per captured graph: S, and (``ramp``) the sizes a replay window opens with, each launch
     covered by the GPU work of the one before (ddpx.runtime.graphs.GraphedSteps.schedule): 1, 4, S - 5, S."""
+    extra = os.environ.get("DDPX_GRAPH_SIZES")  # diagnostics (benchmarks/window_probe.py): exact size set
+    if extra:
+        return sorted({1} | {int(v) for v in extra.split(",") if v.strip()})
     out = {1, S}
     if ramp and S >= 8:
         out |= {4, S - 5}

@@ -849,16 +849,19 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
       case EPI_BIAS_BF16: epilogue_vec<EPI_BIAS_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
       case EPI_BIAS_RELU_BF16: epilogue_vec<EPI_BIAS_RELU_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
       case EPI_BIAS_F32: epilogue_vec<EPI_BIAS_F32, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
-      case EPI_SGD:
-        epilogue_vec<EPI_SGD, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch,
-                                           SGDPF ? reinterpret_cast<const float*>(smem + STAGES * SLOT) : nullptr);
+      case EPI_SGD:  // (not instantiated in the warp-specialised kernels: their register budget is 168)
+        if constexpr (LW == 0)
+          epilogue_vec<EPI_SGD, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch,
+                                             SGDPF ? reinterpret_cast<const float*>(smem + STAGES * SLOT) : nullptr);
         break;
-      case EPI_BNSTAT_BF16: epilogue_vec<EPI_BNSTAT_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
+      case EPI_BNSTAT_BF16:
+        if constexpr (LW == 0) epilogue_vec<EPI_BNSTAT_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch);
+        break;
       default: epilogue_vec<EPI_RELUMASK_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cs[q] += ch[q];
-    if (p.colsum && p.epi == EPI_BNSTAT_BF16) {
+    if (LW == 0 && p.colsum && p.epi == EPI_BNSTAT_BF16) {
       // BatchNorm statistics of the stored (bf16-rounded) values per BMH-row stat tile (tm*EH + h):
       // tile mean, then M2 = sum (y - mean)^2 over this half's rows.
       __syncthreads();
@@ -949,8 +952,8 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
-// cfg 16 / 17: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products, in-launch split-K
-constexpr int kNumCfgs = 18;
+// cfg 16 - 20: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products
+constexpr int kNumCfgs = 21;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
 static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
 
@@ -960,7 +963,8 @@ static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
 static inline void tile_of(int cfg, int* bm, int* bn) {
   static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
                                      {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
-                                     {128, 128}, {128, 128}, {256, 128}, {128, 128}};
+                                     {128, 128}, {128, 128}, {256, 128}, {128, 128}, {64, 128}, {128, 64},
+                                     {64, 64}};
   const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
@@ -984,6 +988,20 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 17:
       if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
         return launch<128, 128, 4, AK, BKc, AMODE, BMODE, 4, 1, false, false, 4>(p, splits, s);
+      return hipErrorInvalidValue;
+    // one tile per CU at M = 512 (256 tiles), 6 x 24 KiB ring: 5 K-steps of LDS-DMA in flight per CU
+    case 18:
+      if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
+        return launch<64, 128, 6, AK, BKc, AMODE, BMODE, 4, 1, false, false, 4>(p, splits, s);
+      return hipErrorInvalidValue;
+    case 19:
+      if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
+        return launch<128, 64, 6, AK, BKc, AMODE, BMODE, 4, 1, false, false, 4>(p, splits, s);
+      return hipErrorInvalidValue;
+    // the 64x64 tile (two per CU) with a 4 x 16 KiB warp-specialised ring
+    case 20:
+      if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
+        return launch<64, 64, 4, AK, BKc, AMODE, BMODE, 4, 1, false, false, 4>(p, splits, s);
       return hipErrorInvalidValue;
     case 0: return launch<128, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);  // 128 KiB LDS, 1 WG/CU
     case 1: return launch<64, 128, 4, AK, BKc, AMODE, BMODE>(p, splits, s);   //  96 KiB

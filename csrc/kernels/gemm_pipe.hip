@@ -152,6 +152,7 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
   p.sgd_plain = sgd_plain;
   int cfg = tile_cfg >= 0 ? tile_cfg : pipe::pick(M, N, K, a_kcontig, b_kcontig);
   if (cs_tcnt && pipe::eight_wave(cfg)) return -11;  // in-launch column sums: 4-wave tiles only
+  if (cfg >= 16 && cfg <= 20 && (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16)) return -12;
   if (splits > 1) {  // in-launch split-K (ddpx_gemm_pipe_plan): the caller's cfg, slab and zeroed tickets
     if (epi == pipe::EPI_SGD || epi == pipe::EPI_BNSTAT_BF16 || !slab || !tcnt || tile_cfg < 0 || !a_kcontig)
       return -7;

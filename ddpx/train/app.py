@@ -83,7 +83,7 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--chunk_mb", type=float, default=None,
                    help="split weights larger than this (MB of gradient) into row-chunk DDP buckets")
-    p.add_argument("--side_optimizer", type=int, default=1,
+    p.add_argument("--side_optimizer", type=int, default=0,
                    help="DDP with optimizer overlap, replicated optimizer: each bucket's SGD update on a side stream "
                         "behind its all-reduce and its weights' last read in backward (0: on the compute stream)")
     p.add_argument("--comm_side_optimizer", action="store_true",

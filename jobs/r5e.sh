@@ -10,3 +10,9 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 200 --warmup 20 > gpurun_out/
 echo bench rc=$?
 timeout -k 10 600 python -u -m pytest -q -s --timeout 300 --timeout-method thread "tests/test_gpu_multirank.py::test_native_sync_batchnorm_two_ranks_one_gpu" > gpurun_out/r5e/syncbn.log 2>&1
 echo syncbn rc=$?
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_dist.py tests/test_gpu_capture.py > gpurun_out/r5e/dist.log 2>&1
+echo dist rc=$?
+for v in 1 0; do
+DDPX_SIDE_OPTIMIZER=$v timeout -k 10 300 python bench.py --gpus 1 --ddp_single --shard_optimizer 0 --bucket_plan default --steps 200 --warmup 20 > gpurun_out/r5e/ddp1_side$v.json 2>/dev/null || exit 1
+done
+echo ddp1 rc=$?

@@ -13,7 +13,7 @@ def _rand_bf16(*shape, dev):
     return (torch.randn(*shape, device=dev) * 0.5).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("tile", list(range(-1, 14)) + [16, 17])
+@pytest.mark.parametrize("tile", list(range(-1, 14)) + [16, 17, 18, 19, 20])
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
                                  (200, 136, 1000), (2048, 4096, 512)])
@@ -301,7 +301,8 @@ def test_native_libs_loaded(gpu):
 
 
 @pytest.mark.parametrize("tile,splits", [(-1, None), (12, None), (14, 2), (5, 2), (8, 4), (0, 3),
-                                         (16, 4), (16, 2), (16, None), (17, 2), (17, None)])
+                                         (16, 4), (16, 2), (16, None), (17, 2), (17, None), (18, None),
+                                         (19, None), (20, None)])
 def test_linear_mlp_shapes_splitk(gpu, tile, splits):
     """The toy-MLP products at M=512: default plan, a fixed single-pass tile, and the in-launch split-K
     (K split over workgroups whose fp32 partials the last split of each tile combines in split order)."""

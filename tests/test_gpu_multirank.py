@@ -260,7 +260,11 @@ def _syncbn_worker(rank, ws, port, mode, errq):
             o.step()
             o_ref.step()
         torch.cuda.synchronize()
-        if mode != "sync":  # bit-for-bit computations on both sides: the updates agree to summation order
+        # "dup" at fp32: the rank-merged statistics sum in another order than the local ones (fp32 round-off, no bf16
+        # rounding to absorb it), which flips max-pool routings below the first BN after the first step: two steps
+        # in, every update differs by ~3-4 % (the first step's gradients are checked above; the exact checks are
+        # test_gpu_f32.py::test_native_fp32_sync_batchnorm_matches_doubled_batch)
+        if mode != "sync" and not (f32 and mode == "dup"):  # bit-for-bit computations on both sides
             bad = []
             for (n, p), q, p0 in zip(ours.named_parameters(), ref.parameters(), w0):
                 du, dr = (p - p0).double(), (q - p0).double()
