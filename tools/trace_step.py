@@ -4,8 +4,13 @@
     python tools/trace_step.py TRACE_CSV [--marker augment] [--steps 3]
 
 Splits the dispatch sequence at every kernel whose name contains ``--marker`` (the batch augment kernel
-starts each ddpx step), and prints the last ``--steps`` complete steps as (order, kernel, us), plus the median
-duration of every position over all complete steps.  Used for the per-layer VGG breakdowns in profiles/.
+starts each ddpx step) and prints the step's dispatch sequence with the median duration of every position.
+The step shown is the MODAL one — the dispatch sequence most segments share (the graph-replayed training
+step) — not the last segment: a segment that ends at the next marker can also hold whatever ran between two
+steps (round 4's VGG table took the segment before the stock recipe's first augment, so it showed the bench's
+digest copies and the stock model's initialisation kernels as part of a step).  Segments
+with any other sequence are counted and listed by kernel count, never mixed into the medians.
+Used for the per-layer breakdowns in profiles/.
 """
 import argparse
 import csv
@@ -35,7 +40,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--marker", default="augment")
-    ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--exclude", default=None, help="drop steps containing a kernel with this substring")
     a = ap.parse_args()
     rows = []
@@ -56,11 +60,15 @@ def main():
     if not steps:
         print("no complete step found")
         return
-    L = len(steps[-1])
-    same = [st for st in steps if len(st) == L and [k for k, _ in st] == [k for k, _ in steps[-1]]]
-    print(f"{len(steps)} steps, {len(same)} with the last step's dispatch sequence ({L} kernels)")
+    from collections import Counter
+    sigs = Counter(tuple(k for k, _ in st) for st in steps)
+    modal, count = sigs.most_common(1)[0]
+    same = [st for st in steps if tuple(k for k, _ in st) == modal]
+    others = sorted(len(sig) for sig in sigs if sig != modal)
+    print(f"{len(steps)} segments; the modal dispatch sequence ({len(modal)} kernels) in {count} of them; "
+          f"{len(steps) - count} other segments (kernel counts {others}) excluded")
     tot = 0.0
-    for i, (k, _) in enumerate(steps[-1]):
+    for i, k in enumerate(modal):
         med = statistics.median(st[i][1] for st in same)
         tot += med
         print(f"{i:3d} {med:9.1f} us  {k}")
