@@ -392,15 +392,16 @@ def torch_runner(args, device, world, loader, idx_all, full, group=None):
     return model, net, opt, sched, run
 
 
-def graph_sizes(S: int, ramp: bool = True):
-    """Training steps per captured graph: S, and (``ramp``) the sizes a replay window opens with, each launch
-    covered by the GPU work of the one before (ddpx.runtime.graphs.GraphedSteps.schedule): 1, 4, S - 5, S."""
+def graph_sizes(S: int, warm: int = 0):
+    """Training steps per captured graph: 1, S, and ``warm`` = the warm-up steps left after capture: the graph the
+    warm-up replays once, so that a short timed window replays only graphs that already ran (a graph's first
+    replay is slow; ddpx.runtime.graphs.GraphedSteps.schedule, profiles/r5_window)."""
     extra = os.environ.get("DDPX_GRAPH_SIZES")  # diagnostics (benchmarks/window_probe.py): exact size set
     if extra:
         return sorted({1} | {int(v) for v in extra.split(",") if v.strip()})
     out = {1, S}
-    if ramp and S >= 8:
-        out |= {4, S - 5}
+    if warm >= 2:
+        out.add(min(warm, S))
     return sorted(out)
 
 
@@ -514,7 +515,7 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
             g = {1: CapturedCycle(step_body, static_x, static_y, signature=sig, use_inputs_as_static=True,
                                   comm=comm_obj)}
             # multi-step graphs: S, plus the ramp sizes a timed window starts with (GraphedSteps.schedule)
-            for m in graph_sizes(S, ramp=os.environ.get("DDPX_GRAPH_RAMP", "1") != "0"):
+            for m in graph_sizes(S, warm=args.warmup - 2):
                 if m == 1:
                     continue
                 g[m] = CapturedCycle(lambda x, y, m=m: multi_body(x, y, m), static_x, static_y, signature=sig,

@@ -61,7 +61,25 @@ def main():
             r["host_ms"].append((t1 - t0) * 1e3)
             r["first_gap_us"].append(e0.elapsed_time(evs[0][0]) * 1e3)
             r["gpu_ms"].append(e0.elapsed_time(evs[-1][1]))
-    out = {}
+    # first vs second replay of freshly captured graphs (GPU time between events around each replay)
+    fresh = {}
+    eng.runner.graphs = eng.runner.make_graphs()
+    for m in sorted(eng.runner.graphs, reverse=True):
+        gm = eng.runner.graphs[m]
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            s0.record()
+            gm()
+            s1.record()
+            t_host = (time.perf_counter() - t0) * 1e3
+            torch.cuda.synchronize()
+            ts.append({"gpu_ms": round(s0.elapsed_time(s1), 4), "launch_host_ms": round(t_host, 4)})
+        fresh[m] = ts
+        print(f"fresh graph of {m} steps, replays 1..3: {ts}", flush=True)
+    out = {"fresh_graph_replays": fresh}
     for name, r in res.items():
         med = {k: sorted(v)[len(v) // 2] for k, v in r.items()}
         out[name] = {k: round(v, 4) for k, v in med.items()}

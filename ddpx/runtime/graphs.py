@@ -431,6 +431,10 @@ class GraphedSteps:
         self.after = after
         self.graphs = None
         self.graph_error = None
+        self.warm = set()  # graph sizes replayed at least once
+        import os
+        # windows this long may replay a graph for the first time (DDPX_GRAPH_COLD_OK=1: any window, as before r5)
+        self.cold_ok = int(os.environ.get("DDPX_GRAPH_COLD_OK", "100"))
 
     def _capture(self):
         ok, err, graphs = True, None, None
@@ -456,29 +460,22 @@ class GraphedSteps:
         # the eager steps that follow must run, not be recorded into a capture the failure left open
         assert_no_capture("after a failed step capture")
 
-    def schedule(self, n: int):
-        """Graph sizes replayed for n consecutive steps: a ramp, then the largest graph, then the remainder.
+    def schedule(self, n: int, capture_run: bool = False):
+        """Graph sizes replayed for n consecutive steps (largest first).
 
-        Launching a graph of s steps costs host time roughly proportional to its s x kernels-per-step nodes, and
-        the GPU starts only after it: a first launch of the 20-step graph left the GPU idle ~0.4 ms at the start
-        of every timed window (the 20-step window ran at 0.2546 ms/step against 0.2327 over 200 steps,
-        profiles/r5_window).  Starting with the 1-step graph and growing (1, 4, 15, 20, ...) keeps every launch
-        shorter than the GPU work already queued ahead of it, so only the first (1-step) launch is exposed."""
+        The first replay of a freshly captured graph runs slower on the GPU than every later one (the 20-step
+        graph's first replay cost ~0.4 ms more: the driver's 20-step window ran at 0.2546 ms/step against 0.2347 with
+        warm graphs in one process, profiles/r5_window).  So a short window replays only graphs that have already
+        run once (the run that captured warms the largest graph fitting its remaining steps), and cold graphs are
+        used only in windows of ``cold_ok`` steps or more, where that one-off cost is amortised."""
         sizes = sorted(self.graphs) if self.graphs else [1]
-        out, ramp = [], True
+        if capture_run or n >= self.cold_ok:
+            pool = sizes
+        else:
+            pool = sorted({1} | {s for s in sizes if s in self.warm})
+        out = []
         while n > 0:
-            fit = [s for s in sizes if s <= n]
-            if not fit:
-                break
-            if ramp:
-                # next ramp size: the smallest graph larger than the last one (ramp ends at the largest)
-                prev = out[-1] if out else 0
-                bigger = [s for s in fit if s > prev]
-                m = bigger[0] if bigger else max(fit)
-                if m == max(sizes):
-                    ramp = False
-            else:
-                m = max(fit)
+            m = max(s for s in pool if s <= n)
             out.append(m)
             n -= m
         return out
@@ -487,17 +484,20 @@ class GraphedSteps:
         """Steps k .. k+n-1; returns the last step's loss."""
         loss = None
         plan = None
+        captured = False
         while n > 0:
             if self.use_graph and k >= self.eager_first and self.graphs is None:
                 self._capture()
+                captured = True
             if not self.use_graph or k < self.eager_first:
                 loss = self.eager_step()
                 m = 1
             else:
                 if plan is None:
-                    plan = self.schedule(n)
+                    plan = self.schedule(n, capture_run=captured)
                 m = plan.pop(0) if plan else 1
                 loss = self.graphs[m]()
+                self.warm.add(m)
             if self.after is not None:
                 self.after(m)
             k += m

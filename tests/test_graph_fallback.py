@@ -49,21 +49,22 @@ def test_capture_success_replays_multi_step_graphs():
     steps = []
     r = GraphedSteps(eager, make_graphs, steps_per_graph=4, after=steps.append)
     r.run(0, 11)
-    # the replay window opens with the smallest graph (its launch is the only one not covered by queued GPU work)
-    assert seen == ["e", "e", "g1", "g4", "g4"] and sum(steps) == 11 and r.graph_error is None
+    # the run that captured replays the largest graph that fits (warming it), then greedily
+    assert seen == ["e", "e", "g4", "g4", "g1"] and sum(steps) == 11 and r.graph_error is None
+    assert r.warm == {1, 4}
 
 
-def test_replay_schedule_ramps_then_uses_the_largest_graph():
+def test_replay_schedule_short_windows_use_warm_graphs_only():
     r = GraphedSteps(lambda: None, lambda: {}, steps_per_graph=20)
-    r.graphs = {1: None, 4: None, 15: None, 20: None}
-    assert r.schedule(20) == [1, 4, 15]
-    assert r.schedule(200) == [1, 4, 15] + [20] * 9
-    assert r.schedule(3) == [1, 1, 1]
-    assert r.schedule(26) == [1, 4, 15, 4, 1, 1]
-    for n in range(1, 90):
+    r.graphs = {1: None, 3: None, 20: None}
+    assert r.schedule(3, capture_run=True) == [3]
+    r.warm = {3}
+    assert r.schedule(20) == [3] * 6 + [1] * 2  # the cold 20-step graph is not replayed in a short window
+    assert r.schedule(200) == [20] * 10  # long window: the one-off first-replay cost is amortised
+    r.warm = {3, 20}
+    assert r.schedule(20) == [20]
+    for n in range(1, 130):
         assert sum(r.schedule(n)) == n
-    r.graphs = {1: None}
-    assert r.schedule(5) == [1] * 5
 
 
 def _rank(rank, world, port, q):
