@@ -133,6 +133,9 @@ def parse(argv=None):
     p.add_argument("--stock_first", type=int, default=None,
                    help="1: time the stock recipe BEFORE the ddpx warm-up instead of after the ddpx timing "
                         "(default 0)")
+    p.add_argument("--stock_between", type=int, default=1,
+                   help="1: time the stock recipe after the ddpx graph capture, before the last ddpx warm-up steps "
+                        "(the timed window then starts on a GPU at sustained-load clocks); 0: after the timed steps")
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args(argv)
 
@@ -748,8 +751,21 @@ def main(argv=None):
     if args.stock_ref and args.stock_first:
         # the baseline first (same process, same data), then the ddpx warm-up and timed steps
         stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
-    # warmup (includes graph capture for ddpx)
-    loss = run(0, args.warmup) if args.warmup else None
+    # warm-up (includes graph capture for ddpx).  The stock recipe is timed between the capture and the last
+    # warm-up replays (--stock_between, default): the GPU's clocks ramp for ~10 ms of sustained load
+    # (profiles/r5_window: per-step GPU time falls from ~0.26 to ~0.245 ms over a 60-step window), and a capture
+    # leaves the GPU idle for a while; this way the timed window starts on a GPU that has just been busy.  The
+    # ddpx engine still runs exactly --warmup untimed steps before its --steps timed ones.
+    loss = None
+    w1 = min(args.warmup, 2)
+    if w1:
+        loss = run(0, w1)
+    if runner is not None and args.warmup > w1:
+        runner.capture_now()
+    if args.stock_ref and not args.stock_first and args.stock_between:
+        stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
+    if args.warmup > w1:
+        loss = run(w1, args.warmup - w1)
     sync()
     if world > 1:
         dist.barrier()
@@ -798,7 +814,7 @@ def main(argv=None):
     if args.digest and args.impl == "ddpx":
         from ddpx.runtime.flat_params import flat_of
         digest = allck[rank] if ddpx_ddp else replica_digest(None, flat=flat_of(model))
-    if args.stock_ref and not args.stock_first:
+    if args.stock_ref and not args.stock_first and not args.stock_between:
         stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0

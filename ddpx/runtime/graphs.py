@@ -432,9 +432,16 @@ class GraphedSteps:
         self.graphs = None
         self.graph_error = None
         self.warm = set()  # graph sizes replayed at least once
+        self._fresh = False
         import os
         # windows this long may replay a graph for the first time (DDPX_GRAPH_COLD_OK=1: any window, as before r5)
         self.cold_ok = int(os.environ.get("DDPX_GRAPH_COLD_OK", "100"))
+
+    def capture_now(self):
+        """Capture at once (after the eager steps; normally done lazily by run()): lets a caller put unrelated GPU
+        work between the capture and the replays that follow it."""
+        if self.use_graph and self.graphs is None:
+            self._capture()
 
     def _capture(self):
         ok, err, graphs = True, None, None
@@ -451,6 +458,7 @@ class GraphedSteps:
         all_ok = self.agree(ok) if self.agree is not None else ok
         if all_ok:
             self.graphs = graphs
+            self._fresh = True  # the next run() warms the largest graph that fits it
             return
         self.graphs = None
         self.use_graph = False
@@ -484,17 +492,16 @@ class GraphedSteps:
         """Steps k .. k+n-1; returns the last step's loss."""
         loss = None
         plan = None
-        captured = False
         while n > 0:
             if self.use_graph and k >= self.eager_first and self.graphs is None:
                 self._capture()
-                captured = True
             if not self.use_graph or k < self.eager_first:
                 loss = self.eager_step()
                 m = 1
             else:
                 if plan is None:
-                    plan = self.schedule(n, capture_run=captured)
+                    plan = self.schedule(n, capture_run=self._fresh)
+                    self._fresh = False
                 m = plan.pop(0) if plan else 1
                 loss = self.graphs[m]()
                 self.warm.add(m)
