@@ -390,6 +390,21 @@ __device__ __forceinline__ void lds_wait_ge(int* c, int target) {
   asm volatile("" ::: "memory");  // no LDS read of the slot moves above the poll
 }
 
+// s_waitcnt vmcnt(n) for a run-time n (the ring's tail), n <= 63
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  switch (n) {
+#define DDPX_VMC(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    DDPX_VMC(0) DDPX_VMC(1) DDPX_VMC(2) DDPX_VMC(3) DDPX_VMC(4) DDPX_VMC(5) DDPX_VMC(6) DDPX_VMC(7)
+    DDPX_VMC(8) DDPX_VMC(9) DDPX_VMC(10) DDPX_VMC(11) DDPX_VMC(12) DDPX_VMC(13) DDPX_VMC(14) DDPX_VMC(15)
+    DDPX_VMC(16) DDPX_VMC(17) DDPX_VMC(18) DDPX_VMC(19) DDPX_VMC(20) DDPX_VMC(21) DDPX_VMC(22) DDPX_VMC(23)
+    DDPX_VMC(24) DDPX_VMC(25) DDPX_VMC(26) DDPX_VMC(27) DDPX_VMC(28) DDPX_VMC(29) DDPX_VMC(30) DDPX_VMC(31)
+    DDPX_VMC(32) DDPX_VMC(33) DDPX_VMC(34) DDPX_VMC(35) DDPX_VMC(36) DDPX_VMC(37) DDPX_VMC(38) DDPX_VMC(39)
+    DDPX_VMC(40) DDPX_VMC(41) DDPX_VMC(42) DDPX_VMC(43) DDPX_VMC(44) DDPX_VMC(45) DDPX_VMC(46) DDPX_VMC(47)
+#undef DDPX_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 __device__ __forceinline__ void lds_signal(int* c, int lane) {
   asm volatile("" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -720,6 +735,9 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
       // ------------------------------------------------------------ loader waves
       const int lw = wave - NW;
       constexpr int LPL = (BM + BN) / (8 * LW);  // LDS-DMA instructions per loader wave per K-step
+      // K-steps kept in flight before one is published: STAGES - 2 (one slot of slack for the math waves)
+      constexpr int D = STAGES > 2 ? STAGES - 2 : 1;
+      static_assert(D * LPL <= 47, "vmcnt range");
       for (int t = 0; t < nk; ++t) {
         const int sl = t % STAGES;
         if (t >= STAGES) lds_wait_ge(ring_free + sl, (t / STAGES) * NW);  // every math wave read step t - STAGES
@@ -727,14 +745,14 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
         const int k0 = kbeg + t * 64;
         stage_tile<BM, AK, AMODE, LW>(ra, slot, p.conv, p.lda, m0, p.M, k0, kend, lw, lane);
         stage_tile<BN, BKc, BMODE, LW>(rb, slot + A_BYTES, p.conv, p.ldb, n0, p.N, k0, kend, lw, lane);
-        if (t >= 1) {  // this wave's share of step t - 1 has landed: publish it
-          wait_vmcnt<LPL>();
-          lds_signal(ring_full + (t - 1) % STAGES, lane);
+        if (t >= D) {  // this wave's share of step t - D has landed (D younger steps may still fly): publish it
+          wait_vmcnt<D * LPL>();
+          lds_signal(ring_full + (t - D) % STAGES, lane);
         }
       }
-      if (nk >= 1) {
-        wait_vmcnt<0>();
-        lds_signal(ring_full + (nk - 1) % STAGES, lane);
+      for (int j = nk > D ? nk - D : 0; j < nk; ++j) {  // the last D steps, oldest first
+        wait_vmcnt_rt((nk - 1 - j) * LPL);
+        lds_signal(ring_full + j % STAGES, lane);
       }
       return;
     }
