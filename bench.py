@@ -120,6 +120,10 @@ def parse(argv=None):
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="host: gloo-staged collectives so several ranks can share one GPU (logic rehearsal on a "
                         "1-GPU box; not graph-capturable, not a performance path)")
+    p.add_argument("--rccl_channels", default=None,
+                   help="RCCL channel (CTA) bounds of the gradient communicator: N or MIN:MAX (default: RCCL's "
+                        "choice, or DDPX_RCCL_CHANNELS); benchmarks/rccl_sweep.py measures the options")
+    p.add_argument("--rccl_proto", default=None, help="NCCL_PROTO for this job (Simple, LL, LL128; default RCCL's)")
     p.add_argument("--stock_ref", type=int, default=None,
                    help="1: also time the stock PyTorch recipe (torch.nn + torch DDP over RCCL at N > 1) in this "
                         "job, after the ddpx timing, on the same data (default 1)")
@@ -299,10 +303,13 @@ def make_comm(args, device, world):
     job, shared by the calibration trials and the timed run."""
     if not (world > 1 or args.ddp_single) or args.impl != "ddpx":
         return None
-    from ddpx.parallel.comm import HostStagedComm, RcclComm, TorchComm
+    from ddpx.parallel.comm import HostStagedComm, RcclComm, TorchComm, set_rccl_protocol
     if device.type == "cpu":
         return TorchComm()
-    return HostStagedComm() if args.comm == "host" else RcclComm(device)
+    if args.comm == "host":
+        return HostStagedComm()
+    set_rccl_protocol(args.rccl_proto)
+    return RcclComm(device, channels=args.rccl_channels)
 
 
 def build_ddpx(args, device, world, comm=None):
@@ -846,6 +853,8 @@ def main(argv=None):
                    "kernels": (args.kernels if args.impl == "ddpx" else None),
                    "launcher": os.environ.get(LAUNCHER_ENV, "torchrun/external" if world > 1 else "none"),
                    "comm": (args.comm if ddpx_ddp else None),
+                   "rccl": ({"channels": args.rccl_channels, "proto": os.environ.get("NCCL_PROTO")}
+                            if (ddpx_ddp and args.comm == "rccl") else None),
                    "graph": bool(runner is not None and runner.use_graph),
                    "graph_steps": (args.graph_steps if (runner is not None and runner.use_graph) else None),
                    "graph_schedule": (runner.schedule(args.steps) if (runner is not None and runner.use_graph)

@@ -253,8 +253,13 @@ DDPX_API int ddpx_comm_version() {
   return v;
 }
 
-DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int device, int high_priority,
-                                double timeout_s, int* err) {
+// min_ctas / max_ctas > 0: the communicator's channel (CTA) bounds through ncclCommInitRankConfig
+// (ncclConfig_t.minCTAs / maxCTAs, per communicator, unlike the process-wide NCCL_MIN/MAX_NCHANNELS).  On an
+// 8 x MI355X node each ring channel drives one xGMI link direction, so a bucket only reaches the 7-link
+// aggregate with >= 7 channels; more channels cost CUs taken from the overlapped backward GEMMs
+// (benchmarks/rccl_sweep.py measures the trade).
+DDPX_API void* ddpx_comm_create2(const char* uid, int nranks, int rank, int device, int high_priority,
+                                 double timeout_s, int min_ctas, int max_ctas, int* err) {
   *err = 0;
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
@@ -276,7 +281,15 @@ DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int devic
   }
   ncclUniqueId id;
   memcpy(&id, uid, sizeof(id));
-  int e = check(ncclCommInitRank(&c->nccl, nranks, id, rank));
+  int e;
+  if (min_ctas > 0 || max_ctas > 0) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (min_ctas > 0) cfg.minCTAs = min_ctas;
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    e = check(ncclCommInitRankConfig(&c->nccl, nranks, id, rank, &cfg));
+  } else {
+    e = check(ncclCommInitRank(&c->nccl, nranks, id, rank));
+  }
   if (e) {
     *err = e;
     hipStreamDestroy(c->stream);
@@ -293,6 +306,11 @@ DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int devic
   if (const char* g = getenv("DDPX_COMM_EXIT_GRACE_S")) c->exit_grace_s = atof(g);
   c->watchdog = std::thread(watchdog_loop, c);
   return c;
+}
+
+DDPX_API void* ddpx_comm_create(const char* uid, int nranks, int rank, int device, int high_priority,
+                                double timeout_s, int* err) {
+  return ddpx_comm_create2(uid, nranks, rank, device, high_priority, timeout_s, 0, 0, err);
 }
 
 // Track a graph replay (or any stream position): call right after hipGraphLaunch on `s`.
@@ -550,9 +568,11 @@ static int issue_bucket(Reducer* r, Bucket& b) {
     e = ddpx_comm_allreduce(c, b.ptr, b.ptr, b.count, b.dtype, r->op, c->stream);
   }
   if (e) return e;
+  // the timing marker goes BEFORE the completion event the consumers join: recorded after it, it would be a
+  // trailing node of the communicator stream that no stream waits for (an unjoined fork inside a captured step)
+  hipEventRecord(r->t_last, c->stream);
   he = hipEventRecord(b.done, c->stream);
   if (he != hipSuccess) return (int)he;
-  hipEventRecord(r->t_last, c->stream);
   r->timed = true;
   r->launched++;
   return 0;

@@ -492,6 +492,15 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
   *comm = reinterpret_cast<ncclComm_t>(c);
   return ncclSuccess;
 }
+
+// channel bounds are a performance setting: the fake world checks them and otherwise ignores them
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks, ncclUniqueId id, int rank, ncclConfig_t* config) {
+  if (config && config->minCTAs > 0 && config->maxCTAs > 0 && config->minCTAs > config->maxCTAs) {
+    violation("ncclCommInitRankConfig: minCTAs > maxCTAs");
+    return ncclInvalidArgument;
+  }
+  return ncclCommInitRank(comm, nranks, id, rank);
+}
 static ncclResult_t release_comm(ncclComm_t comm, const char* what) {
   FakeComm* c = reinterpret_cast<FakeComm*>(comm);
   if (!c->alive.exchange(false)) {

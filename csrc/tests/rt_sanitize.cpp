@@ -127,6 +127,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* c, int, ncclUniqueId, int) {
   *c = reinterpret_cast<ncclComm_t>(g_comms.back().get());
   return ncclSuccess;
 }
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* c, int n, ncclUniqueId id, int r, ncclConfig_t*) {
+  return ncclCommInitRank(c, n, id, r);
+}
 ncclResult_t ncclCommAbort(ncclComm_t comm) {
   FakeComm* c = reinterpret_cast<FakeComm*>(comm);
   if (c->in_flight.load()) violation("ncclCommAbort while a collective is being enqueued");

@@ -193,12 +193,39 @@ class _ScaleOnWait:
         self.t.mul_(self.s)
 
 
+def parse_channels(spec):
+    """None / "" / 0 -> None; N or "N" -> (N, N); (a, b) or "a:b" -> (a, b) (0 = RCCL's bound)."""
+    if spec is None or spec == "" or spec == 0:
+        return None
+    if isinstance(spec, str):
+        parts = [int(v) for v in spec.split(":")]
+        spec = parts[0] if len(parts) == 1 else tuple(parts)
+    if isinstance(spec, int):
+        spec = (spec, spec)
+    lo, hi = (int(spec[0]), int(spec[1]))
+    if lo < 0 or hi < 0 or (hi and lo > hi):
+        raise ValueError(f"bad RCCL channel bounds {spec!r}")
+    return (lo, hi) if (lo or hi) else None
+
+
+def set_rccl_protocol(proto):
+    """RCCL reads ``NCCL_PROTO`` once per process (Simple | LL | LL128, or a comma list): set it before the first
+    communicator.  None leaves RCCL's own per-size choice."""
+    if proto:
+        os.environ["NCCL_PROTO"] = str(proto)
+
+
 class RcclComm(Comm):
     """Native RCCL communicator for one process per MI355X."""
 
-    def __init__(self, device: torch.device, timeout_s: float | None = None, high_priority: bool = True):
+    def __init__(self, device: torch.device, timeout_s: float | None = None, high_priority: bool = True,
+                 channels=None):
+        """``channels``: None (RCCL's choice), N, or (min, max) channel / CTA bounds for THIS communicator
+        (``ncclConfig_t.minCTAs/maxCTAs``); default from ``DDPX_RCCL_CHANNELS`` ("N" or "MIN:MAX").  The
+        protocol is process-wide in RCCL: set ``NCCL_PROTO`` (``--rccl_proto``) before the first communicator."""
         if not dist.is_initialized():
             raise RuntimeError("RcclComm bootstraps through the default c10d store: init_process_group first")
+        self.channels = parse_channels(os.environ.get("DDPX_RCCL_CHANNELS") if channels is None else channels)
         rt = native.runtime()
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
@@ -215,8 +242,9 @@ class RcclComm(Comm):
             timeout_s = float(os.environ.get("DDPX_COMM_TIMEOUT", "600"))
         err = native.ctypes.c_int(0)
         torch.cuda.set_device(self.device)
-        self.handle = rt.ddpx_comm_create(uid, self.world_size, self.rank, self.device.index or 0,
-                                          int(high_priority), float(timeout_s), native.ctypes.byref(err))
+        lo, hi = self.channels or (0, 0)
+        self.handle = rt.ddpx_comm_create2(uid, self.world_size, self.rank, self.device.index or 0,
+                                           int(high_priority), float(timeout_s), lo, hi, native.ctypes.byref(err))
         if not self.handle:
             raise RuntimeError(f"ncclCommInitRank failed (code {err.value})")
         self._rt = rt

@@ -15,6 +15,7 @@ Rules this relies on (all ddpx ops follow them):
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -190,10 +191,13 @@ def capture_step(graph, fn):
             raise
         try:
             # a side stream the body forked and never joined back would make the end fail AND leave both
-            # streams capturing for good (ROCm 7: a second end is refused, WrongThread): join it first
+            # streams capturing for good (ROCm 7: a second end is refused, WrongThread): join every side stream
+            # that took part first.  HIP reports a side stream as part of the capture whether or not its last
+            # nodes were already joined, so this cannot tell a missing join from a done one (an extra edge to
+            # already-joined nodes is free); DDPX_CAPTURE_DEBUG=1 names the streams.
             late = _join_into(cap, stream_capture_info(cap)[1])
-            if late:
-                _warn_once(f"capture_step: joined side stream(s) the captured body left forked: {late}")
+            if late and os.environ.get("DDPX_CAPTURE_DEBUG", "0") == "1":
+                _warn_once(f"capture_step: joined side stream(s) that took part in the capture: {late}")
             graph.capture_end()
         except BaseException:
             _abort_capture(graph, cap)

@@ -109,6 +109,7 @@ def _declare_rt(lib):
     _sig(lib, "ddpx_comm_unique_id", I, ctypes.c_char * 128, I)
     _sig(lib, "ddpx_comm_version", I)
     _sig(lib, "ddpx_comm_create", P, c_char_p, I, I, I, I, D, ctypes.POINTER(c_int))
+    _sig(lib, "ddpx_comm_create2", P, c_char_p, I, I, I, I, D, I, I, ctypes.POINTER(c_int))
     _sig(lib, "ddpx_comm_stream", P, P)
     _sig(lib, "ddpx_comm_renew_stream", I, P)
     _sig(lib, "ddpx_comm_error", I, P)

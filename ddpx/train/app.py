@@ -23,7 +23,7 @@ from ..data.sampler import DistributedIndexSampler
 from ..models import build_model
 from ..optim.schedule import one_cycle, resolve_steps_per_epoch
 from ..optim.sgd import SGD
-from ..parallel.comm import HostStagedComm, RcclComm, TorchComm
+from ..parallel.comm import HostStagedComm, RcclComm, TorchComm, set_rccl_protocol
 from ..parallel.sync_bn import convert_sync_batchnorm
 from ..parallel.ddp import DistributedDataParallel
 from ..runtime.setup import prepare_model
@@ -79,6 +79,9 @@ def build_parser(description: str) -> argparse.ArgumentParser:
                    help="single GPU: run SGD as its own pass instead of inside the backward kernels")
     p.add_argument("--comm", default="rccl", choices=["rccl", "torch", "host"],
                    help="GPU collective backend (host: gloo-staged, lets several ranks share one GPU)")
+    p.add_argument("--rccl_channels", default=None,
+                   help="RCCL channel (CTA) bounds of the gradient communicator: N or MIN:MAX (default RCCL's)")
+    p.add_argument("--rccl_proto", default=None, help="NCCL_PROTO for this job (Simple, LL, LL128)")
     p.add_argument("--shard_optimizer", action="store_true",
                    help="ZeRO-1: reduce-scatter grads, each rank updates its shard, all-gather params")
     p.add_argument("--chunk_mb", type=float, default=None,
@@ -380,7 +383,8 @@ def run(args, rank: int = 0, world_size: int = 1, local_rank: int = 0, distribut
     comm = None
     if distributed:
         if device.type == "cuda" and args.comm == "rccl":
-            comm = RcclComm(device)
+            set_rccl_protocol(getattr(args, "rccl_proto", None))
+            comm = RcclComm(device, channels=getattr(args, "rccl_channels", None))
         elif device.type == "cuda" and args.comm == "host":
             comm = HostStagedComm()
         else:

@@ -61,8 +61,12 @@ def test_failed_capture_leaves_no_stream_capturing(gpu, mode):
     g = torch.cuda.CUDAGraph()
     try:
         if mode == "unjoined":  # joined back before the end (a failed unjoined end cannot be repaired on ROCm 7)
-            with pytest.warns(RuntimeWarning, match="left forked"):
-                capture_step(g, body)
+            os.environ["DDPX_CAPTURE_DEBUG"] = "1"
+            try:
+                with pytest.warns(RuntimeWarning, match="took part in the capture"):
+                    capture_step(g, body)
+            finally:
+                os.environ.pop("DDPX_CAPTURE_DEBUG", None)
             g.replay()
             torch.cuda.synchronize()
             assert float(x[0]) == 2.0
@@ -91,14 +95,14 @@ def test_failed_capture_leaves_no_stream_capturing(gpu, mode):
         unregister_side_stream("test side stream")
 
 
-def _bench_engine(gpu, inject, monkeypatch):
+def _bench_engine(gpu, inject, monkeypatch, shard=1):
     import bench
     from ddpx.parallel.ddp import DistributedDataParallel
-    args = bench.parse(["--gpus", "1", "--ddp_single", "--shard_optimizer", "1", "--bucket_plan", "default",
+    args = bench.parse(["--gpus", "1", "--ddp_single", "--shard_optimizer", str(shard), "--bucket_plan", "default",
                         "--steps", "6", "--warmup", "0", "--train_size", "4096", "--graph_steps", "1"])
     bench.resolve_defaults(args, 1)
-    # the round-4 failing configuration
-    assert args.shard_optimizer and args.comm_side_optimizer and args.defer_gather and args.overlap_optimizer
+    if shard:  # the round-4 failing configuration
+        assert args.shard_optimizer and args.comm_side_optimizer and args.defer_gather and args.overlap_optimizer
     loader = bench.make_data(args, gpu, 0, 1)
     idx_all = loader._epoch_indices()
     full = [i for i in range(len(loader)) if (i + 1) * args.batch_size <= idx_all.numel()]
@@ -119,16 +123,20 @@ def _bench_engine(gpu, inject, monkeypatch):
     return eng, comm, hits
 
 
-@pytest.mark.parametrize("inject", [False, True])
-def test_zero1_comm_side_defer_trial_teardown_then_h2d(gpu, pg, inject, monkeypatch):
+@pytest.mark.parametrize("inject,shard", [(False, 1), (True, 1), (False, 0)])
+def test_zero1_comm_side_defer_trial_teardown_then_h2d(gpu, pg, inject, shard, monkeypatch):
+    import warnings
     from ddpx.models import build_model
     from ddpx.runtime.flat_params import flat_of
     from ddpx.runtime.graphs import assert_no_capture
     from ddpx.runtime.setup import prepare_model
-    eng, comm, hits = _bench_engine(gpu, inject, monkeypatch)
+    eng, comm, hits = _bench_engine(gpu, inject, monkeypatch, shard)
     try:
-        eng.run(0, 3)  # two eager steps, then the capture (+ one replay, or the eager fallback)
-        torch.cuda.synchronize()
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            eng.run(0, 3)  # two eager steps, then the capture (+ one replay, or the eager fallback)
+            torch.cuda.synchronize()
+        assert not [w for w in caught if "capture_step" in str(w.message)]
         if inject:
             assert hits["n"] == 1
             assert not eng.runner.use_graph and "injected" in eng.runner.graph_error

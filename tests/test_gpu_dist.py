@@ -24,9 +24,10 @@ def pg(gpu):
     dist.destroy_process_group()
 
 
-def test_rccl_collectives(gpu, pg):
+@pytest.mark.parametrize("channels", [None, "2:8", 16])
+def test_rccl_collectives(gpu, pg, channels):
     from ddpx.parallel.comm import RcclComm
-    c = RcclComm(gpu)
+    c = RcclComm(gpu, channels=channels)  # explicit bounds: ncclCommInitRankConfig (minCTAs / maxCTAs)
     x = torch.randn(1000, device=gpu)
     y = x.clone()
     c.allreduce_(y, "avg")
