@@ -1,0 +1,314 @@
+// ddpx — fp32 Winograd F(2x2, 3x3) convolutions for the 3x3 / stride 1 / pad 1 layers of the reference's VGG at
+// its own precision (/root/reference/singlegpu.py:60-70 conv blocks, :134 fp32 model).
+//
+// The stock fp32 recipe's forward and data-gradient convolutions are MIOpen's Winograd F(2,3) kernels
+// (profiles/r4_f32: 2.25x fewer multiplies than the direct 3x3 product); this is the same algorithm on CDNA4
+// directly, with the whole transform pipeline inside one GEMM launch:
+//
+//   Y = A^T [ sum_ci (G g G^T)[co,ci] (.) (B^T d B)[tile,ci] ] A        (per 2x2 output tile, 4x4 input patch)
+//
+//   * weights: U[xi][ci][co] = (G g G^T)[xi] once per step (wino_wprep_kernel; the data gradient's U is made
+//     from the flipped, transposed kernel: the transposed 3x3/s1/p1 convolution is a convolution);
+//   * one workgroup = 64 output tiles (256 pixels) x 32 output channels x all 16 transform positions xi:
+//     16 independent 16x16x4 f32 MFMA chains per wave (v_mfma_f32_16x16x4_f32: f32 in, f32 accumulate);
+//   * input patches (4x4 pixels x 4 channels per tile per K-step) go global -> LDS by LDS-DMA with the zero
+//     padding from buffer bounds (an out-of-image pixel reads as 0); each wave fetches the patches of ITS OWN
+//     16 tiles, so only the shared U slab needs the per-K-step barrier;
+//   * the input transform B^T d B runs on the lane that feeds the MFMA: lane l = (channel l/16, tile l%16) is
+//     exactly the A-fragment slot (row l%16, k l/16) of v_mfma_f32_16x16x4_f32, so V never touches LDS;
+//   * the output transform A^T M A runs in the epilogue on the accumulators (each lane holds all 16 xi of its
+//     4 tiles x 2 channels), writes the 2x2 pixels, and (forward) the BatchNorm tile statistics (mean, M2 per
+//     channel over the workgroup's 256 pixels; merged by the existing Chan finalize).
+// Requirements: C % 4 == 0, K % 32 == 0, H and W even (every VGG layer on CIFAR-10).
+#include "ddpx_common.h"
+
+namespace ddpx {
+namespace wino {
+
+constexpr int NT = 256;                  // 4 waves
+constexpr int TP = 64;                   // output tiles per workgroup (16 per wave)
+constexpr int TK = 32;                   // output channels per workgroup
+constexpr int RAW_BYTES = TP * 16 * 16;  // 64 tiles x 16 pixels x 4 channels x 4 B = 16 KiB
+constexpr int U_BYTES = 16 * 4 * TK * 4; // 16 xi x 4 channels x 32 out channels x 4 B = 8 KiB
+constexpr int SLOT = RAW_BYTES + U_BYTES;
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+// y (+ stats) = conv3x3(x) through F(2,3).  x: NHWC [N][H][W][C]; U: [16][C][K]; y: [N*H*W][K].
+template <int STAGES>
+__global__ void __launch_bounds__(NT, 2)  // 2 waves per SIMD: <= 256 VGPR + AGPR (128 are accumulators)
+wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
+                float* __restrict__ stats, int N, int H, int W, int C, int K, int tiles_p, unsigned x_bytes,
+                unsigned u_bytes) {
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // consecutive ids (one XCD's share) walk the tiles inside one output-channel block: its U slab stays in L2
+  const int pb = bid % tiles_p, kb = bid / tiles_p;
+  const int TH = H >> 1, TW = W >> 1, P = N * TH * TW;
+  const int k0 = kb * TK;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc((void*)U, 0, u_bytes, 0x00020000);
+
+  // patch DMA: instruction j = patch row dy, lane l = (patch column dx = l >> 4, tile l & 15 of this wave);
+  // LDS image per wave [dy*4+dx][tile][4 ch] (16 B chunks): the transform's reads are conflict-free
+  unsigned poff[4];
+  {
+    const int t = lane & 15, dx = lane >> 4;
+    const int p = pb * TP + wave * 16 + t;
+    const int pp = p < P ? p : 0;
+    const int n = pp / (TH * TW), r = pp - n * (TH * TW);
+    const int th = r / TW, tw = r - th * TW;
+    const int w = 2 * tw + dx - 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = 2 * th + j - 1;
+      const bool ok = p < P && h >= 0 && h < H && w >= 0 && w < W;
+      poff[j] = ok ? (unsigned)((((size_t)n * H + h) * W + w) * C * 4) : kOOB;
+    }
+  }
+  // U slab DMA: 8 wave-instructions per K-step, 2 per wave; chunk q = row (xi*4 + ci) * 8 + 16-B column
+  unsigned uoff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = (j * 4 + wave) * 64 + lane;
+    const int row = q >> 3, ch = q & 7;
+    const int xi = row >> 2, ci = row & 3;
+    uoff[j] = (unsigned)((((size_t)xi * C + ci) * K + k0 + ch * 4) * 4);
+  }
+  const int nk = C >> 2;
+  auto issue = [&](int t) {
+    char* slot = smem + (t % STAGES) * SLOT;
+    const unsigned cx = (unsigned)(t * 16);  // 4 channels = 16 B further along every pixel
+    char* raw = slot + wave * (RAW_BYTES / 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(rx, raw + j * 1024, poff[j] == kOOB ? kOOB : poff[j] + cx);
+    const unsigned cu = (unsigned)((size_t)t * 4 * K * 4);  // 4 channels = 4 rows of K further
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(ru, slot + RAW_BYTES + (j * 4 + wave) * 1024, uoff[j] + cu);
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+  constexpr int PER_STEP = 6;  // DMA instructions per wave per K-step
+  const int ci = lane >> 4, tl = lane & 15;
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(STAGES - 2, nk - 1 - t);
+    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    const char* slot = smem + (t % STAGES) * SLOT;
+    const float* raw = reinterpret_cast<const float*>(slot + wave * (RAW_BYTES / 4));
+    const float* us = reinterpret_cast<const float*>(slot + RAW_BYTES);
+    float d[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = raw[(q * 16 + tl) * 4 + ci];
+    float b[16][2];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      b[q][0] = us[(q * 4 + ci) * TK + tl];
+      b[q][1] = us[(q * 4 + ci) * TK + 16 + tl];
+    }
+    // V = B^T d B, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
+    float tmp[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      tmp[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
+      tmp[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
+      tmp[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
+      tmp[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+    }
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r * 4 + 0] = tmp[r * 4 + 0] - tmp[r * 4 + 2];
+      v[r * 4 + 1] = tmp[r * 4 + 1] + tmp[r * 4 + 2];
+      v[r * 4 + 2] = tmp[r * 4 + 2] - tmp[r * 4 + 1];
+      v[r * 4 + 3] = tmp[r * 4 + 1] - tmp[r * 4 + 3];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc[q][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q][0], acc[q][0], 0, 0, 0);
+      acc[q][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q][1], acc[q][1], 0, 0, 0);
+    }
+  }
+
+  // epilogue: Y = A^T M A per (tile, channel), A^T = [[1,1,1,0],[0,1,-1,-1]]
+  const int lr = lane >> 4;
+  float out[4][2][4];  // [e (tile row of the fragment)][j (channel fragment)][pixel 2x2]
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float m[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) m[q] = acc[q][j][e];
+      float t0[4], t1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t0[c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
+        t1[c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
+      }
+      out[e][j][0] = t0[0] + t0[1] + t0[2];
+      out[e][j][1] = t0[1] - t0[2] - t0[3];
+      out[e][j][2] = t1[0] + t1[1] + t1[2];
+      out[e][j][3] = t1[1] - t1[2] - t1[3];
+    }
+  bool valid[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int p = pb * TP + wave * 16 + lr * 4 + e;
+    valid[e] = p < P;
+    if (!valid[e]) continue;
+    const int n = p / (TH * TW), r = p - n * (TH * TW);
+    const int th = r / TW, tw = r - th * TW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const size_t pix = ((size_t)n * H + 2 * th + i) * W + 2 * tw + jj;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) y[pix * K + k0 + 16 * j + tl] = out[e][j][i * 2 + jj];
+      }
+  }
+  if (!stats) return;
+  // BatchNorm chunk statistics over this workgroup's pixels (chunk = 256 rows; the last chunk may be short):
+  // per channel, lanes sharing it (xor 16, 32), then the 4 waves in order through LDS; two passes (mean, M2)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the ring: reuse it
+  float* red = reinterpret_cast<float*>(smem);  // [4 waves][32 channels] sums, then [4][32] M2
+  const int rows = min(TP, P - pb * TP) * 4;
+  float mean[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (valid[e]) s += (out[e][j][0] + out[e][j][1]) + (out[e][j][2] + out[e][j][3]);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lr == 0) red[wave * TK + 16 * j + tl] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = 16 * j + tl;
+    mean[j] = (((red[col] + red[TK + col]) + red[2 * TK + col]) + red[3 * TK + col]) / (float)rows;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (valid[e])
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float dv = out[e][j][u] - mean[j];
+          q = fmaf(dv, dv, q);
+        }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    if (lr == 0) red[wave * TK + 16 * j + tl] = q;
+  }
+  __syncthreads();
+  if (wave == 0 && lr == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = 16 * j + tl;
+      stats[(size_t)pb * 2 * K + k0 + col] = mean[j];
+      stats[(size_t)pb * 2 * K + K + k0 + col] = ((red[col] + red[TK + col]) + red[2 * TK + col]) + red[3 * TK + col];
+    }
+  }
+}
+
+// U = G g G^T per (co, ci), G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]].  w: torch [Co][Ci][3][3].
+//   uf: [16][Cp][Co] (forward, channels Ci padded to Cp with zero kernels), ud: [16][Co][Ci] (data gradient:
+//   the kernel flipped in both taps, input and output channels swapped), either may be null.
+__device__ __forceinline__ void g_transform(const float (&g)[9], float (&u)[16]) {
+  float t[4][3];  // G g
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    t[0][s] = g[0 * 3 + s];
+    t[1][s] = 0.5f * ((g[0 * 3 + s] + g[1 * 3 + s]) + g[2 * 3 + s]);
+    t[2][s] = 0.5f * ((g[0 * 3 + s] - g[1 * 3 + s]) + g[2 * 3 + s]);
+    t[3][s] = g[2 * 3 + s];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    u[r * 4 + 0] = t[r][0];
+    u[r * 4 + 1] = 0.5f * ((t[r][0] + t[r][1]) + t[r][2]);
+    u[r * 4 + 2] = 0.5f * ((t[r][0] - t[r][1]) + t[r][2]);
+    u[r * 4 + 3] = t[r][2];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+wino_wprep_kernel(const float* __restrict__ w, int Co, int Ci, int Cp, float* __restrict__ uf, float* __restrict__ ud) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;  // co fastest: coalesced uf stores
+  if (idx >= Co * Cp) return;
+  const int co = idx % Co, ci = idx / Co;
+  float g[9];
+  const bool real = ci < Ci;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) g[q] = real ? w[((size_t)co * Ci + ci) * 9 + q] : 0.f;
+  float u[16];
+  if (uf) {
+    g_transform(g, u);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) uf[((size_t)q * Cp + ci) * Co + co] = u[q];
+  }
+  if (ud && real) {
+    float gf[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) gf[q] = g[8 - q];
+    g_transform(gf, u);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ud[((size_t)q * Co + co) * Ci + ci] = u[q];
+  }
+}
+
+}  // namespace wino
+}  // namespace ddpx
+
+using namespace ddpx;
+
+// Winograd applies: 3x3 / s1 / p1, C % 4 == 0, K % 32 == 0, H and W even.
+DDPX_API int ddpx_f32_wino_ok(int H, int W, int C, int K) {
+  return (C >= 4 && C % 4 == 0 && K % 32 == 0 && H >= 2 && W >= 2 && H % 2 == 0 && W % 2 == 0) ? 1 : 0;
+}
+
+DDPX_API int ddpx_f32_wino_wprep(const float* w, int Co, int Ci, int Cp, float* uf, float* ud, hipStream_t s) {
+  if (Cp < Ci) return -2;
+  const int n = Co * Cp;
+  hipLaunchKernelGGL(wino::wino_wprep_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, Co, Ci, Cp, uf, ud);
+  return -(int)hipGetLastError();
+}
+
+// y [N*H*W][K] = conv3x3(x [N][H][W][C]) with U [16][C][K]; stats (nullable): [tiles_p][2][K] chunk statistics of
+// 256-pixel chunks.  Returns the statistics chunk rows (256) or a negative error.
+DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float* stats, int N, int H, int W, int C,
+                                int K, hipStream_t s) {
+  if (!ddpx_f32_wino_ok(H, W, C, K)) return -2;
+  const size_t xb = (size_t)N * H * W * C * 4, ub = (size_t)16 * C * K * 4;
+  if (xb >= 0x80000000ull || ub >= 0x80000000ull) return -3;  // 32-bit buffer offsets, top bit = out of bounds
+  const int P = N * (H / 2) * (W / 2);
+  const int tiles_p = (P + wino::TP - 1) / wino::TP;
+  const int nwg = tiles_p * (K / wino::TK);
+  hipLaunchKernelGGL((wino::wino_f32_kernel<3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
+                     tiles_p, (unsigned)xb, (unsigned)ub);
+  const int e = (int)hipGetLastError();
+  return e ? -e : 4 * wino::TP;
+}

@@ -41,6 +41,9 @@ for _sig in (
         ("ddpx_f32_conv_fwd_stats", _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
+        ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
+        ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
+        ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P),
 ):
     native.register_kernel_sig(*_sig)
 
@@ -225,6 +228,44 @@ def conv_dgrad(dy, wd, N, H, W, C, Co):
     return dx
 
 
+# ------------------------------------------------------------------ Winograd F(2x2, 3x3) (csrc/kernels/f32_wino.hip)
+# The forward and data-gradient 3x3 convolutions of the VGG layers with >= DDPX_F32_WINO_MIN_C input channels
+# (default 64: every layer but the 3-channel image one) run as fp32 Winograd F(2,3), MIOpen's algorithm for the
+# stock fp32 recipe, with 2.25x fewer multiplies than the exact implicit GEMM.  DDPX_F32_WINO=0: the direct
+# implicit GEMM everywhere (the weight gradient always is).
+import os as _os  # noqa: E402
+
+_WINO = _os.environ.get("DDPX_F32_WINO", "1") != "0"
+_WINO_MIN_C = int(_os.environ.get("DDPX_F32_WINO_MIN_C", "64"))
+
+
+def wino_applies(H, W, C, K) -> bool:
+    return _WINO and C >= _WINO_MIN_C and bool(native.kernels().ddpx_f32_wino_ok(H, W, C, K))
+
+
+def wino_wprep(w, uf, ud):
+    """uf [16][Cp][Co] (forward) and ud [16][Co][Ci] (data gradient, flipped kernel) = G g G^T of w [Co,Ci,3,3]."""
+    Co, Ci = w.shape[:2]
+    Cp = conv_channels(Ci)
+    _req(uf is None or uf.numel() == 16 * Cp * Co, "wino_wprep: bad forward buffer")
+    _req(ud is None or ud.numel() == 16 * Co * Ci, "wino_wprep: bad data-gradient buffer")
+    _call("ddpx_f32_wino_wprep", w.data_ptr(), Co, Ci, Cp, native.ptr(uf), native.ptr(ud))
+
+
+def wino_conv(x, u, K, stats=False):
+    """y [N*H*W, K] = conv3x3(x [N,H,W,C]) through F(2,3) with u [16][C][K]; with ``stats``: (y, (part, T, 256)),
+    the BatchNorm chunk statistics of every 256-pixel output chunk from the epilogue."""
+    N, H, W, C = x.shape
+    _f32(x, "x")
+    y = torch.empty((N * H * W, K), dtype=torch.float32, device=x.device)
+    T = (N * (H // 2) * (W // 2) + 63) // 64
+    st = torch.empty((T, 2, K), dtype=torch.float32, device=x.device) if stats else None
+    r = native.kernels().ddpx_f32_wino_conv(x.data_ptr(), u.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, K,
+                                             native.stream_handle())
+    native.check(r if r < 0 else 0, "ddpx_f32_wino_conv")
+    return (y, (st, T, r)) if stats else y
+
+
 def wgrad_splits(Co, Ncols, P):
     tiles = ((Co + 127) // 128) * ((Ncols + 127) // 128)
     s = max(1, min(P // 1024, (2048 + tiles - 1) // tiles))
@@ -337,11 +378,21 @@ class _VGGPlan:
     def __init__(self, model):
         self.blocks = _blocks_of(model)
         dev = model.classifier.weight.device
-        self.wf, self.wd = [], []
-        for conv, _, _ in self.blocks:
+        self.wf, self.wd, self.uf, self.ud = [], [], [], []
+        H = 32  # CIFAR-10: the pools halve it after blocks 1, 3, 5, 7
+        for bi, (conv, _, pool) in enumerate(self.blocks):
             Co, Ci = conv.weight.shape[:2]
-            self.wf.append(torch.empty(9 * conv_channels(Ci) * Co, dtype=torch.float32, device=dev))
-            self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev) if Ci % 4 == 0 else None)
+            Cp = conv_channels(Ci)
+            # Winograd for the forward (and, below the first block, the data gradient) where it applies; the
+            # direct layouts only where it does not
+            wino = dev.type == "cuda" and wino_applies(H, H, Cp, Co) and (bi == 0 or Ci % 32 == 0)
+            self.uf.append(torch.empty(16 * Cp * Co, dtype=torch.float32, device=dev) if wino else None)
+            self.ud.append(torch.empty(16 * Co * Ci, dtype=torch.float32, device=dev) if wino and bi > 0 else None)
+            self.wf.append(torch.empty(9 * Cp * Co, dtype=torch.float32, device=dev) if not wino else None)
+            self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev)
+                           if (not wino and Ci % 4 == 0) else None)
+            if pool:
+                H //= 2
 
 
 def _blocks_of(model):
@@ -390,11 +441,22 @@ def _vgg_forward(model, x, targets, training):
     N, H, W, C = x.shape
     for bi, (conv, bn, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
-        conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
-        if training:
-            y, st = conv_fwd_stats(x, plan.wf[bi], Co)
+        if plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co):
+            wino_wprep(conv.weight, plan.uf[bi], plan.ud[bi])
+            if training:
+                y, st = wino_conv(x, plan.uf[bi], Co, stats=True)
+            else:
+                y, st = wino_conv(x, plan.uf[bi], Co), None
         else:
-            y, st = conv_fwd(x, plan.wf[bi], Co), None
+            if plan.wf[bi] is None:  # planned for Winograd at another input size: direct layouts on demand
+                plan.wf[bi] = torch.empty(9 * C * Co, dtype=torch.float32, device=x.device)
+                plan.wd[bi] = torch.empty(9 * Co * conv.weight.shape[1], dtype=torch.float32, device=x.device)
+                plan.ud[bi] = None
+            conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
+            if training:
+                y, st = conv_fwd_stats(x, plan.wf[bi], Co)
+            else:
+                y, st = conv_fwd(x, plan.wf[bi], Co), None
         xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool, stats=st, comm=comm)
         saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
         x = xn
@@ -427,7 +489,10 @@ def _vgg_backward(model, saved, last, dl, grad_out):
         flat.grad_done(bn.bias)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
-            g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            if plan.ud[bi] is not None and wino_applies(H, W, Co, C):
+                g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
+            else:
+                g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
 
 
 class _VGGLossF32(torch.autograd.Function):

@@ -268,7 +268,7 @@ def _err_vs_fp64(out, ref):
     return {"rel_l2": ((out - ref).norm() / ref.norm()).item(), "max_abs": (out - ref).abs().max().item()}
 
 
-@pytest.mark.parametrize("case", ["fc1", "conv7", "conv4"])
+@pytest.mark.parametrize("case", ["fc1", "conv7", "conv4", "conv7_wino", "conv4_wino", "conv1_wino"])
 def test_error_no_worse_than_stock(gpu, case):
     """The accuracy bar of the native fp32 kernels is the stock fp32 libraries' own error against fp64
     (hipBLASLt for the MLP's fc1, MIOpen for VGG's conv7 / conv4), measured here on the same inputs: the
@@ -284,7 +284,8 @@ def test_error_no_worse_than_stock(gpu, case):
         stock = x @ w.t()
         ours = f32.linear_fwd(x, w)
     else:
-        N, H, Ci, Co = (512, 4, 512, 512) if case == "conv7" else (512, 8, 256, 512)
+        N, H, Ci, Co = {"conv7": (512, 4, 512, 512), "conv4": (512, 8, 256, 512),
+                        "conv1": (128, 32, 64, 128)}[case.split("_")[0]]
         x = torch.relu(torch.randn(N, Ci, H, H, device=gpu))
         w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
         cols = F.unfold(x.double(), 3, padding=1)                      # [N, Ci*9, H*W]
@@ -292,9 +293,14 @@ def test_error_no_worse_than_stock(gpu, case):
         stock = F.conv2d(x, w, padding=1)
         Cp = f32.conv_channels(Ci)
         xn = F.pad(x.permute(0, 2, 3, 1), (0, Cp - Ci)).contiguous()
-        wf = torch.empty(9 * Cp * Co, device=gpu)
-        f32.conv_wprep(w, wf, None)
-        ours = f32.conv_fwd(xn, wf, Co).view(N, H, H, Co).permute(0, 3, 1, 2)
+        if case.endswith("_wino"):  # the Winograd F(2,3) forward (MIOpen's algorithm for the stock fp32 recipe)
+            uf = torch.empty(16 * Cp * Co, device=gpu)
+            f32.wino_wprep(w, uf, None)
+            ours = f32.wino_conv(xn, uf, Co).view(N, H, H, Co).permute(0, 3, 1, 2)
+        else:
+            wf = torch.empty(9 * Cp * Co, device=gpu)
+            f32.conv_wprep(w, wf, None)
+            ours = f32.conv_fwd(xn, wf, Co).view(N, H, H, Co).permute(0, 3, 1, 2)
         ref, stock = ref.permute(0, 2, 3, 1), stock.permute(0, 2, 3, 1)
         ours = ours.permute(0, 2, 3, 1)
     e_stock, e_ours = _err_vs_fp64(stock, ref), _err_vs_fp64(ours, ref)
@@ -566,3 +572,48 @@ def test_native_fp32_sync_batchnorm_matches_doubled_batch(gpu):
         if not e < (1e-5 if top else 5e-3):  # pooling-decision flips below bn7 (test above)
             bad.append((n, e))
     assert not bad, bad
+
+
+# ---------------------------------------------------------------------------------------------- Winograd F(2,3)
+@pytest.mark.parametrize("shape", [(4, 32, 64, 128), (3, 8, 256, 64), (5, 4, 512, 32), (2, 2, 4, 32), (7, 16, 128, 96)])
+def test_wino_conv_forward_dgrad_stats_match_fp64(gpu, shape):
+    """Winograd F(2x2,3x3) forward (with the BatchNorm chunk statistics) and data gradient against fp64, on shapes
+    with a partial last workgroup (P % 64 != 0) and output channels that are not a power of two."""
+    from ddpx.ops import f32
+    torch.manual_seed(5)
+    N, H, Ci, Co = shape
+    x = torch.randn(N, Ci, H, H, device=gpu)
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    uf = torch.empty(16 * Ci * Co, device=gpu)
+    ud = torch.empty(16 * Co * Ci, device=gpu)
+    f32.wino_wprep(w, uf, ud)
+    y, (st, T, R) = f32.wino_conv(xn, uf, Co, stats=True)
+    ref = F.conv2d(x.double(), w.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _err_vs_fp64(y, ref)["rel_l2"] < 1e-5
+    # chunk statistics: R-row chunks of the pixels in (tile, 2x2) order; their Chan merge is the batch's
+    assert R == 256 and T == (N * (H // 2) * (H // 2) + 63) // 64
+    P = N * H * H
+    cnt = torch.tensor([min(R, P - t * R) for t in range(T)], device=gpu, dtype=torch.float64)
+    mean = (st[:, 0].double() * cnt[:, None]).sum(0) / P
+    m2 = (st[:, 1].double() + cnt[:, None] * (st[:, 0].double() - mean) ** 2).sum(0)
+    assert torch.allclose(mean, ref.mean(0), rtol=1e-4, atol=1e-5)
+    assert torch.allclose(m2 / P, ref.var(0, unbiased=False), rtol=1e-4, atol=1e-6)
+    if Co % 32 == 0 and Ci % 32 == 0 and Co >= 4:
+        dy = torch.randn(N, H, H, Co, device=gpu)
+        dx = f32.wino_conv(dy, ud, Ci).view(N, H, H, Ci)
+        xr = x.double().requires_grad_(True)
+        F.conv2d(xr, w.double(), padding=1).backward(dy.double().permute(0, 3, 1, 2))
+        assert _err_vs_fp64(dx, xr.grad.permute(0, 2, 3, 1))["rel_l2"] < 1e-5
+
+
+def test_vgg_fp32_runs_winograd_layers(gpu):
+    """The fp32 VGG plan puts every layer with >= 64 input channels on Winograd (forward + data gradient)."""
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.ops import f32
+    m = build_model("vgg", dtype="fp32", device=gpu, kernels="native")
+    ddpx.prepare_model(m, gpu)
+    plan = f32._vgg_plan(m)
+    assert plan.uf[0] is None and all(u is not None for u in plan.uf[1:])
+    assert all(u is not None for u in plan.ud[1:])
