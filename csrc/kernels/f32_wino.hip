@@ -20,6 +20,8 @@
 //     4 tiles x 2 channels), writes the 2x2 pixels, and (forward) the BatchNorm tile statistics (mean, M2 per
 //     channel over the workgroup's 256 pixels; merged by the existing Chan finalize).
 // Requirements: C % 4 == 0, K % 32 == 0, H and W even (every VGG layer on CIFAR-10).
+#include <cstdlib>
+
 #include "ddpx_common.h"
 
 namespace ddpx {
@@ -38,8 +40,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
 }
 
 // y (+ stats) = conv3x3(x) through F(2,3).  x: NHWC [N][H][W][C]; U: [16][C][K]; y: [N*H*W][K].
-template <int STAGES>
-__global__ void __launch_bounds__(NT, 2)  // 2 waves per SIMD: <= 256 VGPR + AGPR (128 are accumulators)
+template <int STAGES, int WAVES_PER_SIMD>
+__global__ void __launch_bounds__(NT, WAVES_PER_SIMD)  // 2: <= 256 VGPR + AGPR (128 are accumulators); 3: <= 168
 wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                 float* __restrict__ stats, int N, int H, int W, int C, int K, int tiles_p, unsigned x_bytes,
                 unsigned u_bytes) {
@@ -115,12 +117,11 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
     float d[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) d[q] = raw[(q * 16 + tl) * 4 + ci];
-    float b[16][2];
+    // B fragments: MFMA column tl of fragment j is output channel k0 + 2 tl + j, so a lane's two channels are
+    // adjacent (one ds_read_b64, conflict-free; the epilogue stores them as one 8-B pair)
+    float2 b[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      b[q][0] = us[(q * 4 + ci) * TK + tl];
-      b[q][1] = us[(q * 4 + ci) * TK + 16 + tl];
-    }
+    for (int q = 0; q < 16; ++q) b[q] = *reinterpret_cast<const float2*>(us + (q * 4 + ci) * TK + 2 * tl);
     // V = B^T d B, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
     float tmp[16];
 #pragma unroll
@@ -140,8 +141,8 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      acc[q][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q][0], acc[q][0], 0, 0, 0);
-      acc[q][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q][1], acc[q][1], 0, 0, 0);
+      acc[q][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q].x, acc[q][0], 0, 0, 0);
+      acc[q][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[q], b[q].y, acc[q][1], 0, 0, 0);
     }
   }
 
@@ -179,8 +180,7 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const size_t pix = ((size_t)n * H + 2 * th + i) * W + 2 * tw + jj;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) y[pix * K + k0 + 16 * j + tl] = out[e][j][i * 2 + jj];
+        *reinterpret_cast<float2*>(y + pix * K + k0 + 2 * tl) = make_float2(out[e][0][i * 2 + jj], out[e][1][i * 2 + jj]);
       }
   }
   if (!stats) return;
@@ -199,12 +199,12 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
       if (valid[e]) s += (out[e][j][0] + out[e][j][1]) + (out[e][j][2] + out[e][j][3]);
     s += __shfl_xor(s, 16, 64);
     s += __shfl_xor(s, 32, 64);
-    if (lr == 0) red[wave * TK + 16 * j + tl] = s;
+    if (lr == 0) red[wave * TK + 2 * tl + j] = s;
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int col = 16 * j + tl;
+    const int col = 2 * tl + j;
     mean[j] = (((red[col] + red[TK + col]) + red[2 * TK + col]) + red[3 * TK + col]) / (float)rows;
   }
   __syncthreads();
@@ -221,13 +221,13 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
         }
     q += __shfl_xor(q, 16, 64);
     q += __shfl_xor(q, 32, 64);
-    if (lr == 0) red[wave * TK + 16 * j + tl] = q;
+    if (lr == 0) red[wave * TK + 2 * tl + j] = q;
   }
   __syncthreads();
   if (wave == 0 && lr == 0) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int col = 16 * j + tl;
+      const int col = 2 * tl + j;
       stats[(size_t)pb * 2 * K + k0 + col] = mean[j];
       stats[(size_t)pb * 2 * K + K + k0 + col] = ((red[col] + red[TK + col]) + red[2 * TK + col]) + red[3 * TK + col];
     }
@@ -255,21 +255,18 @@ __device__ __forceinline__ void g_transform(const float (&g)[9], float (&u)[16])
   }
 }
 
+// One 256-thread block per 16 x 16 (co, ci) tile: w is read ci-fastest (9 contiguous floats per thread), ud is
+// written ci-fastest, uf co-fastest through an LDS transpose — every store stream coalesced.
 __global__ void __launch_bounds__(256)
 wino_wprep_kernel(const float* __restrict__ w, int Co, int Ci, int Cp, float* __restrict__ uf, float* __restrict__ ud) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;  // co fastest: coalesced uf stores
-  if (idx >= Co * Cp) return;
-  const int co = idx % Co, ci = idx / Co;
+  __shared__ float tr[16][16][17];
+  const int t = threadIdx.x;
+  const int ci = blockIdx.y * 16 + (t & 15), co = blockIdx.x * 16 + (t >> 4);
+  const bool in = ci < Cp && co < Co, real = in && ci < Ci;
   float g[9];
-  const bool real = ci < Ci;
 #pragma unroll
   for (int q = 0; q < 9; ++q) g[q] = real ? w[((size_t)co * Ci + ci) * 9 + q] : 0.f;
   float u[16];
-  if (uf) {
-    g_transform(g, u);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) uf[((size_t)q * Cp + ci) * Co + co] = u[q];
-  }
   if (ud && real) {
     float gf[9];
 #pragma unroll
@@ -278,6 +275,15 @@ wino_wprep_kernel(const float* __restrict__ w, int Co, int Ci, int Cp, float* __
 #pragma unroll
     for (int q = 0; q < 16; ++q) ud[((size_t)q * Co + co) * Ci + ci] = u[q];
   }
+  if (!uf) return;
+  g_transform(g, u);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) tr[q][t & 15][t >> 4] = u[q];
+  __syncthreads();
+  const int co2 = blockIdx.x * 16 + (t & 15), ci2 = blockIdx.y * 16 + (t >> 4);
+  if (co2 >= Co || ci2 >= Cp) return;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) uf[((size_t)q * Cp + ci2) * Co + co2] = tr[q][t >> 4][t & 15];
 }
 
 }  // namespace wino
@@ -292,8 +298,8 @@ DDPX_API int ddpx_f32_wino_ok(int H, int W, int C, int K) {
 
 DDPX_API int ddpx_f32_wino_wprep(const float* w, int Co, int Ci, int Cp, float* uf, float* ud, hipStream_t s) {
   if (Cp < Ci) return -2;
-  const int n = Co * Cp;
-  hipLaunchKernelGGL(wino::wino_wprep_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, Co, Ci, Cp, uf, ud);
+  hipLaunchKernelGGL(wino::wino_wprep_kernel, dim3((Co + 15) / 16, (Cp + 15) / 16), dim3(256), 0, s, w, Co, Ci, Cp,
+                     uf, ud);
   return -(int)hipGetLastError();
 }
 
@@ -307,8 +313,18 @@ DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float*
   const int P = N * (H / 2) * (W / 2);
   const int tiles_p = (P + wino::TP - 1) / wino::TP;
   const int nwg = tiles_p * (K / wino::TK);
-  hipLaunchKernelGGL((wino::wino_f32_kernel<3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
-                     tiles_p, (unsigned)xb, (unsigned)ub);
+  // ring depth (DDPX_WINO_STAGES, default 2): 2 stages = 48 KiB, 3 workgroups per CU (8-10 % faster on every VGG
+  // layer, profiles/r5_wino); 3 stages = 72 KiB, 2 per CU
+  static const int stages = [] {
+    const char* e = getenv("DDPX_WINO_STAGES");
+    return e && e[0] == '3' ? 3 : 2;
+  }();
+  if (stages == 2)
+    hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
+                       tiles_p, (unsigned)xb, (unsigned)ub);
+  else
+    hipLaunchKernelGGL((wino::wino_f32_kernel<3, 2>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
+                       tiles_p, (unsigned)xb, (unsigned)ub);
   const int e = (int)hipGetLastError();
   return e ? -e : 4 * wino::TP;
 }

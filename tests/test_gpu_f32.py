@@ -182,44 +182,64 @@ def _train_pair(gpu, name, steps, lr=0.05, fp64=None):
 
 @pytest.mark.parametrize("name", ["vgg", "mlp"])
 def test_native_fp32_gradients_match_torch_fp32(gpu, name):
-    """One backward from the same init and batch: every parameter gradient to fp32 round-off."""
+    """One backward from the same init and batch: every parameter gradient against fp64.
+
+    Above every pooling decision (VGG's classifier; every MLP layer) the gradients are exact to 1e-5.
+    Below a 2x2 max-pool a gradient moves by ~2e-3 whenever one of the 131K windows routes to another element
+    because two candidates lie within fp32 round-off of each other, so a single batch says little: over 8 seeds
+    (benchmarks/f32_grad_seeds.py, profiles/r5_wino) the largest below-pool error of torch's own fp32 run (MIOpen
+    Winograd convolutions) has median 4.1e-3 and max 1.0e-2, the native Winograd path 2.8e-3 / 8.9e-3, the native
+    direct GEMM 1.4e-3 / 4.1e-3.  The VGG bar is therefore torch's own distribution over 6 batches: the native
+    median at most 1.5x torch's, and no batch beyond 1.5e-2."""
     import copy
 
     import ddpx
     from ddpx.models import build_model
-    torch.manual_seed(7)
-    native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None, kernels="native")
-    ref = copy.deepcopy(native).to(gpu)
-    ref.use_native = False
-    flat = ddpx.prepare_model(native, gpu)
-    x = torch.rand(64, 3, 32, 32, device=gpu)
-    y = torch.randint(0, 10, (64,), device=gpu)
-    flat.zero_grad()
-    loss, logits = native.forward_loss(x, y)
-    assert logits is None
-    loss.backward()
-    rl = F.cross_entropy(ref(x), y)
-    rl.backward()
-    assert abs(loss.item() - rl.item()) < 1e-5
-    # fp64 on the CPU is the arbiter: gradients that cancel over 65K pixels (conv0 after BatchNorm) differ
-    # between any two fp32 summation orders by more than the usual 1e-5
-    r64 = copy.deepcopy(ref).cpu().double()
-    r64.compute_dtype = torch.float64
-    r64.zero_grad()
-    F.cross_entropy(r64(x.cpu().double()), y.cpu()).backward()
-    rp, p64 = dict(ref.named_parameters()), dict(r64.named_parameters())
-    # Below a 2x2 max-pool, a gradient moves by ~2e-3 when a handful of the 131K windows route to another
-    # element because two candidates lie within fp32 round-off of each other (measured: 3 flips -> 8e-3
-    # before the blocked-summation GEMM, tools/dbg_f32_vgg.py); torch's own fp32 path lands at 1e-3..2.3e-3
-    # on this batch.  Above the last pooling decision (bn7, classifier) the gradients are exact to 1e-5.
-    bad = []
-    for n, p in native.named_parameters():
-        e_native, e_torch = _rel(p.main_grad.cpu(), p64[n].grad), _rel(rp[n].grad.cpu(), p64[n].grad)
-        print(f"{n}: native {e_native:.2e} torch-fp32 {e_torch:.2e}")
-        top = name == "mlp" or n.startswith(("classifier", "backbone.bn7"))
-        if not e_native < (1e-5 if top else 5e-3):
-            bad.append((n, e_native, e_torch))
-    assert not bad, bad
+    seeds = [7] if name == "mlp" else list(range(6))
+    nat_below, tor_below = [], []
+    for seed in seeds:
+        torch.manual_seed(seed)
+        native = build_model(name, dtype="fp32", device=gpu, hidden=256 if name == "mlp" else None, kernels="native")
+        ref = copy.deepcopy(native).to(gpu)
+        ref.use_native = False
+        flat = ddpx.prepare_model(native, gpu)
+        x = torch.rand(64, 3, 32, 32, device=gpu)
+        y = torch.randint(0, 10, (64,), device=gpu)
+        flat.zero_grad()
+        loss, logits = native.forward_loss(x, y)
+        assert logits is None
+        loss.backward()
+        rl = F.cross_entropy(ref(x), y)
+        rl.backward()
+        assert abs(loss.item() - rl.item()) < 1e-5
+        # fp64 on the CPU is the arbiter: gradients that cancel over 65K pixels (conv0 after BatchNorm) differ
+        # between any two fp32 summation orders by more than the usual 1e-5
+        r64 = copy.deepcopy(ref).cpu().double()
+        r64.compute_dtype = torch.float64
+        r64.zero_grad()
+        F.cross_entropy(r64(x.cpu().double()), y.cpu()).backward()
+        rp, p64 = dict(ref.named_parameters()), dict(r64.named_parameters())
+        bad, nb, tb = [], [0.0], [0.0]
+        for n, p in native.named_parameters():
+            e_native, e_torch = _rel(p.main_grad.cpu(), p64[n].grad), _rel(rp[n].grad.cpu(), p64[n].grad)
+            print(f"seed {seed} {n}: native {e_native:.2e} torch-fp32 {e_torch:.2e}")
+            # bn7 sits below pool3's routing (a flip moved its bias gradient by 3.4e-4 on one seed): only the
+            # classifier is above every pooling decision
+            top = name == "mlp" or n.startswith("classifier")
+            if top:
+                if not e_native < 1e-5:
+                    bad.append((seed, n, e_native, e_torch))
+            else:
+                nb.append(e_native)
+                tb.append(e_torch)
+        assert not bad, bad
+        nat_below.append(max(nb))
+        tor_below.append(max(tb))
+    if name == "vgg":
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        print("below-pool max error per seed: native", nat_below, "torch", tor_below)
+        assert med(nat_below) <= 1.5 * med(tor_below), (nat_below, tor_below)
+        assert max(nat_below) < 1.5e-2, (nat_below, tor_below)
 
 
 @pytest.mark.parametrize("name", ["vgg", "mlp"])
