@@ -43,8 +43,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
 template <int STAGES, int WAVES_PER_SIMD>
 __global__ void __launch_bounds__(NT, WAVES_PER_SIMD)  // 2: <= 256 VGPR + AGPR (128 are accumulators); 3: <= 168
 wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
-                float* __restrict__ stats, int N, int H, int W, int C, int K, int tiles_p, unsigned x_bytes,
-                unsigned u_bytes) {
+                float* __restrict__ stats, const float* __restrict__ bias, int relu, int N, int H, int W, int C, int K,
+                int tiles_p, unsigned x_bytes, unsigned u_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,6 +167,20 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
       out[e][j][2] = t1[0] + t1[1] + t1[2];
       out[e][j][3] = t1[1] - t1[2] - t1[3];
     }
+  if (bias || relu) {  // DeepNN's conv + bias + ReLU (y = relu(conv + b)); VGG's convolutions have neither
+    const float b0 = bias ? bias[k0 + 2 * tl] : 0.f, b1 = bias ? bias[k0 + 2 * tl + 1] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        out[e][0][u] += b0;
+        out[e][1][u] += b1;
+        if (relu) {
+          out[e][0][u] = fmaxf(out[e][0][u], 0.f);
+          out[e][1][u] = fmaxf(out[e][1][u], 0.f);
+        }
+      }
+  }
   bool valid[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -303,10 +317,10 @@ DDPX_API int ddpx_f32_wino_wprep(const float* w, int Co, int Ci, int Cp, float* 
   return -(int)hipGetLastError();
 }
 
-// y [N*H*W][K] = conv3x3(x [N][H][W][C]) with U [16][C][K]; stats (nullable): [tiles_p][2][K] chunk statistics of
-// 256-pixel chunks.  Returns the statistics chunk rows (256) or a negative error.
-DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float* stats, int N, int H, int W, int C,
-                                int K, hipStream_t s) {
+// y [N*H*W][K] = conv3x3(x [N][H][W][C]) with U [16][C][K] [+ bias[K]] [relu]; stats (nullable): [tiles_p][2][K]
+// chunk statistics of 256-pixel chunks.  Returns the statistics chunk rows (256) or a negative error.
+DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float* stats, const float* bias, int relu,
+                                int N, int H, int W, int C, int K, hipStream_t s) {
   if (!ddpx_f32_wino_ok(H, W, C, K)) return -2;
   const size_t xb = (size_t)N * H * W * C * 4, ub = (size_t)16 * C * K * 4;
   if (xb >= 0x80000000ull || ub >= 0x80000000ull) return -3;  // 32-bit buffer offsets, top bit = out of bounds
@@ -320,11 +334,11 @@ DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float*
     return e && e[0] == '3' ? 3 : 2;
   }();
   if (stages == 2)
-    hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
-                       tiles_p, (unsigned)xb, (unsigned)ub);
+    hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
+                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
   else
-    hipLaunchKernelGGL((wino::wino_f32_kernel<3, 2>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, N, H, W, C, K,
-                       tiles_p, (unsigned)xb, (unsigned)ub);
+    hipLaunchKernelGGL((wino::wino_f32_kernel<3, 2>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
+                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
   const int e = (int)hipGetLastError();
   return e ? -e : 4 * wino::TP;
 }

@@ -43,7 +43,7 @@ for _sig in (
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
         ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
         ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
-        ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P),
+        ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P),
 ):
     native.register_kernel_sig(*_sig)
 
@@ -229,14 +229,14 @@ def conv_dgrad(dy, wd, N, H, W, C, Co):
 
 
 # ------------------------------------------------------------------ Winograd F(2x2, 3x3) (csrc/kernels/f32_wino.hip)
-# The forward and data-gradient 3x3 convolutions of the VGG layers with >= DDPX_F32_WINO_MIN_C input channels
-# (default 64: every layer but the 3-channel image one) run as fp32 Winograd F(2,3), MIOpen's algorithm for the
+# The forward and data-gradient 3x3 convolutions with >= DDPX_F32_WINO_MIN_C input channels (default 16: every
+# layer but the 3-channel image one) run as fp32 Winograd F(2,3), MIOpen's algorithm for the
 # stock fp32 recipe, with 2.25x fewer multiplies than the exact implicit GEMM.  DDPX_F32_WINO=0: the direct
 # implicit GEMM everywhere (the weight gradient always is).
 import os as _os  # noqa: E402
 
 _WINO = _os.environ.get("DDPX_F32_WINO", "1") != "0"
-_WINO_MIN_C = int(_os.environ.get("DDPX_F32_WINO_MIN_C", "64"))
+_WINO_MIN_C = int(_os.environ.get("DDPX_F32_WINO_MIN_C", "16"))
 
 
 def wino_applies(H, W, C, K) -> bool:
@@ -252,16 +252,16 @@ def wino_wprep(w, uf, ud):
     _call("ddpx_f32_wino_wprep", w.data_ptr(), Co, Ci, Cp, native.ptr(uf), native.ptr(ud))
 
 
-def wino_conv(x, u, K, stats=False):
-    """y [N*H*W, K] = conv3x3(x [N,H,W,C]) through F(2,3) with u [16][C][K]; with ``stats``: (y, (part, T, 256)),
-    the BatchNorm chunk statistics of every 256-pixel output chunk from the epilogue."""
+def wino_conv(x, u, K, stats=False, bias=None, relu=False):
+    """y [N*H*W, K] = [relu](conv3x3(x [N,H,W,C]) [+ bias]) through F(2,3) with u [16][C][K]; with ``stats``:
+    (y, (part, T, 256)), the BatchNorm chunk statistics of every 256-pixel output chunk from the epilogue."""
     N, H, W, C = x.shape
     _f32(x, "x")
     y = torch.empty((N * H * W, K), dtype=torch.float32, device=x.device)
     T = (N * (H // 2) * (W // 2) + 63) // 64
     st = torch.empty((T, 2, K), dtype=torch.float32, device=x.device) if stats else None
-    r = native.kernels().ddpx_f32_wino_conv(x.data_ptr(), u.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, K,
-                                             native.stream_handle())
+    r = native.kernels().ddpx_f32_wino_conv(x.data_ptr(), u.data_ptr(), y.data_ptr(), native.ptr(st),
+                                             native.ptr(bias), int(relu), N, H, W, C, K, native.stream_handle())
     native.check(r if r < 0 else 0, "ddpx_f32_wino_conv")
     return (y, (st, T, r)) if stats else y
 
@@ -385,12 +385,14 @@ class _VGGPlan:
             Cp = conv_channels(Ci)
             # Winograd for the forward (and, below the first block, the data gradient) where it applies; the
             # direct layouts only where it does not
-            wino = dev.type == "cuda" and wino_applies(H, H, Cp, Co) and (bi == 0 or Ci % 32 == 0)
+            wino = dev.type == "cuda" and wino_applies(H, H, Cp, Co)
+            dwino = wino and bi > 0 and wino_applies(H, H, Co, Ci)  # the data gradient: Co -> Ci channels
             self.uf.append(torch.empty(16 * Cp * Co, dtype=torch.float32, device=dev) if wino else None)
-            self.ud.append(torch.empty(16 * Co * Ci, dtype=torch.float32, device=dev) if wino and bi > 0 else None)
-            self.wf.append(torch.empty(9 * Cp * Co, dtype=torch.float32, device=dev) if not wino else None)
+            self.ud.append(torch.empty(16 * Co * Ci, dtype=torch.float32, device=dev) if dwino else None)
+            direct = not wino or (bi > 0 and not dwino)
+            self.wf.append(torch.empty(9 * Cp * Co, dtype=torch.float32, device=dev) if direct else None)
             self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev)
-                           if (not wino and Ci % 4 == 0) else None)
+                           if (direct and Ci % 4 == 0) else None)
             if pool:
                 H //= 2
 
@@ -443,6 +445,8 @@ def _vgg_forward(model, x, targets, training):
         Co = conv.weight.shape[0]
         if plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co):
             wino_wprep(conv.weight, plan.uf[bi], plan.ud[bi])
+            if plan.wd[bi] is not None:  # data gradient on the direct GEMM
+                conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
             if training:
                 y, st = wino_conv(x, plan.uf[bi], Co, stats=True)
             else:
@@ -489,7 +493,7 @@ def _vgg_backward(model, saved, last, dl, grad_out):
         flat.grad_done(bn.bias)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
-            if plan.ud[bi] is not None and wino_applies(H, W, Co, C):
+            if plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
                 g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
             else:
                 g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
@@ -540,11 +544,21 @@ class _DeepNNPlan:
         cls = list(model.classifier.children())
         self.lin0, self.drop, self.lin1 = cls[0], cls[2], cls[3]
         dev = self.lin0.weight.device
-        self.wf, self.wd = [], []
-        for conv, _ in self.blocks:
+        self.wf, self.wd, self.uf, self.ud = [], [], [], []
+        H = 32
+        for bi, (conv, pool) in enumerate(self.blocks):
             Co, Ci = conv.weight.shape[:2]
-            self.wf.append(torch.empty(9 * conv_channels(Ci) * Co, dtype=torch.float32, device=dev))
+            Cp = conv_channels(Ci)
+            # Winograd F(2,3) forward (+ bias + ReLU epilogue) and data gradient where it applies (the 128 -> 64,
+            # 64 -> 64 and 64 -> 32 layers), the direct implicit GEMM elsewhere
+            wino = dev.type == "cuda" and wino_applies(H, H, Cp, Co)
+            dwino = wino and bi > 0 and wino_applies(H, H, Co, Ci)  # the data gradient: Co -> Ci channels
+            self.uf.append(torch.empty(16 * Cp * Co, dtype=torch.float32, device=dev) if wino else None)
+            self.ud.append(torch.empty(16 * Co * Ci, dtype=torch.float32, device=dev) if dwino else None)
+            self.wf.append(torch.empty(9 * Cp * Co, dtype=torch.float32, device=dev))
             self.wd.append(torch.empty(9 * Co * Ci, dtype=torch.float32, device=dev) if Ci % 4 == 0 else None)
+            if pool:
+                H //= 2
         cmax = max(c.weight.shape[0] for c, _ in self.blocks)
         self.ones = torch.ones(cmax, dtype=torch.float32, device=dev)
         self.zeros = torch.zeros(cmax, dtype=torch.float32, device=dev)
@@ -588,11 +602,18 @@ def _deepnn_forward(model, x, targets, training):
     N, H, W, C = x.shape
     for bi, (conv, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
-        conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
         P = N * H * W
-        y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
-        gemm(IM2COL_KC, x, 0, DENSE_OC, plan.wf[bi], Co, P, Co, 9 * C, y, geom=(C, H, W, 1), bias=conv.bias,
-             relu=True)
+        if plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co):
+            wino_wprep(conv.weight, plan.uf[bi], plan.ud[bi])
+            if bi > 0 and plan.ud[bi] is None:  # data gradient on the direct GEMM
+                conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
+            y = wino_conv(x, plan.uf[bi], Co, bias=conv.bias, relu=True)
+        else:
+            conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
+            plan.ud[bi] = None  # this input size takes the direct path: so does the data gradient
+            y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
+            gemm(IM2COL_KC, x, 0, DENSE_OC, plan.wf[bi], Co, P, Co, 9 * C, y, geom=(C, H, W, 1), bias=conv.bias,
+                 relu=True)
         if pool:
             xn = torch.empty((N, H // 2, W // 2, Co), dtype=torch.float32, device=x.device)
             _call("ddpx_f32_bn_apply", y.data_ptr(), plan.ones.data_ptr(), plan.zeros.data_ptr(),
@@ -638,7 +659,10 @@ def _deepnn_backward(model, saved, last, dl, grad_out):
         _grad_write(flat, conv.bias, bias_grad)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
-            g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            if plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
+                g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
+            else:
+                g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
 
 
 class _DeepNNLossF32(torch.autograd.Function):

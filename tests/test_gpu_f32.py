@@ -637,3 +637,28 @@ def test_vgg_fp32_runs_winograd_layers(gpu):
     plan = f32._vgg_plan(m)
     assert plan.uf[0] is None and all(u is not None for u in plan.uf[1:])
     assert all(u is not None for u in plan.ud[1:])
+
+
+def test_wino_conv_bias_relu_epilogue(gpu):
+    """DeepNN's conv + bias + ReLU through the Winograd epilogue, against fp64."""
+    from ddpx.ops import f32
+    torch.manual_seed(6)
+    N, H, Ci, Co = 6, 16, 128, 64
+    x = torch.randn(N, Ci, H, H, device=gpu)
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+    b = torch.randn(Co, device=gpu)
+    uf = torch.empty(16 * Ci * Co, device=gpu)
+    f32.wino_wprep(w, uf, None)
+    y = f32.wino_conv(x.permute(0, 2, 3, 1).contiguous(), uf, Co, bias=b, relu=True)
+    ref = torch.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)).permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _err_vs_fp64(y, ref)["rel_l2"] < 1e-5
+
+
+def test_deepnn_fp32_runs_winograd_layers(gpu):
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.ops import f32
+    m = build_model("deepnn", dtype="fp32", device=gpu, kernels="native")
+    ddpx.prepare_model(m, gpu)
+    plan = f32._deepnn_plan(m)
+    assert plan.uf[0] is None and all(u is not None for u in plan.uf[1:]), [u is not None for u in plan.uf]
