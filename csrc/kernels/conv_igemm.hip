@@ -314,7 +314,10 @@ DDPX_API int ddpx_conv_wgrad_splits(int P, int C, int Co, int tile_cfg) {
       best = S;
     }
   }
-  return best;
+  // the splits that actually get a K range (64-aligned split lengths can leave the last ones empty): the caller
+  // sizes the partial slabs and the reduce by this, so no slab needs zeroing inside the step
+  const int klen = ((P + best - 1) / best + 63) / 64 * 64;
+  return (P + klen - 1) / klen;
 }
 
 // part[S][Co][9C] (fp32) = split-K partial weight gradients.  dy [P][Co], x NHWC [N][H][W][C].
