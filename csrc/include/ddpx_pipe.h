@@ -45,6 +45,8 @@ enum Epi : int {
   EPI_RELUMASK_BF16 = 5,  // C(bf16) = acc * (aux[m][n] > 0)
   EPI_SGD = 6,            // fused optimizer: acc is the gradient of the parameter at C's index
   EPI_BNSTAT_BF16 = 7,    // C(bf16) = acc; per-tile column (mean, M2) of the stored values -> colsum
+  EPI_BNBWD_BF16 = 8,     // conv data gradient g (bf16) + the BatchNorm backward sums of the block below:
+                          // per-tile column (sum dz, sum dz*xhat) -> colsum, dz = g routed / ReLU-masked by bn_y
 };
 
 enum Mode : int { MODE_PLAIN = 0, MODE_IM2COL_FWD = 1, MODE_IM2COL_BWD = 2, MODE_IM2COL_COL = 3 };
@@ -118,6 +120,15 @@ struct Params {
   // diagnostics (ddpx_gemm_set_stamps): per-workgroup s_memrealtime stamps (100 MHz) at kernel start, main loop
   // end, split-K ticket taken, combine done, epilogue done: [workgroup][8] int64; nullptr = off
   long long* stamp;
+  // EPI_BNBWD_BF16 (conv data gradient whose output g feeds the BatchNorm + ReLU [+ 2x2 max-pool] backward of
+  // the block below): that block's pre-BN activation y (bf16, [P'][N], P' = 4 P when pooled) and per-channel
+  // a = gamma*rstd, b = beta - mean*a, mean, rstd; bn_pool = 1 when a pool sits between y and g
+  const unsigned short* bn_y;
+  const float* bn_a;
+  const float* bn_b;
+  const float* bn_mean;
+  const float* bn_rstd;
+  int bn_pool;
 };
 
 __device__ __forceinline__ void stamp_at(const Params& p, int tid, int k) {
@@ -563,6 +574,88 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
 }  // chunk
 }
 
+// EPI_BNBWD_BF16: store g = bf16(acc) like EPI_BF16 and accumulate, per column, the BatchNorm backward sums of
+// the block below over this thread's rows: dz = g at the window's first max of relu(a*y+b) (pooled) / at its own
+// pixel, zeroed where a*y+b <= 0 (the routing and mask of bn_pool.hip's grad_z / grad_window, recomputed from y),
+// s1 += dz, s2 += dz * (y - mean) * rstd.  The standalone reduce pass over g and y is gone (g never re-read).
+template <int BM, int BN, int NT = 256>
+__device__ __forceinline__ void epilogue_bnbwd(const Params& p, void* Cbase, const float* T, int m0, int n0, int tid,
+                                               float (&s1)[4], float (&s2)[4]) {
+  constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BM / RSTEP, TLD = BN + 4;
+  const int cq = tid % Q, r0 = tid / Q;
+  const int n = n0 + 4 * cq;
+  if (n + 3 >= p.N) return;  // the host requires N % 8 == 0: a quad is all in or all out
+  float av[4], bv[4], mu[4], rs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    av[q] = p.bn_a[n + q];
+    bv[q] = p.bn_b[n + q];
+    mu[q] = p.bn_mean[n + q];
+    rs[q] = p.bn_rstd[n + q];
+  }
+  const int Ho = p.conv.H, Wo = p.conv.W;  // g's spatial size (the dgrad's im2col'd dy)
+  const int ldy = p.N;
+  // rows whose y loads are in flight together: 2 (8 VGPRs of y per row when pooled; the 8-wave dgrad tiles
+  // already spill in their plain epilogue)
+  constexpr int CH = NV < 2 ? NV : 2;
+#pragma unroll
+  for (int i0 = 0; i0 < NV; i0 += CH) {
+    u32x2 yv[CH][4];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int m = m0 + r0 + (i0 + i) * RSTEP;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) yv[i][k] = (u32x2){0u, 0u};
+      if (m >= p.M) continue;
+      if (p.bn_pool) {
+        const int wo = m % Wo, t = m / Wo, ho = t % Ho, img = t / Ho;
+        const size_t base = ((size_t)img * 2 * Ho + 2 * ho) * (2 * Wo) + 2 * wo;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          yv[i][k] = *reinterpret_cast<const u32x2*>(p.bn_y + (base + (k >> 1) * 2 * Wo + (k & 1)) * ldy + n);
+      } else {
+        yv[i][0] = *reinterpret_cast<const u32x2*>(p.bn_y + (size_t)m * ldy + n);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int r = r0 + (i0 + i) * RSTEP;
+      const int m = m0 + r;
+      if (m >= p.M) continue;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(T + r * TLD + 4 * cq);
+      float g[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] = bf2f(f2bf(v[q] * p.alpha));
+      *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(Cbase) + (size_t)m * p.ldc + n) =
+          (u32x2){pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3])};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float ysel, zsel;
+        if (p.bn_pool) {
+          float best = -INFINITY;
+          ysel = 0.f;
+          zsel = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const unsigned w = yv[i][k][q >> 1];
+            const float yk = __uint_as_float((q & 1) ? (w & 0xffff0000u) : (w << 16));
+            const float z = fmaf(av[q], yk, bv[q]);
+            const float zr = fmaxf(z, 0.f);
+            if (zr > best) { best = zr; ysel = yk; zsel = z; }  // strict: the first max wins, as torch
+          }
+        } else {
+          const unsigned w = yv[i][0][q >> 1];
+          ysel = __uint_as_float((q & 1) ? (w & 0xffff0000u) : (w << 16));
+          zsel = fmaf(av[q], ysel, bv[q]);
+        }
+        const float dz = zsel > 0.f ? g[q] : 0.f;
+        s1[q] += dz;
+        s2[q] = fmaf(dz, (ysel - mu[q]) * rs[q], s2[q]);
+      }
+    }
+  }
+}
+
 // Column reductions of the stored tile: thread (cq, r0) holds partial sums of 4 columns.
 template <int BN, int NT = 256>
 __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], int tid, float* out /* BN */) {
@@ -875,6 +968,24 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
       case EPI_BNSTAT_BF16:
         if constexpr (LW == 0) epilogue_vec<EPI_BNSTAT_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch);
         break;
+      case EPI_BNBWD_BF16:
+        // conv data-gradient kernels, only the tiles where the fused sums measured faster than the separate
+        // reduce pass (256x128 / 3 stages and 128x128 / 4 stages / 8 waves, profiles/r5_vgg/NOTES.md): the
+        // others do not carry the epilogue's registers
+        if constexpr (LW == 0 && AMODE == MODE_IM2COL_BWD && NW == 8 &&
+                      ((BM == 256 && BN == 128 && STAGES == 3) || (BM == 128 && BN == 128 && STAGES == 4))) {
+          float s2[4] = {0.f, 0.f, 0.f, 0.f};
+          epilogue_bnbwd<BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch, s2);
+          __syncthreads();
+          quad_colsum<BN, NT>(red, ch, tid, colres);
+          const size_t st = (size_t)tm * EH + h;
+          if (tid < BN && n0 + tid < p.N) p.colsum[(st * 2) * p.N + n0 + tid] = colres[tid];
+          quad_colsum<BN, NT>(red, s2, tid, colres);
+          if (tid < BN && n0 + tid < p.N) p.colsum[(st * 2 + 1) * p.N + n0 + tid] = colres[tid];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ch[q] = 0.f;
+        }
+        break;
       default: epilogue_vec<EPI_RELUMASK_BF16, BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch); break;
     }
 #pragma unroll
@@ -913,7 +1024,7 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
     }
   }
   stamp_at(p, tid, 4);
-  if (!p.colsum || p.epi == EPI_BNSTAT_BF16) return;
+  if (!p.colsum || p.epi == EPI_BNSTAT_BF16 || p.epi == EPI_BNBWD_BF16) return;
 
   // ---- per-tile column sums (bias gradient) ----
   __syncthreads();

@@ -784,6 +784,23 @@ DDPX_API int ddpx_bn_bwd_sums(const void* gout, const void* y, const float* a, c
   return (int)hipGetLastError();
 }
 
+// The second half of ddpx_bn_bwd when the pass-1 partials part[B][2][C] were produced elsewhere (the conv data
+// gradient's EPI_BNBWD_BF16 epilogue): merge them (c1, c2, dgamma / dbeta or their fused SGD), then dy.
+DDPX_API int ddpx_bn_bwd_tail(const void* gout, const void* y, const float* a, const float* b, const float* mean,
+                              const float* rstd, int N, int H, int W, int C, int pool, int relu, const float* part,
+                              int B, float* c1, float* c2, void* dgamma, void* dbeta, int out_bf16, int accumulate,
+                              void* dy, float* sg_p, float* sg_buf, float* sb_p, float* sb_buf, const float* lr,
+                              float mom, float wd, hipStream_t s) {
+  if (C % 8 || C > 512 || B < 1 || (pool && (H % 2 || W % 2))) return -1;
+  launch_bwd_finalize(part, B, C, N * H * W, c1, c2, dgamma, dbeta, out_bf16, accumulate,
+                      SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd}, SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd}, s);
+  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
+  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, a, b, mean, rstd, c1, c2, N, H, W, C, pool, relu, 1,
+                     (unsigned short*)dy);
+  return (int)hipGetLastError();
+}
+
 DDPX_API int ddpx_bn_bwd_apply(const void* gout, const void* y, const float* a, const float* b, const float* mean,
                                const float* rstd, const float* c1, const float* c2, int N, int H, int W, int C,
                                int pool, int relu, void* dy, hipStream_t s) {

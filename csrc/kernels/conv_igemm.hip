@@ -270,6 +270,48 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
   return (int)dispatch_conv_dgrad(p, cfg, s);
 }
 
+// Data gradient fused with the BatchNorm backward sums of the block below (EPI_BNBWD_BF16): dx as ddpx_conv_dgrad,
+// plus part[B][2][C] = per-row-tile (sum dz, sum dz*xhat) of the routed, ReLU-masked gradient, B =
+// ddpx_conv_dgrad_parts(...).  bn_y: the block below's pre-BN activation [N][H'][W'][C] (H' = 2H when pooled).
+// Returns 0 when the picked tile has no fused variant (the caller then runs the plain data gradient and the
+// separate reduce).
+DDPX_API int ddpx_conv_dgrad_parts(int N, int H, int W, int C, int Co, int tile_cfg) {
+  const int P = N * H * W;
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
+  if (cfg != 8 && cfg != 15) return 0;  // the configs instantiating EPI_BNBWD_BF16 (ddpx_pipe.h)
+  int bm, bn;
+  tile_of(cfg, &bm, &bn);
+  return (P + bm - 1) / bm * epilogue_halves(cfg);
+}
+
+DDPX_API int ddpx_conv_dgrad_bn(const void* dy, const void* wd, void* dx, int N, int H, int W, int C, int Co,
+                                int tile_cfg, const void* bn_y, const float* a, const float* b, const float* mean,
+                                const float* rstd, int pool, float* part, hipStream_t s) {
+  if (C % 8 || Co % 8 || !bn_y || !a || !b || !mean || !rstd || !part) return -1;
+  if (!chk16(dy) || !chk16(wd) || !chk16(dx) || !chk16(bn_y)) return -3;
+  const int P = N * H * W, K = 9 * Co;
+  Params p{};
+  p.A = (const unsigned short*)dy;
+  p.B = (const unsigned short*)wd;
+  p.C = dx;
+  p.M = P; p.N = C; p.K = K;
+  p.lda = Co; p.ldb = C; p.ldc = C;
+  p.epi = EPI_BNBWD_BF16;
+  p.alpha = 1.f;
+  p.im_slow = im_slow();
+  const size_t ab = (size_t)P * Co * 2, bb = (size_t)K * C * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = make_geom(H, W, Co, P);
+  p.colsum = part;
+  p.bn_y = (const unsigned short*)bn_y;
+  p.bn_a = a; p.bn_b = b; p.bn_mean = mean; p.bn_rstd = rstd;
+  p.bn_pool = pool;
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
+  if (cfg != 8 && cfg != 15) return -5;
+  return (int)dispatch_conv_dgrad(p, cfg, s);
+}
+
 static int pick_wgrad(int P, int C, int Co) {
   (void)P;
   if (C <= 8) return 12;      // conv0 (K = 9 x 8): 64x64, BK 128

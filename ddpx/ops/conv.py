@@ -64,6 +64,25 @@ def conv_dgrad(dy, wd, N, H, W, C, Co, tile=-1):
     return dx
 
 
+def conv_dgrad_bn(dy, wd, N, H, W, C, Co, bn_y, a, b, mean, rstd, pool, tile=-1):
+    """(dx, (part, B)): the data gradient of the conv, with the BatchNorm backward pass-1 sums of the block below
+    (its pre-BN activation ``bn_y`` [N, H', W', C], H' = 2H when a 2x2 max-pool sits between) from the GEMM
+    epilogue: ``bn_backward(..., part=(part, B))`` then skips its own reduce over dx and bn_y.  (dx, None) for
+    the layers whose data-gradient tile has no fused variant (measured slower there, profiles/r5_vgg)."""
+    _nhwc(dy, "dy", Co)
+    _req(wd.numel() == 9 * Co * C, "conv_dgrad_bn: bad weight buffer")
+    lib = native.kernels()
+    B = lib.ddpx_conv_dgrad_parts(N, H, W, C, Co, tile)
+    if B == 0:  # no fused variant for this layer's tile: plain data gradient, bn_backward reduces itself
+        return conv_dgrad(dy, wd, N, H, W, C, Co, tile), None
+    part = torch.empty((B, 2, C), dtype=torch.float32, device=dy.device)
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    native.check(lib.ddpx_conv_dgrad_bn(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), N, H, W, C, Co, tile,
+                                        bn_y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                        int(pool), part.data_ptr(), native.stream_handle()), "ddpx_conv_dgrad_bn")
+    return dx, (part, B)
+
+
 def conv_wgrad(dy, x, Co, Cr, out=None, accumulate=False, sgd=None, tile=-1, prepared=None):
     """Weight gradient in torch layout [Co,Cr,3,3] (written to ``out`` or applied through ``sgd``).
     ``prepared`` = (wf, wd) with ``sgd``: the update also rewrites the bf16 GEMM layouts ``weight_prep`` makes
@@ -155,13 +174,30 @@ def bn_apply(y, a, b, N, H, W, C, relu=True, pool=False):
 
 
 def bn_backward(gout, y, a, b, mean, rstd, N, H, W, C, pool, dgamma=None, dbeta=None, accumulate=False,
-                sgd_gamma=None, sgd_beta=None):
-    """dy [N*H*W, C] bf16; dgamma/dbeta stored (fp32/bf16) or applied through sgd_gamma / sgd_beta."""
+                sgd_gamma=None, sgd_beta=None, part=None):
+    """dy [N*H*W, C] bf16; dgamma/dbeta stored (fp32/bf16) or applied through sgd_gamma / sgd_beta.  ``part`` =
+    (partials [B, 2, C], B): the pass-1 sums already made by the data gradient that produced ``gout``
+    (``conv_dgrad_bn``)."""
     _nhwc(gout, "gout", C)
     _nhwc(y, "y", C)
     lib = native.kernels()
-    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
     dev = y.device
+    if part is not None:
+        pt, B = part
+        c1 = torch.empty(C, dtype=torch.float32, device=dev)
+        c2 = torch.empty(C, dtype=torch.float32, device=dev)
+        dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)
+        gdt = dgamma.dtype if dgamma is not None else torch.float32
+        sg, sb = native.sgd_args(sgd_gamma), native.sgd_args(sgd_beta)
+        lr = sg[3] if sgd_gamma is not None else None
+        mom, wd = (sg[4], sg[5]) if sgd_gamma is not None else (0.0, 0.0)
+        native.check(lib.ddpx_bn_bwd_tail(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                          rstd.data_ptr(), N, H, W, C, int(pool), 1, pt.data_ptr(), B, c1.data_ptr(),
+                                          c2.data_ptr(), native.ptr(dgamma), native.ptr(dbeta),
+                                          int(gdt == torch.bfloat16), int(accumulate), dy.data_ptr(), sg[0], sg[1],
+                                          sb[0], sb[1], lr, mom, wd, native.stream_handle()), "ddpx_bn_bwd_tail")
+        return dy
+    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
     part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
     c1 = torch.empty(C, dtype=torch.float32, device=dev)
     c2 = torch.empty(C, dtype=torch.float32, device=dev)

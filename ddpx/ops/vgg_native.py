@@ -35,6 +35,9 @@ from .head import head_backward, head_forward
 # DDPX_CONV_PREP_FROM_UPDATE=0: re-derive the bf16 conv layouts every forward (weight_prep) even when the fused
 # update already wrote them (A/B checks)
 _PREP_FROM_UPDATE = os.environ.get("DDPX_CONV_PREP_FROM_UPDATE", "1") != "0"
+# DDPX_BN_BWD_FUSE=0: the BatchNorm backward sums by their own reduce pass over g and y, instead of in the epilogue
+# of the conv data gradient that produces g (csrc/include/ddpx_pipe.h EPI_BNBWD_BF16)
+_BN_BWD_FUSE = os.environ.get("DDPX_BN_BWD_FUSE", "1") != "0"
 
 
 class _Plan:
@@ -135,11 +138,20 @@ def _backward(model, saved, last, dl, grad_out):
         flat.grad_done(cls.weight)
         flat.grad_done(cls.bias)
     g = K.avgpool_backward(dfeat, *xshape)
+    comm = _sync_comm(model, True)
+    gpart = None  # BatchNorm pass-1 sums of g, when the data gradient that made g produced them
+
+    def dgrad(dy, wd, bi, N, H, W, C, Co):
+        """g of the block below, with its BatchNorm backward sums from the GEMM epilogue when possible."""
+        if _BN_BWD_FUSE and comm is None:
+            _, yp, ap, bp, mp, rp, _, poolp = saved[bi - 1]
+            return K.conv_dgrad_bn(dy, wd, N, H, W, C, Co, yp, ap, bp, mp, rp, poolp)
+        return K.conv_dgrad(dy, wd, N, H, W, C, Co), None
+
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, bn, pool = plan.blocks[bi]
         x, y, a, b, mean, rstd, (N, H, W, C, Co), _ = saved[bi]
         sg, sbeta = flat.fused_spec(bn.weight), flat.fused_spec(bn.bias)
-        comm = _sync_comm(model, True)
         if comm is not None:
             if sg is not None:
                 raise RuntimeError("SyncBatchNorm runs under DDP; the fused single-process optimizer does not apply")
@@ -150,13 +162,14 @@ def _backward(model, saved, last, dl, grad_out):
             flat.grad_done(bn.weight)
             flat.grad_done(bn.bias)
         elif sg is not None:
-            dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, sgd_gamma=sg, sgd_beta=sbeta)
+            dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, sgd_gamma=sg, sgd_beta=sbeta, part=gpart)
             flat.mark_updated(bn.weight)
             flat.mark_updated(bn.bias)
         else:
             dgam, accg = flat.grad_target(bn.weight)
             dbet, _ = flat.grad_target(bn.bias)
-            dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgamma=dgam, dbeta=dbet, accumulate=accg)
+            dy = K.bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgamma=dgam, dbeta=dbet, accumulate=accg,
+                               part=gpart)
             flat.grad_done(bn.weight)
             flat.grad_done(bn.bias)
         Cr = conv.weight.shape[1]
@@ -166,7 +179,7 @@ def _backward(model, saved, last, dl, grad_out):
             # them with the updated weight, after this block's dgrad below has read wd (stream order)
             prep = _PREP_FROM_UPDATE and plan.wver[bi] == flat.version_of(conv.weight)
             if prep and bi > 0:
-                g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+                g, gpart = dgrad(dy, plan.wd[bi], bi, N, H, W, C, Co)
             K.conv_wgrad(dy, x, Co, Cr, sgd=sw, prepared=(plan.wf[bi], plan.wd[bi]) if prep else None)
             flat.mark_updated(conv.weight)
             if prep:
@@ -177,7 +190,7 @@ def _backward(model, saved, last, dl, grad_out):
             K.conv_wgrad(dy, x, Co, Cr, out=dw, accumulate=accw)
             flat.grad_done(conv.weight)
         if bi > 0:
-            g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            g, gpart = dgrad(dy, plan.wd[bi], bi, N, H, W, C, Co)
 
 
 class _VGGLoss(torch.autograd.Function):

@@ -74,6 +74,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I)
     _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_dgrad_parts", I, I, I, I, I, I, I)
+    _sig(lib, "ddpx_conv_dgrad_bn", I, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, P, P)
     _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I, I)
     _sig(lib, "ddpx_conv_wgrad", I, P, P, P, I, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_wgrad_reduce", I, P, I, I, I, I, P, I, I, P, P, P, P, F, F, P, P, P)
@@ -84,6 +86,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_bn_bwd_apply", I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P)
     _sig(lib, "ddpx_bn_bwd_blocks", I, I, I, I, I)
     _sig(lib, "ddpx_bn_bwd", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_bn_bwd_tail", I, P, P, P, P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, F, F,
+         P)
     _sig(lib, "ddpx_bias_act_bwd", I, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P)
     _sig(lib, "ddpx_dropout_fwd", I, P, P, I64, F, P, P, P)
     _sig(lib, "ddpx_avgpool", I, P, I, I, I, P, P)

@@ -318,3 +318,36 @@ def test_wgrad_fused_sgd_writes_prepared_layouts(gpu, N, H, C, Co):
     torch.cuda.synchronize()
     assert torch.equal(wf, wf_ref) and torch.equal(wd, wd_ref)
     assert torch.allclose(p, p_ref, rtol=1e-6, atol=1e-6) and torch.allclose(buf, buf_ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,H,C,Co,pool", [(8, 16, 64, 128, True), (2, 8, 256, 256, False), (64, 16, 128, 256, True),
+                                           (64, 16, 256, 256, False), (16, 4, 512, 512, True), (256, 8, 256, 512, False)])
+def test_dgrad_bn_epilogue_matches_separate_reduce(gpu, N, H, C, Co, pool):
+    """The conv data gradient with the BatchNorm backward sums of the block below in its epilogue
+    (EPI_BNBWD_BF16 on tile configs 15 and 8; the other picks fall back to the plain data gradient) = the plain
+    data gradient + bn_backward's own reduce: g bitwise, the sums / dgamma / dbeta / dy to fp32 summation order."""
+    from ddpx.ops import conv as K
+    from ddpx.runtime import native
+    torch.manual_seed(3)
+    Hy = 2 * H if pool else H
+    y = (torch.randn(N, Hy, Hy, C, device=gpu) * 1.5 + 0.3).to(torch.bfloat16).contiguous()
+    a = torch.rand(C, device=gpu) + 0.5
+    mean = y.float().mean((0, 1, 2))
+    rstd = torch.rsqrt(y.float().var((0, 1, 2), unbiased=False) + 1e-5)
+    b = torch.randn(C, device=gpu) * 0.3 - mean * a
+    w = torch.randn(Co, C, 3, 3, device=gpu) / (9 * C) ** 0.5
+    wf = torch.empty(Co * 9 * C, dtype=torch.bfloat16, device=gpu)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w, wf, wd)
+    dy = (torch.randn(N * H * H, Co, device=gpu) * 0.1).to(torch.bfloat16)
+    g_f, part = K.conv_dgrad_bn(dy, wd, N, H, H, C, Co, y, a, b, mean, rstd, pool)
+    fused = native.kernels().ddpx_conv_dgrad_parts(N, H, H, C, Co, -1) > 0
+    assert (part is not None) == fused
+    g_u = K.conv_dgrad(dy, wd, N, H, H, C, Co)
+    assert torch.equal(g_f, g_u)
+    dg_f, db_f, dg_u, db_u = (torch.empty(C, device=gpu) for _ in range(4))
+    dz_f = K.bn_backward(g_f, y, a, b, mean, rstd, N, Hy, Hy, C, pool, dgamma=dg_f, dbeta=db_f, part=part)
+    dz_u = K.bn_backward(g_u, y, a, b, mean, rstd, N, Hy, Hy, C, pool, dgamma=dg_u, dbeta=db_u)
+    assert torch.allclose(db_f, db_u, rtol=1e-4, atol=1e-4 * db_u.abs().max().item())
+    assert torch.allclose(dg_f, dg_u, rtol=1e-4, atol=1e-4 * dg_u.abs().max().item())
+    assert _rel(dz_f, dz_u) < 1e-3
