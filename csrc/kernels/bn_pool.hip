@@ -801,6 +801,17 @@ DDPX_API int ddpx_bn_bwd_tail(const void* gout, const void* y, const float* a, c
   return (int)hipGetLastError();
 }
 
+// SyncBatchNorm with the pass-1 partials from the data-gradient epilogue: sums[2][C] (M = 1) and the local
+// dgamma / dbeta, as ddpx_bn_bwd_sums without its reduce pass.
+DDPX_API int ddpx_bn_bwd_sums_from_part(const float* part, int B, int C, float* sums, void* dgamma, void* dbeta,
+                                        int out_bf16, int accumulate, hipStream_t s) {
+  if (C % 8 || C > 512 || B < 1) return -1;
+  launch_bwd_finalize(part, B, C, 1, sums, sums + C, dgamma, dbeta, out_bf16, accumulate,
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, s);
+  return (int)hipGetLastError();
+}
+
 DDPX_API int ddpx_bn_bwd_apply(const void* gout, const void* y, const float* a, const float* b, const float* mean,
                                const float* rstd, const float* c1, const float* c2, int N, int H, int W, int C,
                                int pool, int relu, void* dy, hipStream_t s) {

@@ -139,22 +139,29 @@ def bn_finalize_sync(stats, T, BM, M, bn_mod, a, b, mean, rstd, comm):
 
 
 def bn_backward_sync(gout, y, a, b, mean, rstd, N, H, W, C, pool, comm, dgamma=None, dbeta=None,
-                     accumulate=False):
+                     accumulate=False, part=None):
     """SyncBatchNorm backward: local (sum dy, sum dy*xhat) -> all-reduce -> dy with the global means;
-    dgamma / dbeta stay local (DDP averages them, as torch's SyncBatchNorm)."""
+    dgamma / dbeta stay local (DDP averages them, as torch's SyncBatchNorm).  ``part``: the local pass-1
+    partials from the data gradient's epilogue (``conv_dgrad_bn``), as in ``bn_backward``."""
     _nhwc(gout, "gout", C)
     _nhwc(y, "y", C)
     lib = native.kernels()
     dev = y.device
-    B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
-    part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
     sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
     gdt = dgamma.dtype if dgamma is not None else torch.float32
     s = native.stream_handle()
-    native.check(lib.ddpx_bn_bwd_sums(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
-                                      rstd.data_ptr(), N, H, W, C, int(pool), 1, part.data_ptr(), sums.data_ptr(),
-                                      native.ptr(dgamma), native.ptr(dbeta), int(gdt == torch.bfloat16),
-                                      int(accumulate), s), "ddpx_bn_bwd_sums")
+    if part is not None:
+        pt, B = part
+        native.check(lib.ddpx_bn_bwd_sums_from_part(pt.data_ptr(), B, C, sums.data_ptr(), native.ptr(dgamma),
+                                                    native.ptr(dbeta), int(gdt == torch.bfloat16), int(accumulate),
+                                                    s), "ddpx_bn_bwd_sums_from_part")
+    else:
+        B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
+        pt = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
+        native.check(lib.ddpx_bn_bwd_sums(gout.data_ptr(), y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                          rstd.data_ptr(), N, H, W, C, int(pool), 1, pt.data_ptr(), sums.data_ptr(),
+                                          native.ptr(dgamma), native.ptr(dbeta), int(gdt == torch.bfloat16),
+                                          int(accumulate), s), "ddpx_bn_bwd_sums")
     comm.allreduce_(sums, op="sum")
     native.check(lib.ddpx_scale_f32(sums.data_ptr(), 2 * C, 1.0 / (comm.world_size * N * H * W), s), "ddpx_scale_f32")
     dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)

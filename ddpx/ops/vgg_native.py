@@ -143,7 +143,7 @@ def _backward(model, saved, last, dl, grad_out):
 
     def dgrad(dy, wd, bi, N, H, W, C, Co):
         """g of the block below, with its BatchNorm backward sums from the GEMM epilogue when possible."""
-        if _BN_BWD_FUSE and comm is None:
+        if _BN_BWD_FUSE:
             _, yp, ap, bp, mp, rp, _, poolp = saved[bi - 1]
             return K.conv_dgrad_bn(dy, wd, N, H, W, C, Co, yp, ap, bp, mp, rp, poolp)
         return K.conv_dgrad(dy, wd, N, H, W, C, Co), None
@@ -158,7 +158,7 @@ def _backward(model, saved, last, dl, grad_out):
             dgam, accg = flat.grad_target(bn.weight)
             dbet, _ = flat.grad_target(bn.bias)
             dy = K.bn_backward_sync(g, y, a, b, mean, rstd, N, H, W, Co, pool, comm, dgamma=dgam, dbeta=dbet,
-                                    accumulate=accg)
+                                    accumulate=accg, part=gpart)
             flat.grad_done(bn.weight)
             flat.grad_done(bn.bias)
         elif sg is not None:

@@ -86,6 +86,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_bn_bwd_apply", I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P)
     _sig(lib, "ddpx_bn_bwd_blocks", I, I, I, I, I)
     _sig(lib, "ddpx_bn_bwd", I, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, I, P, P, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_bn_bwd_sums_from_part", I, P, I, I, P, P, P, I, I, P)
     _sig(lib, "ddpx_bn_bwd_tail", I, P, P, P, P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, F, F,
          P)
     _sig(lib, "ddpx_bias_act_bwd", I, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P)
