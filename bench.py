@@ -328,7 +328,7 @@ def build_ddpx(args, device, world, comm=None):
     # single process: the SGD update may be fused into the kernels that produce each gradient
     opt = SGD(model.parameters(), lr=0.4, momentum=0.9, weight_decay=5e-4,
               capturable=not (args.no_graph or cpu),
-              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not fp32))
+              fused_backward=(world == 1 and not args.ddp_single and bool(args.fused_optimizer) and not cpu))
     net = model
     if comm is not None:
         net = DistributedDataParallel(model, comm=comm, bucket_cap_mb=args.bucket_cap_mb,

@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(NT)
 gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int kchunk, float* __restrict__ C,
                     int ldc, long split_stride, const float* __restrict__ bias, const float* __restrict__ mask,
                     int flags, int tiles_m, int tiles_n, unsigned a_bytes, unsigned b_bytes,
-                    float* __restrict__ stats) {
+                    float* __restrict__ stats, SgdArgs sgd) {
   constexpr int A_SUB = BM * 64, B_SUB = BN * 64, SLOT = A_SUB + B_SUB;
   constexpr int LW = (BM + BN) * 64 / 1024 / 4;  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
@@ -407,6 +407,74 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
     }
   }
   float* out = (flags & F_SPLIT) ? C + (size_t)z * split_stride : C;
+  if (sgd.p && !(flags & F_SPLIT)) {
+    // fused optimizer (single-process weight gradients): the tile's gradient updates the parameter it belongs to
+    // right here, with sgd_apply's fma sequence (bitwise the flat SGD's); the gradient is never stored.  The
+    // accumulators are staged through the (now idle) LDS ring in row parts so every thread streams 16-B vectors
+    // of the master / momentum rows (per-element 4-B accesses ran the update at a fraction of the HBM rate).
+    constexpr int TLD = BN + 4;
+    constexpr int EH = (BM * TLD * 4 <= STAGES * SLOT) ? 1 : 2;
+    constexpr int BMH = BM / EH;
+    static_assert(BMH * TLD * 4 <= STAGES * SLOT, "SGD epilogue staging does not fit the ring");
+    constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BMH / RSTEP, CH = NV < 4 ? NV : 4;
+    float* T = reinterpret_cast<float*>(smem);
+    const float slr = *sgd.lr;
+    const bool has_mom = sgd.mom != 0.f;
+    const int cq = tid % Q, r0 = tid / Q;
+    const int col = n0 + 4 * cq;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < EH; ++h) {
+      __syncthreads();  // the ring (h = 0) / the previous part's reads (h = 1) are done
+      if (wm == h || EH == 1) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = (EH == 1 ? wm * (BM / 2) : 0) + i * 16 + lr * 4 + e;
+              T[r * TLD + wn * (BN / 2) + j * 16 + lc] = acc[i][j][e];
+            }
+      }
+      __syncthreads();
+      const int mh = m0 + h * BMH;
+#pragma unroll
+      for (int i0 = 0; i0 < NV; i0 += CH) {
+        f32x4 pv[CH], bv[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int row = mh + r0 + (i0 + i) * RSTEP;
+          pv[i] = bv[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          if (row >= M || col >= N) continue;
+          const size_t o = (size_t)row * ldc + col;
+          pv[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sgd.p + o));
+          if (has_mom) bv[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sgd.buf + o));
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int r = r0 + (i0 + i) * RSTEP;
+          const int row = mh + r;
+          if (row >= M || col >= N) continue;
+          const size_t o = (size_t)row * ldc + col;
+          const f32x4 g = *reinterpret_cast<const f32x4*>(T + r * TLD + 4 * cq);
+          f32x4 po, bo;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float d = fmaf(sgd.wd, pv[i][q], g[q]);
+            if (has_mom) d = fmaf(sgd.mom, bv[i][q], d);
+            bo[q] = d;
+            po[q] = fmaf(-slr, d, pv[i][q]);
+          }
+          __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(sgd.p + o));
+          if (has_mom) __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>(sgd.buf + o));
+          if (sgd.shadow)
+            *reinterpret_cast<u32x2*>(sgd.shadow + o) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -471,7 +539,7 @@ static int f32_block() {
 template <int BM, int BN, int AM, int BMD>
 static void launch(const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C, int ldc,
                    long split_stride, const float* bias, const float* mask, int flags, hipStream_t s,
-                   unsigned a_bytes, unsigned b_bytes, float* stats = nullptr) {
+                   unsigned a_bytes, unsigned b_bytes, float* stats = nullptr, SgdArgs sgd = SgdArgs{}) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   int kchunk = (K + splits - 1) / splits;
   kchunk = (kchunk + BK - 1) / BK * BK;
@@ -482,19 +550,19 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
   if (f32_dma() && a_bytes && b_bytes) {
     if (plain)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
-                         N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+                         N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
     else if (f32_block() == 2)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 2>), dim3(nwg), dim3(NT), 0, s, A,
-                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
     else if (f32_block() == 4)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 4>), dim3(nwg), dim3(NT), 0, s, A,
-                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
     else if (f32_block() == 8)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages, 8>), dim3(nwg), dim3(NT), 0, s, A,
-                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+                         B, M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
     else
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B,
-                         M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats);
+                         M, N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
     return;
   }
   if (plain)
@@ -508,12 +576,12 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
 template <int AM, int BMD>
 static void dispatch_tile(int tile, const Operand& A, const Operand& B, int M, int N, int K, int splits, float* C,
                           int ldc, long ss, const float* bias, const float* mask, int flags, hipStream_t s,
-                          unsigned ab, unsigned bb, float* stats = nullptr) {
+                          unsigned ab, unsigned bb, float* stats = nullptr, SgdArgs sgd = SgdArgs{}) {
   switch (tile) {
-    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
-    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
-    case 3: launch<64, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
-    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats); break;
+    case 0: launch<128, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats, sgd); break;
+    case 1: launch<128, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats, sgd); break;
+    case 3: launch<64, 128, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats, sgd); break;
+    default: launch<64, 64, AM, BMD>(A, B, M, N, K, splits, C, ldc, ss, bias, mask, flags, s, ab, bb, stats, sgd); break;
   }
 }
 
@@ -1326,6 +1394,25 @@ DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const 
     default:
       return -5;
   }
+  return (int)hipGetLastError();
+}
+
+// Weight gradient dW [N][K] = dy^T x (dy [M][N], x [M][K], both DENSE_OC) applied straight to the parameter by an
+// SGD epilogue (single process, SGD(fused_backward)): no gradient stored.  LDS-DMA core only (-6 otherwise).
+DDPX_API int ddpx_f32_wgrad_sgd(const float* dy, int ldy, const float* x, int ldx, int M, int N, int K, int tile,
+                                float* sgd_p, float* sgd_buf, void* sgd_shadow, const float* lr, float mom, float wd,
+                                hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!f32_dma()) return -6;
+  if (!sgd_p || !lr || (mom != 0.f && !sgd_buf)) return -1;
+  if (N % 4 || K % 4 || ldy % 4 || ldx % 4) return -3;
+  // output [N rows][K cols]: A = dy^T (rows = N, reduction = M), B = x (cols = K)
+  Operand A{dy, ldy, N, 0, 0, 0, 1}, B{x, ldx, K, 0, 0, 0, 1};
+  const unsigned ab = operand_bytes(DENSE_OC, ldy, N, M, 0, 0), bb = operand_bytes(DENSE_OC, ldx, K, M, 0, 0);
+  if (!ab || !bb) return -4;
+  if (tile < 0) tile = auto_tile(N, K, 1);
+  dispatch_tile<DENSE_OC, DENSE_OC>(tile, A, B, N, K, M, 1, sgd_p, K, 0, nullptr, nullptr, 0, s, ab, bb, nullptr,
+                                    SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, lr, mom, wd});
   return (int)hipGetLastError();
 }
 

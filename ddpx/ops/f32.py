@@ -41,6 +41,7 @@ for _sig in (
         ("ddpx_f32_conv_fwd_stats", _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
+        ("ddpx_f32_wgrad_sgd", _I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P),
         ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
         ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P),
@@ -118,6 +119,23 @@ def linear_wgrad(dy, x, out, accumulate=False):
     K = x.shape[1]
     _req(out.shape == (N, K) and out.is_contiguous(), "linear_wgrad: bad output")
     gemm(DENSE_OC, dy, N, DENSE_OC, x, K, N, K, M, out, accumulate=accumulate)
+
+
+def linear_wgrad_sgd(dy, x, sgd):
+    """W -= SGD(dy^T x) in the weight-gradient GEMM's epilogue (fused optimizer, single process); ``sgd`` =
+    FlatParams.fused_spec(W).  False when the core cannot (register-staged core): the caller stores the
+    gradient instead."""
+    M, N = dy.shape
+    K = x.shape[1]
+    p, buf, sh, lr, mom, wd = sgd
+    _req(p.numel() == N * K, "linear_wgrad_sgd: parameter size")
+    r = native.kernels().ddpx_f32_wgrad_sgd(dy.data_ptr(), N, x.data_ptr(), K, M, N, K, -1, p.data_ptr(),
+                                             native.ptr(buf), native.ptr(sh), lr.data_ptr(), float(mom), float(wd),
+                                             native.stream_handle())
+    if r == -6:
+        return False
+    native.check(r, "ddpx_f32_wgrad_sgd")
+    return True
 
 
 def colsum(x, out, accumulate=False):
@@ -711,6 +729,20 @@ def _mlp_backward(model, hs, dl, grad_out):
     flat.grad_done(last.bias)
     for i in range(len(lins) - 2, -1, -1):
         lin = lins[i]
+        sw = flat.fused_spec(lin.weight)
+        if sw is not None:
+            # single process, SGD(fused_backward): the data gradient reads W_i first, then the weight-gradient
+            # GEMM updates W_i in its epilogue (no gradient stored, no separate optimizer pass over W_i)
+            dz_next = linear_dgrad(dz, lin.weight, mask=hs[i]) if i > 0 else None
+            if linear_wgrad_sgd(dz, hs[i], sw):
+                flat.mark_updated(lin.weight)
+            else:
+                _grad_write(flat, lin.weight, lambda o, ac: linear_wgrad(dz, hs[i], o, ac))
+            _grad_write(flat, lin.bias, lambda o, ac: colsum(dz, o, ac))
+            if i > 0:
+                flat.release(lin.weight)
+                dz = dz_next
+            continue
         _grad_write(flat, lin.weight, lambda o, ac: linear_wgrad(dz, hs[i], o, ac))
         _grad_write(flat, lin.bias, lambda o, ac: colsum(dz, o, ac))
         if i > 0:

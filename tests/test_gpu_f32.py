@@ -662,3 +662,35 @@ def test_deepnn_fp32_runs_winograd_layers(gpu):
     ddpx.prepare_model(m, gpu)
     plan = f32._deepnn_plan(m)
     assert plan.uf[0] is None and all(u is not None for u in plan.uf[1:]), [u is not None for u in plan.uf]
+
+
+def test_mlp_fp32_fused_optimizer_bitwise(gpu):
+    """SGD(fused_backward=True) on the fp32 MLP: the hidden layers' weight-gradient GEMMs apply the update in their
+    epilogue (ddpx_f32_wgrad_sgd) - bitwise the unfused step (stored gradient + flat SGD), over 3 steps."""
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.optim.sgd import SGD
+    models = []
+    for _ in range(2):
+        torch.manual_seed(4)
+        m = build_model("mlp", hidden=512, dtype="fp32", device=gpu, kernels="native")
+        ddpx.prepare_model(m, gpu)
+        models.append(m)
+    a, b = models
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, fused_backward=True)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    flat = a.linears()[0].weight._ddpx_flat
+    for _ in range(3):
+        x = torch.rand(64, 3, 32, 32, device=gpu)
+        t = torch.randint(0, 10, (64,), device=gpu)
+        for m, o in ((a, oa), (b, ob)):
+            o.sync_lr()
+            o.zero_grad()
+            loss, logits = m.forward_loss(x, t)
+            assert logits is None  # the native fp32 path
+            loss.backward()
+            if m is a:
+                assert flat.updated[flat.index[id(a.linears()[0].weight)]], "fused update did not run"
+            o.step()
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(p, q), n
