@@ -642,6 +642,34 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   out[i] = accumulate ? out[i] + acc : acc;
 }
 
+// Split-K finish of a [M][N] fp32 GEMM with its epilogue: out = relu?(sum_z part[z] + bias[n]) * (mask > 0)?,
+// 16-B vectors (N % 4 == 0), slabs summed in split order.
+__global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                          float* __restrict__ out, const float* __restrict__ bias,
+                                                          const float* __restrict__ mask, int relu) {
+  const long nv = (long)M * N / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nv) return;
+  const long n4 = (long)M * N / 4;
+  f32x4 acc = reinterpret_cast<const f32x4*>(part)[i];
+  for (int z = 1; z < S; ++z) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(part)[z * n4 + i];
+    acc += v;
+  }
+  const int col = (int)((i * 4) % N);
+  f32x4 mk = {1.f, 1.f, 1.f, 1.f};
+  if (mask) mk = reinterpret_cast<const f32x4*>(mask)[i];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v = acc[q];
+    if (bias) v += bias[col + q];
+    if (relu) v = fmaxf(v, 0.f);
+    if (mask && !(mk[q] > 0.f)) v = 0.f;
+    acc[q] = v;
+  }
+  reinterpret_cast<f32x4*>(out)[i] = acc;
+}
+
 // ------------------------------------------------------------------ BatchNorm (NHWC [P][C], fp32)
 // Threads: channel c = tid % C, row group g = tid / C (G = blockDim / C groups).  blockDim = max(256, C).
 __device__ __forceinline__ float block_group_sum(float v, float* red, int C, int G, int tid) {
@@ -1418,6 +1446,15 @@ DDPX_API int ddpx_f32_wgrad_sgd(const float* dy, int ldy, const float* x, int ld
 
 DDPX_API int ddpx_f32_splitk_reduce(const float* part, int S, int64_t n, float* out, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nblk(n)), dim3(256), 0, s, part, S, (long)n, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_splitk_epi(const float* part, int S, int M, int N, float* out, const float* bias,
+                                 const float* mask, int relu, hipStream_t s) {
+  if (N % 4 || S < 1) return -1;
+  const long nv = (long)M * N / 4;
+  hipLaunchKernelGGL(splitk_epi_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, part, S, M, N, out, bias,
+                     mask, relu);
   return (int)hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ for _sig in (
         ("ddpx_dropout_fwd_f32", _I, _P, _P, _I64, _F, _P, _P, _P),
         ("ddpx_f32_colsum", _I, _P, _I, _I, _P, _I, _P),
         ("ddpx_f32_wgrad_sgd", _I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P),
+        ("ddpx_f32_splitk_epi", _I, _P, _I, _I, _I, _P, _P, _P, _I, _P),
         ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
         ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P),
@@ -91,6 +92,27 @@ def gemm(amode, a, lda, bmode, b, ldb, M, N, K, out, ldc=None, bias=None, mask=N
 
 
 # ---------------------------------------------------------------------------------------------- Linear
+# DDPX_F32_SPLITK (default 2): the batch-row (M <= 1024) Linear forward / data gradient as 2 in-grid K splits on
+# 64x64 tiles (1024 workgroups instead of 512: 4 per CU) and one finishing pass with the epilogue
+# (profiles/r5_mlp32: fc0 / fc1 152 / 178 -> 129 / 153 us + 7 us); 1 = one pass.  The split changes the summation
+# into two half-length chains added at the end (closer to fp64, not bitwise the one-pass result).
+import os as _os_lin  # noqa: E402
+
+_F32_SPLITK = int(_os_lin.environ.get("DDPX_F32_SPLITK", "2"))
+
+
+def _splitk_linear(amode, a, lda, bmode, b, ldb, M, N, K, bias=None, mask=None, relu=False):
+    S = _F32_SPLITK
+    if S < 2 or M > 1024 or N % 4 or K < 1024 or (M * N) < (1 << 20):
+        return None
+    part = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
+    gemm(amode, a, lda, bmode, b, ldb, M, N, K, part, tile=2, splits=S, split_stride=M * N)
+    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    _call("ddpx_f32_splitk_epi", part.data_ptr(), S, M, N, out.data_ptr(), native.ptr(bias), native.ptr(mask),
+          int(relu))
+    return out
+
+
 def linear_fwd(x, w, bias=None, relu=False):
     """y = x W^T + b [relu] — x [M,K], W [N,K] (torch layout)."""
     M, K = x.shape
@@ -98,6 +120,9 @@ def linear_fwd(x, w, bias=None, relu=False):
     _f32(x, "x")
     _f32(w, "w")
     _req(w.shape[1] == K, "linear_fwd: shape mismatch")
+    y = _splitk_linear(DENSE_KC, x, K, DENSE_KC, w, K, M, N, K, bias=bias, relu=relu)
+    if y is not None:
+        return y
     y = torch.empty((M, N), dtype=torch.float32, device=x.device)
     gemm(DENSE_KC, x, K, DENSE_KC, w, K, M, N, K, y, bias=bias, relu=relu)
     return y
@@ -108,6 +133,9 @@ def linear_dgrad(dy, w, mask=None):
     M, N = dy.shape
     K = w.shape[1]
     _f32(dy, "dy")
+    dx = _splitk_linear(DENSE_KC, dy, N, DENSE_OC, w, K, M, K, N, mask=mask)
+    if dx is not None:
+        return dx
     dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
     gemm(DENSE_KC, dy, N, DENSE_OC, w, K, M, K, N, dx, mask=mask)
     return dx
