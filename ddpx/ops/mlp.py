@@ -32,6 +32,34 @@ from .head import head_backward, head_forward
 _PAIR_WGRAD = os.environ.get("DDPX_WGRAD_PAIR", "1") != "0"
 # DDPX_FP8_WGRAD=1: MX-FP8 weight-gradient GEMMs too (default: MX-FP8 forward GEMMs, bf16 backward)
 _FP8_WGRAD = os.environ.get("DDPX_FP8_WGRAD", "0") == "1"
+# DDPX_FP8_DGRAD=1 (fp8 models): the hidden layers' data gradients on MX-FP8 too - dY row-quantised, W_l quantised
+# transposed (32-blocks along its output dimension, the data gradient's K) every step, the ReLU mask in the MX
+# GEMM's epilogue.  Opt-in: at N = 1 the per-step transposed quantisation of W costs about what the 1.8x faster
+# GEMM saves (profiles/r5_fp8/NOTES.md)
+_FP8_DGRAD = os.environ.get("DDPX_FP8_DGRAD", "0") == "1"
+
+
+def _dgrad_mx8(dpre, w_bf16, h, bias_grad=None, bias_acc=False, bias_sgd=None):
+    """dX = (dpre W) * (h > 0) on MX-FP8, plus the bias gradient of the layer below (stored / accumulated into
+    ``bias_grad`` or applied through ``bias_sgd``), as G.linear_dgrad's epilogue does on the bf16 pipe."""
+    from . import fp8 as F8
+    from .elementwise import colsum_bf16, sgd_flat_
+    wq = F8.quant(w_bf16, F8.E4M3, rows=False, cols=True)  # W^T [in][out], blocks along out
+    dq = F8.quant(dpre, F8.E4M3)                            # dpre [batch][out], blocks along out
+    dx = F8.gemm(dq, wq, epi=G.EPI_RELUMASK_BF16, aux=h)
+    if bias_sgd is not None:
+        p, buf, sh, lr, mom, wd = bias_sgd
+        g = torch.empty(p.numel(), dtype=torch.float32, device=dx.device)
+        colsum_bf16(dx, g)
+        sgd_flat_(p, buf if buf is not None else torch.zeros_like(p), g, sh, lr, mom, wd)
+    elif bias_grad is not None:
+        if bias_grad.dtype == torch.float32:
+            colsum_bf16(dx, bias_grad, accumulate=bias_acc)
+        else:
+            g = torch.empty(bias_grad.numel(), dtype=torch.float32, device=dx.device)
+            colsum_bf16(dx, g)
+            bias_grad.copy_(g + bias_grad.float() if bias_acc else g)
+    return dx
 # DDPX_DGRAD_FUSE=1: fc1's data gradient inside the pair's launch (csrc/include/ddpx_wsgd_dgrad.h, fc1's bf16
 # weight copy ping-ponged between two buffers).  Opt-in: measured slower than the two launches on MI355X
 # (toy step 0.2905 vs 0.2379-0.2391 ms, one box, profiles/r4_dgfuse): the pair's math waves are bound by their
@@ -129,6 +157,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
     wl, bl = ps[-1]
     bprev = ps[L - 1][1]
     fused = flat.fused_spec(wl) is not None
+    fp8_dgrad = _FP8_DGRAD and bool(getattr(model, "fp8", False)) and hs[L].is_cuda
     dpre = torch.empty_like(hs[L])
     if fused:
         # optimizer fused into backward: each kernel that produces a gradient applies the SGD
@@ -137,7 +166,8 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                       sgd_w=flat.fused_spec(wl), sgd_b=flat.fused_spec(bl), sgd_prev=flat.fused_spec(bprev))
         for p in (wl, bl, bprev):
             flat.mark_updated(p)
-        if L == 2 and not saved8 and _PAIR_WGRAD and _DGRAD_FUSE and _fused_dgrad(model, flat, ps, hs, dpre):
+        if L == 2 and not saved8 and not fp8_dgrad and _PAIR_WGRAD and _DGRAD_FUSE and \
+                _fused_dgrad(model, flat, ps, hs, dpre):
             return
         deferred = None  # layer 1's update, launched together with layer 0's (one warp-specialised launch)
         for l in range(L - 1, -1, -1):
@@ -146,7 +176,10 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             if l > 0:  # data gradient first: it must read W_l before the fused update rewrites it
                 bp = ps[l - 1][1]
                 flat.normalize_pingpong()  # (the unfused update writes the main bf16 copy)
-                dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
+                if fp8_dgrad:
+                    dnext = _dgrad_mx8(dpre, flat.shadow_of(w), hs[l], bias_sgd=flat.fused_spec(bp))
+                else:
+                    dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
                 flat.mark_updated(bp)
             if l == 1 and not saved8 and _PAIR_WGRAD:
                 deferred = (dpre, hs[1], flat.fused_spec(w), w)
@@ -198,8 +231,11 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             bp = ps[l - 1][1]
             dbl, accl = flat.grad_target(bp)
             # ReLU backward + bias gradient of layer l-1 fused into the dgrad epilogue
-            dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_grad=dbl,
-                                   bias_grad_accumulate=accl)
+            if fp8_dgrad:
+                dnext = _dgrad_mx8(dpre, flat.shadow_of(w), hs[l], bias_grad=dbl, bias_acc=accl)
+            else:
+                dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_grad=dbl,
+                                       bias_grad_accumulate=accl)
             flat.release(w)  # W_l's last read: a side-stream update of its bucket may start now
             flat.grad_done(bp)
             dpre = dnext

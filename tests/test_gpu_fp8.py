@@ -221,3 +221,35 @@ def test_mlp_fp8_weight_copy_written_by_optimizer(gpu, fused, from_opt):
                 torch.cuda.synchronize()
                 assert torch.equal(q, ref.q) and torch.equal(s, ref.s), (step, lin)
     assert torch.isfinite(loss).item()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_mlp_fp8_dgrad_step_tracks_bf16(gpu, fused, monkeypatch):
+    """DDPX_FP8_DGRAD=1: the hidden data gradients on MX-FP8 (W quantised transposed per step) - the step's
+    gradients / updates stay close to the bf16 step's, with the fused optimizer and with stored gradients."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.ops import mlp as mlp_ops
+    from ddpx.optim.sgd import SGD
+    monkeypatch.setattr(mlp_ops, "_FP8_DGRAD", True)
+    torch.manual_seed(5)
+    a, b = MLP(hidden=1024), MLP(hidden=1024)
+    b.load_state_dict(a.state_dict())
+    a.fp8 = True
+    for m in (a, b):
+        ddpx.prepare_model(m, gpu)
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, fused_backward=fused)
+    ob = SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, fused_backward=fused)
+    w0 = [p.detach().clone() for p in b.parameters()]
+    x = torch.rand(256, 3072, device=gpu).to(torch.bfloat16)
+    t = torch.randint(0, 10, (256,), device=gpu)
+    for m, o in ((a, oa), (b, ob)):
+        o.sync_lr()
+        o.zero_grad()
+        loss, _ = m.forward_loss(x, t)
+        loss.backward()
+        o.step()
+    for (n, p), q, p0 in zip(a.named_parameters(), b.parameters(), w0):
+        du, dr = (p - p0).float().flatten(), (q - p0).float().flatten()
+        cos = torch.nn.functional.cosine_similarity(du, dr, dim=0).item()
+        assert cos > 0.97, (n, cos)
