@@ -82,7 +82,9 @@ constexpr int kQcR = 128, kQcC = 128;
 __global__ void __launch_bounds__(512) quant_cols_kernel(const unsigned short* __restrict__ x, int R, int C, int ld,
                                                          unsigned char* __restrict__ qt, int ldq,
                                                          unsigned char* __restrict__ st, int e5m2) {
-  __shared__ unsigned short tile[kQcR][kQcC + 2];
+  // row r sits at column offset 2 (r / 32): the 4 32-row blocks a wave reads in one instruction land in 4 different
+  // banks (a plain row stride put them all on one)
+  __shared__ unsigned short tile[kQcR][kQcC + 8];
   const int r0 = blockIdx.y * kQcR, c0 = blockIdx.x * kQcC;
   const int t = threadIdx.x;
   // load: 128 rows x 16 chunks of 8 bf16; 512 threads x 4 chunks (16 consecutive threads read one row's 256 B)
@@ -92,7 +94,7 @@ __global__ void __launch_bounds__(512) quant_cols_kernel(const unsigned short* _
     const int rr = chunk >> 4, cc = (chunk & 15) * 8;
     u32x4 w = (u32x4){0u, 0u, 0u, 0u};
     if (r0 + rr < R && c0 + cc < C) w = *reinterpret_cast<const u32x4*>(x + (size_t)(r0 + rr) * ld + c0 + cc);
-    unsigned* d = reinterpret_cast<unsigned*>(&tile[rr][cc]);
+    unsigned* d = reinterpret_cast<unsigned*>(&tile[rr][cc + 2 * (rr >> 5)]);
     d[0] = w[0];
     d[1] = w[1];
     d[2] = w[2];
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(512) quant_cols_kernel(const unsigned short* _
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
-    v[i] = bf2f(tile[q * 32 + i][cl]);
+    v[i] = bf2f(tile[q * 32 + i][cl + 2 * q]);
     amax = fmaxf(amax, fabsf(v[i]));
   }
   const float maxv = e5m2 ? kMaxE5M2 : kMaxE4M3;
