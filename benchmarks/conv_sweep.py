@@ -38,11 +38,17 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--out", default=None)
     ap.add_argument("--net", default="vgg", choices=["vgg", "deepnn"])
+    ap.add_argument("--cfgs", default="", help="comma list of tile configs (default 0-15)")
+    ap.add_argument("--layers", default="", help="comma list of layer indices (default all)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N = a.batch
     res = []
-    for (Ci, Co, H) in (LAYERS if a.net == "vgg" else DEEPNN_LAYERS):
+    cfgs = [int(c) for c in a.cfgs.split(",") if c] or list(range(16))
+    layers = LAYERS if a.net == "vgg" else DEEPNN_LAYERS
+    if a.layers:
+        layers = [layers[int(i)] for i in a.layers.split(",")]
+    for (Ci, Co, H) in layers:
         Cp = K.padded_channels(Ci)
         x = (torch.rand(N, H, H, Cp, device=dev) * 2 - 1).to(torch.bfloat16)
         w = torch.randn(Co, Ci, 3, 3, device=dev) * 0.05
@@ -56,12 +62,12 @@ def main():
         xt = x[..., :Ci].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         wt = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         row["miopen_fwd"] = round(timeit(lambda: F.conv2d(xt, wt, padding=1)), 1)
-        for cfg in range(16):
+        for cfg in cfgs:
             row[f"fwd{cfg}"] = round(timeit(lambda: K.conv_fwd(x, wf, Co, stats=True, tile=cfg)), 1)
             row[f"dgrad{cfg}"] = round(timeit(lambda: K.conv_dgrad(dy, wd, N, H, H, Cp, Co, tile=cfg)), 1)
             row[f"wgrad{cfg}"] = round(timeit(lambda: K.conv_wgrad(dy, x, Co, Ci, out=dw, tile=cfg)), 1)
         for kind in ("fwd", "dgrad", "wgrad"):
-            best = min(range(16), key=lambda c: row[f"{kind}{c}"])
+            best = min(cfgs, key=lambda c: row[f"{kind}{c}"])
             row[f"best_{kind}"] = best
             row[f"best_{kind}_tflops"] = round(flop / row[f"{kind}{best}"] / 1e6, 1)
         res.append(row)

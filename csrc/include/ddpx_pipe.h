@@ -685,7 +685,10 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 // combine and epilogue (an s_barrier waits only for waves that have not ended).
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
           bool SGDPF = false, bool SK = false, int LW = 0>
-__global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
+// the 2-deep 128x128 rings (configs 21 / 22) are built for two workgroups per CU: held to that register budget
+__global__ void __launch_bounds__((NW + LW) * 64)
+__attribute__((amdgpu_waves_per_eu((BM == 128 && BN == 128 && STAGES == 2 && LW == 0) ? NW / 2 : 1)))
+gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
   constexpr int BK = 64 * KSUB;
@@ -970,10 +973,10 @@ __global__ void __launch_bounds__((NW + LW) * 64) gemm_pipe_kernel(Params p) {
         break;
       case EPI_BNBWD_BF16:
         // conv data-gradient kernels, only the tiles where the fused sums measured faster than the separate
-        // reduce pass (256x128 / 3 stages and 128x128 / 4 stages / 8 waves, profiles/r5_vgg/NOTES.md): the
+        // reduce pass (256x128 / 3 stages and 128x128 / 4 or 2 stages / 8 waves, profiles/r5_vgg/NOTES.md): the
         // others do not carry the epilogue's registers
         if constexpr (LW == 0 && AMODE == MODE_IM2COL_BWD && NW == 8 &&
-                      ((BM == 256 && BN == 128 && STAGES == 3) || (BM == 128 && BN == 128 && STAGES == 4))) {
+                      ((BM == 256 && BN == 128 && STAGES == 3) || (BM == 128 && BN == 128 && STAGES != 3))) {
           float s2[4] = {0.f, 0.f, 0.f, 0.f};
           epilogue_bnbwd<BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch, s2);
           __syncthreads();
@@ -1082,18 +1085,18 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
 }
 
 // cfg 16 - 20: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products
-constexpr int kNumCfgs = 21;
+constexpr int kNumCfgs = 23;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
 static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
 
 // Row-parts the epilogue stages the tile in (BatchNorm statistics come out per part).
-static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : 1; }
+static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : (cfg == 21 || cfg == 22) ? 2 : 1; }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {
   static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
                                      {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
                                      {128, 128}, {128, 128}, {256, 128}, {128, 128}, {64, 128}, {128, 64},
-                                     {64, 64}};
+                                     {64, 64},   {128, 128}, {128, 128}};
   const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
@@ -1110,6 +1113,9 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     case 13: return launch<256, 256, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 64x128 each, 128 KiB
     case 14: return launch<128, 128, 3, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 96 KiB
     case 15: return launch<128, 128, 4, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each, 128 KiB
+    // 128x128 with a 2-deep ring (64 KiB): two workgroups per CU, one's epilogue / ring fill under the other's loop
+    case 21: return launch<128, 128, 2, AK, BKc, AMODE, BMODE, 4>(p, splits, s);   // 4 waves, 64x64 each
+    case 22: return launch<128, 128, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each
     case 16:  // warp-specialised (plain operands only)
       if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
         return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8, 1, false, false, 4>(p, splits, s);

@@ -32,7 +32,7 @@ namespace bn {
 // 64 threads (one wave) per channel: each lane merges a strided subset of tiles,
 // then a fixed-shape butterfly merges the lanes.
 __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
-  if (nb == 0.f) return;
+  if (nb <= 0.f) return;  // (a trailing epilogue part wholly past M: min(BM, M - t*BM) < 0)
   if (n == 0.f) { n = nb; mean = meanb; m2 = m2b; return; }
   const float nn = n + nb;
   const float d = meanb - mean;
@@ -122,6 +122,8 @@ finalize_kernel(const float* __restrict__ stats, int T, int BM, int M, int C, co
 // over S workgroups per 64-channel group, and the LAST workgroup of a group to finish (agent-scope ticket)
 // merges the S partials in split order: deterministic, and the hand-off is MI355X_MICROARCH "Valid forms" row 1
 // (sc1 stores drained by vmcnt(0) before the ticket, sc1 loads after it).  Tickets reset by their last arriver.
+// up to 32 splits (every split takes one ticket on the same address: 128 splits measured no faster), a lane's
+// tiles loaded 16 at a time (profiles/r5_conv/NOTES.md)
 constexpr int kMergeMaxC = 1024, kFinMaxS = 32, kBwdMaxS = 32;
 // Which merges use the two-level kernels: 0 both, 1 neither (the per-channel kernels above), 2 the backward sums
 // only (default).  Split, the forward statistics merge measured no faster (86.8 vs 87 us per VGG step) and the
@@ -139,7 +141,10 @@ static inline int merge_mode() {
   }
   return g_merge_mode;
 }
-static inline bool merge_legacy() { return merge_mode() != 0; }        // forward statistics
+// forward statistics: the default mode still splits the merge when the tile count is large (T >= 4096: VGG conv1
+// with the 128x128 forward tile's 64-row statistics, 8192 tiles: the per-channel kernel's strided loads took
+// 25.5 us there, profiles/r5_conv/NOTES.md)
+static inline bool merge_legacy(int T = 0) { return merge_mode() == 1 || (merge_mode() == 2 && T < 4096); }
 static inline bool merge_legacy_bwd() { return merge_mode() == 1; }    // backward sums
 __device__ int g_merge_tickets[2][kMergeMaxC / 64];
 __device__ float g_fin_scratch[kFinMaxS * 3 * kMergeMaxC];
@@ -188,6 +193,16 @@ finalize_split_kernel(const float* __restrict__ stats, int T, int BM, int M, int
   float n = 0.f, mu = 0.f, m2 = 0.f;
   const int step = 4 * S;
   int t = 4 * sp + w;
+  for (; t + 15 * step < T; t += 16 * step) {  // 16 tiles' loads in flight per lane
+    float tm[16], tq[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      tm[u] = stats[((size_t)(t + u * step) * 2) * C + cc];
+      tq[u] = stats[((size_t)(t + u * step) * 2 + 1) * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) chan_merge(n, mu, m2, (float)min(BM, M - (t + u * step) * BM), tm[u], tq[u]);
+  }
   for (; t + 3 * step < T; t += 4 * step) {
     float tm[4], tq[4];
 #pragma unroll
@@ -219,18 +234,20 @@ finalize_split_kernel(const float* __restrict__ stats, int T, int BM, int M, int
   // waves' states merge in wave order through LDS (a fixed tree: deterministic)
   {
     const unsigned bytes = (unsigned)((size_t)S * 3 * C * 4);
-    constexpr int PW = kFinMaxS / 4;
-    float v[PW][3];
-#pragma unroll
-    for (int u = 0; u < PW; ++u)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int sp2 = w + 4 * u;
-        v[u][k] = (cok && sp2 < S) ? ld_sc1(part, bytes, (unsigned)((((size_t)sp2 * 3 + k) * C + c) * 4)) : 0.f;
-      }
+    constexpr int PC = 8;  // partials per chunk, all loads of a chunk in flight together
     n = mu = m2 = 0.f;
+    for (int u0 = 0; 4 * u0 < S; u0 += PC) {
+      float v[PC][3];
 #pragma unroll
-    for (int u = 0; u < PW; ++u) chan_merge(n, mu, m2, v[u][0], v[u][1], v[u][2]);
+      for (int u = 0; u < PC; ++u)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int sp2 = w + 4 * (u0 + u);
+          v[u][k] = (cok && sp2 < S) ? ld_sc1(part, bytes, (unsigned)((((size_t)sp2 * 3 + k) * C + c) * 4)) : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < PC; ++u) chan_merge(n, mu, m2, v[u][0], v[u][1], v[u][2]);
+    }
     __syncthreads();  // wres reuse
     wres[w][0][lane] = n;
     wres[w][1][lane] = mu;
@@ -276,6 +293,16 @@ bwd_finalize_split_kernel(const float* __restrict__ part, int B, int C, int M, i
   float s1 = 0.f, s2 = 0.f;
   const int step = 4 * S;
   int k = 4 * sp + w;
+  for (; k + 15 * step < B; k += 16 * step) {  // 16 partials' loads in flight per lane
+    float a[16], q[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      a[u] = part[((size_t)(k + u * step) * 2) * C + cc];
+      q[u] = part[((size_t)(k + u * step) * 2 + 1) * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { s1 += a[u]; s2 += q[u]; }
+  }
   for (; k + 3 * step < B; k += 4 * step) {
     float a[4], q[4];
 #pragma unroll
@@ -306,18 +333,20 @@ bwd_finalize_split_kernel(const float* __restrict__ part, int B, int C, int M, i
   if (threadIdx.x == 0) __hip_atomic_store(&g_merge_tickets[1][cg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   {
     const unsigned bytes = (unsigned)((size_t)S * 2 * C * 4);
-    constexpr int PW = kBwdMaxS / 4;
-    float v[PW][2];
-#pragma unroll
-    for (int u = 0; u < PW; ++u)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int sp2 = w + 4 * u;
-        v[u][j] = (cok && sp2 < S) ? ld_sc1(sc, bytes, (unsigned)((((size_t)sp2 * 2 + j) * C + c) * 4)) : 0.f;
-      }
+    constexpr int PC = 8;
     s1 = s2 = 0.f;
+    for (int u0 = 0; 4 * u0 < S; u0 += PC) {
+      float v[PC][2];
 #pragma unroll
-    for (int u = 0; u < PW; ++u) { s1 += v[u][0]; s2 += v[u][1]; }
+      for (int u = 0; u < PC; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int sp2 = w + 4 * (u0 + u);
+          v[u][j] = (cok && sp2 < S) ? ld_sc1(sc, bytes, (unsigned)((((size_t)sp2 * 2 + j) * C + c) * 4)) : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < PC; ++u) { s1 += v[u][0]; s2 += v[u][1]; }
+    }
     __syncthreads();
     wres[w][0][lane] = s1;
     wres[w][1][lane] = s2;
@@ -684,7 +713,7 @@ DDPX_API void ddpx_bn_set_merge(int mode) { bn::g_merge_mode = mode < 0 || mode 
 DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
                               float* a, float* b, float* mean, float* rstd, hipStream_t s) {
-  if (training && C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+  if (training && C <= bn::kMergeMaxC && !bn::merge_legacy(T)) {
     const int S = bn::fin_splits(T);
     hipLaunchKernelGGL(bn::finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, stats, T, BM, M, C, S,
                        gamma, beta, rmean, rvar, nbt, momentum, eps, a, b, mean, rstd, (float*)nullptr);
@@ -700,7 +729,7 @@ DDPX_API int ddpx_bn_finalize(const float* stats, int T, int BM, int M, int C, c
 // [ws][2][C] and ddpx_bn_finalize(gathered, T = ws, BM = M, M = ws * M) merges them in rank order — the
 // same Chan merge on every rank, so every rank normalises with bitwise-identical statistics.
 DDPX_API int ddpx_bn_local_stats(const float* stats, int T, int BM, int M, int C, float* out, hipStream_t s) {
-  if (C <= bn::kMergeMaxC && !bn::merge_legacy()) {
+  if (C <= bn::kMergeMaxC && !bn::merge_legacy(T)) {
     const int S = bn::fin_splits(T);
     hipLaunchKernelGGL(bn::finalize_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, stats, T, BM, M, C, S,
                        (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr,

@@ -160,20 +160,34 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // profiles/r1_fdiv/conv_sweep_fdiv.json): the 8-wave 256x256 tile (cfg 13) wins every >= 128-channel
 // layer at 16x16 and 8x8 (fwd 512->512@8: 151 vs 198 us for 256x128); the 32x32 layers keep 256x128
 // (cfg 8); 4x4 layers (P = 8192) want 64x128; <= 64-channel outputs stay on 64x64.
-static int pick_fwd(int P, int Co) {
+// Picks re-measured in round 5 with the 2-deep 128x128 rings (configs 21 / 22: two workgroups per CU, so one
+// workgroup's ring fill and epilogue run under the other's main loop; profiles/r5_conv/NOTES.md).
+// DDPX_CONV_PICKS=r4 restores the round-4 picks (A/B runs).
+static int g_picks_r4 = -1;
+static bool picks_r4() {
+  if (g_picks_r4 < 0) {
+    const char* e = getenv("DDPX_CONV_PICKS");
+    g_picks_r4 = (e && e[0] == 'r' && e[1] == '4') ? 1 : 0;
+  }
+  return g_picks_r4 == 1;
+}
+static int pick_fwd(int P, int C, int Co) {
   if (Co <= 64) return 7;     // conv0 (3->64 @32), DeepNN's 64/32-channel layers: 64x64, 3 stages
   if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
-  if (P >= 524288) return 8;  // 32x32 layers: 256x128, 8 waves
+  if (picks_r4()) return P >= 524288 ? 8 : 13;
+  if (C <= 128) return 22;    // K <= 1152 (VGG conv1 @32, conv2 @16): 115.6 vs 149.3 us (cfg 8) on conv1
   return 13;                  // 256x256, 8 waves
 }
 // Data-gradient picks do not change any result bit (every tile sums K in the same order, no statistics), so
-// they follow the round-4 measurements directly: VGG conv1's dx 128x64 with the cached im2col rows (141 vs
-// 153 us for 64x64, profiles/r4_vgg/probe_*.jsonl), the 4x4 layers 8-wave 128x128 / 4 stages (66 vs 73 us,
-// profiles/r4_final/conv_sweep.json).
+// they follow the measurements directly: VGG conv1's dx 128x64 with the cached im2col rows (141 vs 153 us
+// for 64x64, profiles/r4_vgg/probe_*.jsonl).
 static int pick_dgrad(int P, int C, int Co) {
   if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32, DeepNN): 128x64, 3 stages
+  if (picks_r4()) return P <= 8192 ? 15 : (Co <= 64 || Co > C) ? 8 : 13;
+  // 4x4 layers: 8-wave 128x128 / 4 stages (the 2-deep cfg 22 is faster alone, 56.5 vs 63.1 us, but slower with
+  // the fused BatchNorm sums in its epilogue, 78.4 vs 68.5 us in the step, profiles/r5_conv)
   if (P <= 8192) return 15;
-  if (Co <= 64 || Co > C) return 8;  // widening layers (dx narrower than dy) and thin DeepNN layers
+  if (Co <= 64 || Co > C) return 22;  // widening layers (dx narrower than dy), thin DeepNN layers: 124 vs 140 us
   return 13;
 }
 
@@ -207,15 +221,15 @@ DDPX_API int ddpx_conv_weight_prep(const float* w, int Co, int Cr, int Cp, void*
 }
 
 // Row tiles the forward GEMM uses (for sizing the BatchNorm statistics partials).
-DDPX_API int ddpx_conv_fwd_tiles_m(int P, int Co, int tile_cfg) {
-  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+DDPX_API int ddpx_conv_fwd_tiles_m(int P, int C, int Co, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
   int bm, bn;
   tile_of(cfg, &bm, &bn);
   return (P + bm - 1) / bm * epilogue_halves(cfg);
 }
 
-DDPX_API int ddpx_conv_fwd_tile_rows(int P, int Co, int tile_cfg) {
-  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+DDPX_API int ddpx_conv_fwd_tile_rows(int P, int C, int Co, int tile_cfg) {
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
   int bm, bn;
   tile_of(cfg, &bm, &bn);
   return bm / epilogue_halves(cfg);
@@ -242,7 +256,7 @@ DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats,
   if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
   p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
   p.conv = make_geom(H, W, C, P);
-  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, Co);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
   return (int)dispatch_conv_fwd(p, cfg, s);
 }
 
@@ -278,7 +292,7 @@ DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, in
 DDPX_API int ddpx_conv_dgrad_parts(int N, int H, int W, int C, int Co, int tile_cfg) {
   const int P = N * H * W;
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
-  if (cfg != 8 && cfg != 15) return 0;  // the configs instantiating EPI_BNBWD_BF16 (ddpx_pipe.h)
+  if (cfg != 8 && cfg != 15 && cfg != 22) return 0;  // the configs instantiating EPI_BNBWD_BF16 (ddpx_pipe.h)
   int bm, bn;
   tile_of(cfg, &bm, &bn);
   return (P + bm - 1) / bm * epilogue_halves(cfg);
@@ -308,20 +322,20 @@ DDPX_API int ddpx_conv_dgrad_bn(const void* dy, const void* wd, void* dx, int N,
   p.bn_a = a; p.bn_b = b; p.bn_mean = mean; p.bn_rstd = rstd;
   p.bn_pool = pool;
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
-  if (cfg != 8 && cfg != 15) return -5;
+  if (cfg != 8 && cfg != 15 && cfg != 22) return -5;
   return (int)dispatch_conv_dgrad(p, cfg, s);
 }
 
 static int pick_wgrad(int P, int C, int Co) {
-  (void)P;
   if (C <= 8) return 12;      // conv0 (K = 9 x 8): 64x64, BK 128
   // M = Co <= 64 (DeepNN's 128->64, 64->64, 64->32 layers): a 256-row tile would be 3/4 empty;
   // 64x64 / 3 stages measured 2.6x faster on 128->64@32 (profiles/r1_deepnn/conv_sweep_deepnn.json)
   if (Co <= 64) return 7;
-  // VGG conv1 (64->128 @32): 8-wave 128x128 / 4 stages (156 vs 181 us for 64x64 in the round-4 sweep,
-  // profiles/r4_final/conv_sweep.json; a different split-K summation order, judged by the multi-seed
-  // tests/test_gpu_parity.py)
-  if (C <= 64) return 15;
+  if (conv::picks_r4()) return C <= 64 ? 15 : 13;
+  // (a different split-K summation order than round 4's picks, judged by the multi-seed tests/test_gpu_parity.py)
+  // VGG conv1 (64->128 @32): 100.6 vs 133.0 us (cfg 15); conv2 (128->256 @16): 95.7 vs 99.0 us, and more splits
+  // (two workgroups per CU) with a cheaper reduce (12.3 vs 16.6 us); in-step, profiles/r5_conv
+  if (C <= 128) return 22;
   return 13;                  // 256x256, 8 waves (283 vs 393 us for 256x128 on 256->256@16)
 }
 
@@ -329,6 +343,7 @@ static int pick_wgrad(int P, int C, int Co) {
 // workgroup out of 160 KiB; the 8-wave configs also hold one per CU by registers).
 static int wgs_per_cu(int cfg) {
   static const int t[14] = {1, 1, 1, 2, 1, 2, 2, 3, 1, 1, 1, 1, 2, 1};
+  if (cfg == 21 || cfg == 22) return 2;
   return (cfg >= 0 && cfg <= 13) ? t[cfg] : 1;
 }
 

@@ -46,8 +46,8 @@ def conv_fwd(x, wf, Co, stats=True, tile=-1):
     y = torch.empty((P, Co), dtype=torch.bfloat16, device=x.device)
     st, T, BM = None, 0, 0
     if stats:
-        T = lib.ddpx_conv_fwd_tiles_m(P, Co, tile)
-        BM = lib.ddpx_conv_fwd_tile_rows(P, Co, tile)
+        T = lib.ddpx_conv_fwd_tiles_m(P, C, Co, tile)
+        BM = lib.ddpx_conv_fwd_tile_rows(P, C, Co, tile)
         st = torch.empty((T, 2, Co), dtype=torch.float32, device=x.device)
     native.check(lib.ddpx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), native.ptr(st), N, H, W, C, Co, tile,
                                    native.stream_handle()), "ddpx_conv_fwd")

@@ -70,8 +70,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_weight_prep", I, P, I, I, I, P, P, P)
     _sig(lib, "ddpx_bn_set_merge", None, I)
     _sig(lib, "ddpx_conv_set_rowcache", None, I)
-    _sig(lib, "ddpx_conv_fwd_tiles_m", I, I, I, I)
-    _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I)
+    _sig(lib, "ddpx_conv_fwd_tiles_m", I, I, I, I, I)
+    _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I, I)
     _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad_parts", I, I, I, I, I, I, I)

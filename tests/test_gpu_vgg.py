@@ -54,6 +54,42 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
     assert _rel(dw, wr.grad) < 5e-3
 
 
+@pytest.mark.parametrize("tile", [21, 22])
+@pytest.mark.parametrize("N,H,Ci,Co", [(8, 32, 64, 128), (3, 12, 24, 40), (16, 8, 256, 256)])
+def test_conv_two_deep_128_tiles(gpu, tile, N, H, Ci, Co):
+    """The 2-deep 128x128 ring configs (two workgroups per CU; statistics come out per 64-row epilogue half)."""
+    from ddpx.ops import conv as K
+    torch.manual_seed(3)
+    Cp = K.padded_channels(Ci)
+    x = _bf(torch.randn(N, Ci, H, H, device=gpu))
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) * (1.0 / (Ci * 9) ** 0.5)
+    xn = F.pad(x.permute(0, 2, 3, 1), (0, Cp - Ci)).to(torch.bfloat16).contiguous()
+    wf = torch.empty(Co * 9 * Cp, dtype=torch.bfloat16, device=gpu)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w, wf, wd)
+    y, st, T, BM = K.conv_fwd(xn, wf, Co, tile=tile)
+    assert BM == 64
+    refn = F.conv2d(x, _bf(w), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _rel(y, refn) < 1e-2
+    yf = y.float()
+    for t in (0, T // 2, T - 1):
+        rows = yf[t * BM:min((t + 1) * BM, yf.shape[0])]
+        if rows.shape[0] == 0:  # a trailing epilogue half wholly past P: zero statistics, weight 0 in the merge
+            assert torch.all(st[t] == 0)
+            continue
+        assert torch.allclose(st[t, 0], rows.mean(0), rtol=1e-3, atol=1e-3)
+        assert torch.allclose(st[t, 1], ((rows - rows.mean(0)) ** 2).sum(0), rtol=2e-3, atol=1e-2)
+    dy = _bf(torch.randn(N * H * H, Co, device=gpu))
+    xr = x.clone().requires_grad_(True)
+    wr = _bf(w).clone().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy.view(N, H, H, Co).permute(0, 3, 1, 2))
+    dx = K.conv_dgrad(dy.to(torch.bfloat16), wd, N, H, H, Cp, Co, tile=tile)
+    assert _rel(dx[..., :Ci].permute(0, 3, 1, 2), xr.grad) < 1e-2
+    dw = torch.empty(Co, Ci, 3, 3, device=gpu)
+    K.conv_wgrad(dy.to(torch.bfloat16), xn, Co, Ci, out=dw, tile=tile)
+    assert _rel(dw, wr.grad) < 5e-3
+
+
 @pytest.mark.parametrize("pool", [False, True])
 def test_bn_relu_pool_fwd_bwd(gpu, pool):
     from ddpx.ops import conv as K
