@@ -683,11 +683,20 @@ __device__ __forceinline__ void quad_colsum(float* red, const float (&cs)[4], in
 // math wave (the barrier-coupled ring lets 8 waves meet at every K-step: 52 vs 77 GB/s of L2 -> LDS per CU on
 // the 128x128 tile, profiles/r2_splitk).  The loaders end after the last publish; the math waves then run the
 // combine and epilogue (an s_barrier waits only for waves that have not ended).
+// The 2-deep rings of configs 21 - 23 are built for several workgroups per CU: held to that register budget
+// (waves per SIMD).
+template <int BM, int BN, int STAGES, int NW, int KSUB, int LW>
+constexpr int pipe_waves_per_eu() {
+  if (LW != 0 || KSUB != 1 || STAGES != 2) return 1;
+  if (BM == 128 && BN == 128) return NW / 2;         // 64 KiB: 2 per CU
+  if (BM == 256 && BN == 64 && NW == 4) return 2;    // 80 KiB: 2 per CU
+  return 1;
+}
+
 template <int BM, int BN, int STAGES, bool AK, bool BKc, int AMODE, int BMODE, int NW = 4, int KSUB = 1,
           bool SGDPF = false, bool SK = false, int LW = 0>
-// the 2-deep 128x128 rings (configs 21 / 22) are built for two workgroups per CU: held to that register budget
 __global__ void __launch_bounds__((NW + LW) * 64)
-__attribute__((amdgpu_waves_per_eu((BM == 128 && BN == 128 && STAGES == 2 && LW == 0) ? NW / 2 : 1)))
+__attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu<BM, BN, STAGES, NW, KSUB, LW>())))
 gemm_pipe_kernel(Params p) {
   constexpr int NT = NW * 64;
   constexpr int WGM = NW / 2;
@@ -975,8 +984,10 @@ gemm_pipe_kernel(Params p) {
         // conv data-gradient kernels, only the tiles where the fused sums measured faster than the separate
         // reduce pass (256x128 / 3 stages and 128x128 / 4 or 2 stages / 8 waves, profiles/r5_vgg/NOTES.md): the
         // others do not carry the epilogue's registers
-        if constexpr (LW == 0 && AMODE == MODE_IM2COL_BWD && NW == 8 &&
-                      ((BM == 256 && BN == 128 && STAGES == 3) || (BM == 128 && BN == 128 && STAGES != 3))) {
+        if constexpr (LW == 0 && AMODE == MODE_IM2COL_BWD &&
+                      ((NW == 8 && BM == 256 && BN == 128 && STAGES == 3) ||
+                       (NW == 8 && BM == 128 && BN == 128 && STAGES != 3))) {
+          // (256x64 / cfg 23 measured 129 -> 190 us with it, more than the 35 us reduce it removes)
           float s2[4] = {0.f, 0.f, 0.f, 0.f};
           epilogue_bnbwd<BMH, BN, NT>(p, Cbase, T, mh, n0, tid, ch, s2);
           __syncthreads();
@@ -1085,7 +1096,7 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
 }
 
 // cfg 16 - 20: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products
-constexpr int kNumCfgs = 23;
+constexpr int kNumCfgs = 24;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
 static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
 
@@ -1096,7 +1107,7 @@ static inline void tile_of(int cfg, int* bm, int* bn) {
   static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
                                      {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
                                      {128, 128}, {128, 128}, {256, 128}, {128, 128}, {64, 128}, {128, 64},
-                                     {64, 64},   {128, 128}, {128, 128}};
+                                     {64, 64},   {128, 128}, {128, 128}, {256, 64}};
   const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
@@ -1116,6 +1127,9 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     // 128x128 with a 2-deep ring (64 KiB): two workgroups per CU, one's epilogue / ring fill under the other's loop
     case 21: return launch<128, 128, 2, AK, BKc, AMODE, BMODE, 4>(p, splits, s);   // 4 waves, 64x64 each
     case 22: return launch<128, 128, 2, AK, BKc, AMODE, BMODE, 8>(p, splits, s);   // 8 waves, 32x64 each
+    // narrow (N = 64) products: 256x64, 2-deep (80 KiB, 2 per CU), 4 waves of 128x32 (8 waves would need 128
+    // VGPRs each and spilled)
+    case 23: return launch<256, 64, 2, AK, BKc, AMODE, BMODE, 4>(p, splits, s);
     case 16:  // warp-specialised (plain operands only)
       if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
         return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8, 1, false, false, 4>(p, splits, s);

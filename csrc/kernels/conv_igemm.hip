@@ -172,7 +172,9 @@ static bool picks_r4() {
   return g_picks_r4 == 1;
 }
 static int pick_fwd(int P, int C, int Co) {
-  if (Co <= 64) return 7;     // conv0 (3->64 @32), DeepNN's 64/32-channel layers: 64x64, 3 stages
+  // 64-channel outputs at 32x32 (VGG conv0, DeepNN 128->64): 256x64, 2-deep (47.9 vs 53.4 us, 120.7 vs 159.9 us)
+  if (Co <= 64 && P >= 524288 && !picks_r4()) return 23;
+  if (Co <= 64) return 7;     // DeepNN's 64/32-channel layers at 16x16: 64x64, 3 stages
   if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
   if (picks_r4()) return P >= 524288 ? 8 : 13;
   if (C <= 128) return 22;    // K <= 1152 (VGG conv1 @32, conv2 @16): 115.6 vs 149.3 us (cfg 8) on conv1
@@ -182,7 +184,8 @@ static int pick_fwd(int P, int C, int Co) {
 // they follow the measurements directly: VGG conv1's dx 128x64 with the cached im2col rows (141 vs 153 us
 // for 64x64, profiles/r4_vgg/probe_*.jsonl).
 static int pick_dgrad(int P, int C, int Co) {
-  if (C <= 64) return 6;      // dx of a 64-channel input (VGG conv1 @32, DeepNN): 128x64, 3 stages
+  if (C <= 64 && P >= 524288 && !picks_r4()) return 23;  // VGG conv1's dx @32: 256x64, 2-deep (116.6 vs 144.5 us)
+  if (C <= 64) return 6;      // dx of a 64-channel input (DeepNN @16): 128x64, 3 stages
   if (picks_r4()) return P <= 8192 ? 15 : (Co <= 64 || Co > C) ? 8 : 13;
   // 4x4 layers: 8-wave 128x128 / 4 stages (the 2-deep cfg 22 is faster alone, 56.5 vs 63.1 us, but slower with
   // the fused BatchNorm sums in its epilogue, 78.4 vs 68.5 us in the step, profiles/r5_conv)
@@ -343,7 +346,7 @@ static int pick_wgrad(int P, int C, int Co) {
 // workgroup out of 160 KiB; the 8-wave configs also hold one per CU by registers).
 static int wgs_per_cu(int cfg) {
   static const int t[14] = {1, 1, 1, 2, 1, 2, 2, 3, 1, 1, 1, 1, 2, 1};
-  if (cfg == 21 || cfg == 22) return 2;
+  if (cfg == 21 || cfg == 22 || cfg == 23) return 2;
   return (cfg >= 0 && cfg <= 13) ? t[cfg] : 1;
 }
 

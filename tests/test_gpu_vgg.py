@@ -54,10 +54,10 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
     assert _rel(dw, wr.grad) < 5e-3
 
 
-@pytest.mark.parametrize("tile", [21, 22])
+@pytest.mark.parametrize("tile", [21, 22, 23])
 @pytest.mark.parametrize("N,H,Ci,Co", [(8, 32, 64, 128), (3, 12, 24, 40), (16, 8, 256, 256)])
 def test_conv_two_deep_128_tiles(gpu, tile, N, H, Ci, Co):
-    """The 2-deep 128x128 ring configs (two workgroups per CU; statistics come out per 64-row epilogue half)."""
+    """The 2-deep ring configs (two workgroups per CU): 128x128 (statistics per 64-row epilogue half), 256x64."""
     from ddpx.ops import conv as K
     torch.manual_seed(3)
     Cp = K.padded_channels(Ci)
@@ -68,7 +68,7 @@ def test_conv_two_deep_128_tiles(gpu, tile, N, H, Ci, Co):
     wd = torch.empty_like(wf)
     K.weight_prep(w, wf, wd)
     y, st, T, BM = K.conv_fwd(xn, wf, Co, tile=tile)
-    assert BM == 64
+    assert BM == (256 if tile == 23 else 64)
     refn = F.conv2d(x, _bf(w), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
     assert _rel(y, refn) < 1e-2
     yf = y.float()
@@ -357,10 +357,11 @@ def test_wgrad_fused_sgd_writes_prepared_layouts(gpu, N, H, C, Co):
 
 
 @pytest.mark.parametrize("N,H,C,Co,pool", [(8, 16, 64, 128, True), (2, 8, 256, 256, False), (64, 16, 128, 256, True),
-                                           (64, 16, 256, 256, False), (16, 4, 512, 512, True), (256, 8, 256, 512, False)])
+                                           (64, 16, 256, 256, False), (16, 4, 512, 512, True), (256, 8, 256, 512, False),
+                                           (512, 32, 64, 128, False)])  # VGG conv1's dx: 256x64 tile (cfg 23), unfused
 def test_dgrad_bn_epilogue_matches_separate_reduce(gpu, N, H, C, Co, pool):
     """The conv data gradient with the BatchNorm backward sums of the block below in its epilogue
-    (EPI_BNBWD_BF16 on tile configs 15 and 8; the other picks fall back to the plain data gradient) = the plain
+    (EPI_BNBWD_BF16 on tile configs 8, 15 and 22; the other picks fall back to the plain data gradient) = the plain
     data gradient + bn_backward's own reduce: g bitwise, the sums / dgamma / dbeta / dy to fp32 summation order."""
     from ddpx.ops import conv as K
     from ddpx.runtime import native
