@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""fp32 VGG convolutions per layer: Winograd F(2,3) (csrc/kernels/f32_wino.hip) vs the exact implicit GEMM.
+"""fp32 VGG convolutions per layer: Winograd F(2,3) (csrc/kernels/f32_wino.hip) vs the exact implicit GEMM
+(forward, data gradient, weight gradient).
 
     python benchmarks/wino_bench.py [--out FILE]        (DDPX_WINO_STAGES=2|3 selects the Winograd ring depth)
 
@@ -69,8 +70,12 @@ def main():
             "direct_dgrad": timed(lambda: f32.conv_dgrad(dy.view(-1, Co), wd, N, H, H, Ci, Co)),
             "wprep": timed(lambda: f32.wino_wprep(w, uf, ud)),
         }
+        gw = torch.empty(Co, Ci, 3, 3, device=dev)
+        dyf = dy.view(-1, Co)
+        row["wino_wgrad"] = timed(lambda: f32.wino_wgrad(dyf, x, Co, Ci, gw))
+        row["direct_wgrad"] = timed(lambda: f32.direct_wgrad(dyf, x, Co, Ci, gw))
         row = {k: round(v, 1) for k, v in row.items()}
-        for k in ("wino_fwd", "direct_fwd", "wino_dgrad", "direct_dgrad"):
+        for k in ("wino_fwd", "direct_fwd", "wino_dgrad", "direct_dgrad", "wino_wgrad", "direct_wgrad"):
             row[k + "_tflops"] = round(flops / row[k] / 1e6, 1)
         key = f"H{H}_C{Ci}_K{Co}"
         res[key] = row

@@ -300,6 +300,209 @@ wino_wprep_kernel(const float* __restrict__ w, int Co, int Ci, int Cp, float* __
   for (int q = 0; q < 16; ++q) uf[((size_t)q * Cp + ci2) * Co + co2] = tr[q][t >> 4][t & 15];
 }
 
+// ---------------------------------------------------------------------------------------- weight gradient
+// dW = G^T dU G,  dU[xi][co][ci] = sum over output tiles of (A dY A^T)[xi][tile][co] * (B^T d B)[xi][tile][ci]
+// (A = (A^T)^T, 4x2): the forward's U = G g G^T enters Y = A^T (U (.) V) A linearly, so its gradient is the
+// tile sum of the transformed output gradient times the transformed input patch, and g's is G^T dU G.  16
+// GEMMs of [Co x tiles] x [tiles x Ci]: 4/9 of the direct weight gradient's multiplies.
+//   * one workgroup = 64 output channels x 32 input channels x all 16 xi, over one split's range of tiles;
+//     wave w owns output channels 16w..16w+15 and both 16-channel input halves: 32 f32 16x16x4 MFMA chains;
+//   * K-step = 8 tiles (two MFMA k-steps of 4): the tiles' 4x4 input patches (32 channels) and 2x2 output
+//     gradients (64 channels) go global -> LDS by LDS-DMA (zero padding from buffer bounds);
+//   * lane l = (tile l/16, channel l%16) is the MFMA A slot (row = output channel) and B slot (column = input
+//     channel) at once: each lane transforms its own dy 2x2 / patch 4x4 in registers, nothing else touches LDS;
+//   * partial dU per split [S][16][Co][Cp]; ddpx_f32_wino_wgrad_reduce sums the splits in order and applies
+//     G^T . G (fixed order: deterministic).
+constexpr int WG_CO = 64, WG_CI = 32, WKT = 8;   // output channels, input channels, tiles per K-step
+constexpr int XS_T = 16 * WG_CI + 16;             // floats per tile of the patch image (padded: bank shift 16)
+constexpr int DS_T = 4 * WG_CO + 16;              // floats per tile of the dy image
+constexpr int WX_BYTES = WKT * XS_T * 4, WD_BYTES = WKT * DS_T * 4;
+constexpr int WSLOT = WX_BYTES + WD_BYTES;        // 25 KiB
+
+template <int STAGES>
+__global__ void __launch_bounds__(NT, 2)
+wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int H,
+                  int W, int Cp, int Co, int Pt, int L, int nb_ci, unsigned x_bytes, unsigned dy_bytes) {
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * WSLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = nb_ci * (Co / WG_CO);
+  const int blk = blockIdx.x % nblk, sp = blockIdx.x / nblk;
+  const int ci0 = (blk % nb_ci) * WG_CI, co0 = (blk / nb_ci) * WG_CO;
+  const int TH = H >> 1, TW = W >> 1;
+  const int t_beg = sp * L, t_end = min(Pt, t_beg + L);
+  const int nk = (t_end - t_beg + WKT - 1) / WKT;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, dy_bytes, 0x00020000);
+
+  // DMA roles (per K-step): patch instruction j = 4*wave + u (u < 4): tile j/2, patch rows 2(j%2), 2(j%2)+1
+  // (lane = (pixel q%8 of the half, 16-B chunk c of the 32 channels)); dy instruction u < 2: tile 2*wave + u,
+  // lane = (pixel q = lane/16, 16-B chunk lane%16 of the 64 channels)
+  auto issue = [&](int k) {
+    char* slot = smem + (k % STAGES) * WSLOT;
+    const int tb = t_beg + k * WKT;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * wave + u, t = j >> 1, half = j & 1;
+      const int q = half * 8 + (lane >> 3), c = lane & 7;
+      const int p = tb + t;
+      unsigned off = kOOB;
+      if (p < t_end) {
+        const int n = p / (TH * TW), r = p - n * (TH * TW);
+        const int th = r / TW, tw = r - th * TW;
+        const int h = 2 * th - 1 + (q >> 2), w = 2 * tw - 1 + (q & 3);
+        if (h >= 0 && h < H && w >= 0 && w < W) off = (unsigned)(((((size_t)n * H + h) * W + w) * Cp + ci0 + 4 * c) * 4);
+      }
+      dma16(rx, slot + (t * XS_T + half * 8 * WG_CI) * 4, off);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = 2 * wave + u, q = lane >> 4, c = lane & 15;
+      const int p = tb + t;
+      unsigned off = kOOB;
+      if (p < t_end) {
+        const int n = p / (TH * TW), r = p - n * (TH * TW);
+        const int th = r / TW, tw = r - th * TW;
+        const size_t pix = ((size_t)n * H + 2 * th + (q >> 1)) * W + 2 * tw + (q & 1);
+        off = (unsigned)((pix * Co + co0 + 4 * c) * 4);
+      }
+      dma16(rd, slot + WX_BYTES + t * DS_T * 4, off);
+    }
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+  constexpr int PER_STEP = 6;  // DMA instructions per wave per K-step
+  const int tl = lane >> 4, ch = lane & 15;
+  for (int k = 0; k < nk; ++k) {
+    const int ahead = min(STAGES - 2, nk - 1 - k);
+    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + STAGES - 1 < nk) issue(k + STAGES - 1);
+    const char* slot = smem + (k % STAGES) * WSLOT;
+    const float* xs = reinterpret_cast<const float*>(slot);
+    const float* ds = reinterpret_cast<const float*>(slot + WX_BYTES);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int t = sub * 4 + tl;
+      // A fragment: M = A dY A^T of (tile t, output channel co0 + 16 wave + ch), A = [[1,0],[1,1],[1,-1],[0,-1]]
+      float d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = ds[t * DS_T + q * WG_CO + wave * 16 + ch];
+      float rr[4][2];  // A dY
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        rr[0][j] = d[0 * 2 + j];
+        rr[1][j] = d[0 * 2 + j] + d[1 * 2 + j];
+        rr[2][j] = d[0 * 2 + j] - d[1 * 2 + j];
+        rr[3][j] = -d[1 * 2 + j];
+      }
+      float m[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        m[a * 4 + 0] = rr[a][0];
+        m[a * 4 + 1] = rr[a][0] + rr[a][1];
+        m[a * 4 + 2] = rr[a][0] - rr[a][1];
+        m[a * 4 + 3] = -rr[a][1];
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        // B fragment: V = B^T x B of (tile t, input channel ci0 + 16 cb + ch)
+        float xv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xv[q] = xs[t * XS_T + q * WG_CI + cb * 16 + ch];
+        float tmp[16];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          tmp[0 * 4 + c] = xv[0 * 4 + c] - xv[2 * 4 + c];
+          tmp[1 * 4 + c] = xv[1 * 4 + c] + xv[2 * 4 + c];
+          tmp[2 * 4 + c] = xv[2 * 4 + c] - xv[1 * 4 + c];
+          tmp[3 * 4 + c] = xv[1 * 4 + c] - xv[3 * 4 + c];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v0 = tmp[r * 4 + 0] - tmp[r * 4 + 2];
+          const float v1 = tmp[r * 4 + 1] + tmp[r * 4 + 2];
+          const float v2 = tmp[r * 4 + 2] - tmp[r * 4 + 1];
+          const float v3 = tmp[r * 4 + 1] - tmp[r * 4 + 3];
+          acc[r * 4 + 0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 0], v0, acc[r * 4 + 0][cb], 0, 0, 0);
+          acc[r * 4 + 1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 1], v1, acc[r * 4 + 1][cb], 0, 0, 0);
+          acc[r * 4 + 2][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 2], v2, acc[r * 4 + 2][cb], 0, 0, 0);
+          acc[r * 4 + 3][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 3], v3, acc[r * 4 + 3][cb], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // partial dU[sp][xi][co][ci]: lane holds rows (output channels) 4 (lane/16) + r, column (input channel) lane%16
+  const size_t plane = (size_t)Co * Cp;
+  float* dst = part + (size_t)sp * 16 * plane;
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wave * 16 + 4 * tl + r, ci = ci0 + cb * 16 + ch;
+        dst[(size_t)q * plane + (size_t)co * Cp + ci] = acc[q][cb][r];
+      }
+}
+
+// dU[xi][co][ci] = sum over splits (in split order), 4 input channels per thread
+__global__ void __launch_bounds__(256)
+wino_wgrad_sum_kernel(const float* __restrict__ part, int S, size_t n4, float* __restrict__ du) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const f32x4* src = reinterpret_cast<const f32x4*>(part);
+  f32x4 acc = src[i];
+  int s = 1;
+  for (; s + 7 < S; s += 8) {  // 8 splits' loads in flight, added in split order
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(s + u) * n4 + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; s < S; ++s) acc += src[(size_t)s * n4 + i];
+  reinterpret_cast<f32x4*>(du)[i] = acc;
+}
+
+// grad[co][ci][3][3] (+)= G^T dU[.][co][ci] G, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]]; ci < Ci only
+__global__ void __launch_bounds__(256)
+wino_wgrad_out_kernel(const float* __restrict__ du, int Co, int Ci, int Cp, float* __restrict__ grad, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Co * Ci) return;
+  const int co = i / Ci, ci = i - co * Ci;
+  const size_t plane = (size_t)Co * Cp;
+  float u[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) u[q] = du[(size_t)q * plane + (size_t)co * Cp + ci];
+  float t[3][4];  // G^T dU
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    t[0][b] = u[0 * 4 + b] + 0.5f * (u[1 * 4 + b] + u[2 * 4 + b]);
+    t[1][b] = 0.5f * (u[1 * 4 + b] - u[2 * 4 + b]);
+    t[2][b] = 0.5f * (u[1 * 4 + b] + u[2 * 4 + b]) + u[3 * 4 + b];
+  }
+  float* g = grad + (size_t)i * 9;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float g0 = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
+    const float g1 = 0.5f * (t[r][1] - t[r][2]);
+    const float g2 = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+    g[r * 3 + 0] = accumulate ? g[r * 3 + 0] + g0 : g0;
+    g[r * 3 + 1] = accumulate ? g[r * 3 + 1] + g1 : g1;
+    g[r * 3 + 2] = accumulate ? g[r * 3 + 2] + g2 : g2;
+  }
+}
+
 }  // namespace wino
 }  // namespace ddpx
 
@@ -341,4 +544,43 @@ DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float*
                        H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
   const int e = (int)hipGetLastError();
   return e ? -e : 4 * wino::TP;
+}
+
+// Winograd weight gradient applies: 3x3 / s1 / p1, H and W even, Cp % 32 == 0, Co % 64 == 0.
+DDPX_API int ddpx_f32_wino_wgrad_ok(int H, int W, int Cp, int Co) {
+  return (Cp >= 32 && Cp % wino::WG_CI == 0 && Co % wino::WG_CO == 0 && H >= 2 && W >= 2 && H % 2 == 0 &&
+          W % 2 == 0) ? 1 : 0;
+}
+
+// Splits of the tile range: enough workgroups for two rounds of the chip (2 per CU), >= 16 K-steps each.
+DDPX_API int ddpx_f32_wino_wgrad_splits(int N, int H, int W, int Cp, int Co) {
+  const int Pt = N * (H / 2) * (W / 2);
+  const int nblk = (Cp / wino::WG_CI) * (Co / wino::WG_CO);
+  const int maxS = Pt / (16 * wino::WKT) > 1 ? Pt / (16 * wino::WKT) : 1;
+  int S = (2 * 256 * 2 + nblk - 1) / nblk;
+  if (S > maxS) S = maxS;
+  if (S < 1) S = 1;
+  const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
+  return (Pt + L - 1) / L;  // the splits that get a tile range
+}
+
+// part [S][16][Co][Cp] = per-split dU; du [16][Co][Cp] (scratch) = their sum; grad [Co][Ci][3][3] (+)= G^T dU G.
+// x NHWC [N][H][W][Cp], dy [N*H*W][Co].  S = ddpx_f32_wino_wgrad_splits(...).
+DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, float* du, int N, int H, int W, int Cp,
+                                 int Co, int Ci, int S, float* grad, int accumulate, hipStream_t s) {
+  if (!ddpx_f32_wino_wgrad_ok(H, W, Cp, Co) || Ci > Cp || S < 1) return -2;
+  const size_t xb = (size_t)N * H * W * Cp * 4, db = (size_t)N * H * W * Co * 4;
+  if (xb >= 0x80000000ull || db >= 0x80000000ull) return -3;
+  if (S != ddpx_f32_wino_wgrad_splits(N, H, W, Cp, Co)) return -4;
+  const int Pt = N * (H / 2) * (W / 2);
+  const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
+  const int nb_ci = Cp / wino::WG_CI;
+  const int nwg = nb_ci * (Co / wino::WG_CO) * S;
+  hipLaunchKernelGGL((wino::wino_wgrad_kernel<2>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co, Pt, L,
+                     nb_ci, (unsigned)xb, (unsigned)db);
+  const size_t n4 = (size_t)16 * Co * Cp / 4;
+  hipLaunchKernelGGL(wino::wino_wgrad_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part, S, n4, du);
+  hipLaunchKernelGGL(wino::wino_wgrad_out_kernel, dim3((Co * Ci + 255) / 256), dim3(256), 0, s, du, Co, Ci, Cp, grad,
+                     accumulate);
+  return -(int)hipGetLastError();
 }

@@ -46,6 +46,9 @@ for _sig in (
         ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
         ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P),
+        ("ddpx_f32_wino_wgrad_ok", _I, _I, _I, _I, _I),
+        ("ddpx_f32_wino_wgrad_splits", _I, _I, _I, _I, _I, _I),
+        ("ddpx_f32_wino_wgrad", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P),
 ):
     native.register_kernel_sig(*_sig)
 
@@ -318,8 +321,40 @@ def wgrad_splits(Co, Ncols, P):
     return s
 
 
+# Weight gradient through F(2,3) too (csrc/kernels/f32_wino.hip wino_wgrad_kernel: dW = G^T (sum over tiles of
+# (A dY A^T) (.) (B^T x B)) G, 4/9 of the direct product's multiplies); DDPX_F32_WINO_WGRAD=0: the direct split-K
+# implicit GEMM.  Applies at Cp % 32 == 0, Co % 64 == 0, even H and W.
+_WINO_WGRAD = _os.environ.get("DDPX_F32_WINO_WGRAD", "1") != "0"
+
+
+def wino_wgrad_applies(H, W, Cp, Co) -> bool:
+    return _WINO and _WINO_WGRAD and bool(native.kernels().ddpx_f32_wino_wgrad_ok(H, W, Cp, Co))
+
+
+def wino_wgrad(dy, x, Co, Ci, out, accumulate=False):
+    """out [Co,Ci,3,3] (+)= the Winograd F(2,3) weight gradient from dy [P, Co] and x [N,H,W,Cp]."""
+    N, H, W, Cp = x.shape
+    _f32(x, "x")
+    _req(dy.dtype == torch.float32 and dy.is_contiguous() and dy.numel() == N * H * W * Co, "wino_wgrad: bad dy")
+    _req(out.dtype == torch.float32 and out.is_contiguous() and out.numel() == Co * Ci * 9, "wino_wgrad: bad out")
+    lib = native.kernels()
+    S = lib.ddpx_f32_wino_wgrad_splits(N, H, W, Cp, Co)
+    part = torch.empty((S, 16, Co, Cp), dtype=torch.float32, device=dy.device)
+    du = torch.empty((16, Co, Cp), dtype=torch.float32, device=dy.device)
+    _call("ddpx_f32_wino_wgrad", x.data_ptr(), dy.data_ptr(), part.data_ptr(), du.data_ptr(), N, H, W, Cp, Co, Ci, S,
+          out.data_ptr(), int(accumulate))
+
+
 def conv_wgrad(dy, x, Co, Ci, out, accumulate=False):
     """out [Co,Ci,3,3] (+)= weight gradient from dy [P, Co] and x [N,H,W,Cp]."""
+    N, H, W, Cp = x.shape
+    if wino_wgrad_applies(H, W, Cp, Co):
+        return wino_wgrad(dy, x, Co, Ci, out, accumulate)
+    return direct_wgrad(dy, x, Co, Ci, out, accumulate)
+
+
+def direct_wgrad(dy, x, Co, Ci, out, accumulate=False):
+    """conv_wgrad on the exact implicit GEMM (split over N*H*W, reduced in fixed order)."""
     N, H, W, Cp = x.shape
     P = N * H * W
     ncol = 9 * Cp

@@ -627,6 +627,38 @@ def test_wino_conv_forward_dgrad_stats_match_fp64(gpu, shape):
         assert _err_vs_fp64(dx, xr.grad.permute(0, 2, 3, 1))["rel_l2"] < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(2, 8, 64, 64), (3, 6, 32, 128), (4, 16, 128, 64), (64, 4, 512, 512),
+                                   (5, 2, 96, 192)])
+def test_wino_wgrad_matches_fp64(gpu, shape):
+    """Winograd F(2,3) weight gradient (dW = G^T sum_tiles (A dY A^T) (.) (B^T x B) G) against fp64 and against the
+    direct split-K implicit GEMM's own error: partial last K-step (tiles % 8), several splits, accumulate."""
+    from ddpx.ops import f32
+    torch.manual_seed(6)
+    N, H, Ci, Co = shape
+    x = torch.randn(N, Ci, H, H, device=gpu)
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+    dy = torch.randn(N, H, H, Co, device=gpu)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    assert f32.wino_wgrad_applies(H, H, Ci, Co)
+    xr = x.double()
+    wr = w.double().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+    ref = wr.grad
+    out = torch.full((Co, Ci, 3, 3), 0.25, device=gpu)
+    f32.wino_wgrad(dy.reshape(-1, Co), xn, Co, Ci, out, accumulate=True)
+    err = _err_vs_fp64(out - 0.25, ref)["rel_l2"]
+    assert err < 1e-5, err
+    f32.wino_wgrad(dy.reshape(-1, Co), xn, Co, Ci, out)
+    assert _err_vs_fp64(out, ref)["rel_l2"] < 1e-5
+    # no worse than 2x the direct implicit GEMM on the same operands (which needs power-of-two H, W, C)
+    if H & (H - 1) or Ci & (Ci - 1):
+        return
+    direct = torch.empty_like(out)
+    f32.direct_wgrad(dy.reshape(-1, Co), xn, Co, Ci, direct)
+    e_direct = _err_vs_fp64(direct, ref)["rel_l2"]
+    assert err < max(2 * e_direct, 2e-6), (err, e_direct)
+
+
 def test_vgg_fp32_runs_winograd_layers(gpu):
     """The fp32 VGG plan puts every layer with >= 64 input channels on Winograd (forward + data gradient)."""
     import ddpx
