@@ -47,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--only", default="", help="wgrad: time only the weight gradients")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -63,6 +64,13 @@ def main():
         f32.conv_wprep(w, wf, wd)
         dy = torch.randn(N, H, H, Co, device=dev)
         flops = 2.0 * N * H * H * Co * 9 * Ci
+        if a.only == "wgrad":
+            gw = torch.empty(Co, Ci, 3, 3, device=dev)
+            row = {"wino_wgrad": round(timed(lambda: f32.wino_wgrad(dy.view(-1, Co), x, Co, Ci, gw)), 1)}
+            key = f"H{H}_C{Ci}_K{Co}"
+            res[key] = row
+            print(key, json.dumps(row), flush=True)
+            continue
         row = {
             "wino_fwd": timed(lambda: f32.wino_conv(x, uf, Co, stats=True)),
             "direct_fwd": timed(lambda: f32.conv_fwd_stats(x, wf, Co)),

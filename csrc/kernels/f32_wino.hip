@@ -319,7 +319,10 @@ constexpr int DS_T = 4 * WG_CO + 16;              // floats per tile of the dy i
 constexpr int WX_BYTES = WKT * XS_T * 4, WD_BYTES = WKT * DS_T * 4;
 constexpr int WSLOT = WX_BYTES + WD_BYTES;        // 25 KiB
 
-template <int STAGES>
+// WS (wave split): 0 = wave w owns output channels 16w.. and both input-channel halves (each wave transforms
+// all 32 channels' patches); 1 = wave w owns output channels 32(w/2).. and input channels 16(w%2).. (two dy
+// transforms, one patch transform per MFMA k-step: a third fewer LDS reads)
+template <int STAGES, int WS>
 __global__ void __launch_bounds__(NT, 2)
 wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int H,
                   int W, int Cp, int Co, int Pt, int L, int nb_ci, unsigned x_bytes, unsigned dy_bytes) {
@@ -390,13 +393,11 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     const char* slot = smem + (k % STAGES) * WSLOT;
     const float* xs = reinterpret_cast<const float*>(slot);
     const float* ds = reinterpret_cast<const float*>(slot + WX_BYTES);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int t = sub * 4 + tl;
-      // A fragment: M = A dY A^T of (tile t, output channel co0 + 16 wave + ch), A = [[1,0],[1,1],[1,-1],[0,-1]]
+    // A = [[1,0],[1,1],[1,-1],[0,-1]]: M = A dY A^T of (tile t, output channel col) from the 2x2 dy
+    auto dy_transform = [&](int t, int col, float (&m)[16]) {
       float d[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = ds[t * DS_T + q * WG_CO + wave * 16 + ch];
+      for (int q = 0; q < 4; ++q) d[q] = ds[t * DS_T + q * WG_CO + col];
       float rr[4][2];  // A dY
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -405,7 +406,6 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
         rr[2][j] = d[0 * 2 + j] - d[1 * 2 + j];
         rr[3][j] = -d[1 * 2 + j];
       }
-      float m[16];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         m[a * 4 + 0] = rr[a][0];
@@ -413,30 +413,50 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
         m[a * 4 + 2] = rr[a][0] - rr[a][1];
         m[a * 4 + 3] = -rr[a][1];
       }
+    };
+    // V = B^T x B of (tile t, input channel col) from the 4x4 patch
+    auto x_transform = [&](int t, int col, float (&v)[16]) {
+      float xv[16];
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        // B fragment: V = B^T x B of (tile t, input channel ci0 + 16 cb + ch)
-        float xv[16];
+      for (int q = 0; q < 16; ++q) xv[q] = xs[t * XS_T + q * WG_CI + col];
+      float tmp[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) xv[q] = xs[t * XS_T + q * WG_CI + cb * 16 + ch];
-        float tmp[16];
+      for (int c = 0; c < 4; ++c) {
+        tmp[0 * 4 + c] = xv[0 * 4 + c] - xv[2 * 4 + c];
+        tmp[1 * 4 + c] = xv[1 * 4 + c] + xv[2 * 4 + c];
+        tmp[2 * 4 + c] = xv[2 * 4 + c] - xv[1 * 4 + c];
+        tmp[3 * 4 + c] = xv[1 * 4 + c] - xv[3 * 4 + c];
+      }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          tmp[0 * 4 + c] = xv[0 * 4 + c] - xv[2 * 4 + c];
-          tmp[1 * 4 + c] = xv[1 * 4 + c] + xv[2 * 4 + c];
-          tmp[2 * 4 + c] = xv[2 * 4 + c] - xv[1 * 4 + c];
-          tmp[3 * 4 + c] = xv[1 * 4 + c] - xv[3 * 4 + c];
+      for (int r = 0; r < 4; ++r) {
+        v[r * 4 + 0] = tmp[r * 4 + 0] - tmp[r * 4 + 2];
+        v[r * 4 + 1] = tmp[r * 4 + 1] + tmp[r * 4 + 2];
+        v[r * 4 + 2] = tmp[r * 4 + 2] - tmp[r * 4 + 1];
+        v[r * 4 + 3] = tmp[r * 4 + 1] - tmp[r * 4 + 3];
+      }
+    };
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int t = sub * 4 + tl;
+      if constexpr (WS == 0) {
+        float m[16];
+        dy_transform(t, wave * 16 + ch, m);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          float v[16];
+          x_transform(t, cb * 16 + ch, v);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[q], v[q], acc[q][cb], 0, 0, 0);
         }
+      } else {
+        float v[16];
+        x_transform(t, (wave & 1) * 16 + ch, v);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v0 = tmp[r * 4 + 0] - tmp[r * 4 + 2];
-          const float v1 = tmp[r * 4 + 1] + tmp[r * 4 + 2];
-          const float v2 = tmp[r * 4 + 2] - tmp[r * 4 + 1];
-          const float v3 = tmp[r * 4 + 1] - tmp[r * 4 + 3];
-          acc[r * 4 + 0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 0], v0, acc[r * 4 + 0][cb], 0, 0, 0);
-          acc[r * 4 + 1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 1], v1, acc[r * 4 + 1][cb], 0, 0, 0);
-          acc[r * 4 + 2][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 2], v2, acc[r * 4 + 2][cb], 0, 0, 0);
-          acc[r * 4 + 3][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[r * 4 + 3], v3, acc[r * 4 + 3][cb], 0, 0, 0);
+        for (int cb = 0; cb < 2; ++cb) {  // here cb = the output-channel half of the wave's 32
+          float m[16];
+          dy_transform(t, (wave >> 1) * 32 + cb * 16 + ch, m);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(m[q], v[q], acc[q][cb], 0, 0, 0);
         }
       }
     }
@@ -450,7 +470,8 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wave * 16 + 4 * tl + r, ci = ci0 + cb * 16 + ch;
+        const int co = WS == 0 ? co0 + wave * 16 + 4 * tl + r : co0 + (wave >> 1) * 32 + cb * 16 + 4 * tl + r;
+        const int ci = WS == 0 ? ci0 + cb * 16 + ch : ci0 + (wave & 1) * 16 + ch;
         dst[(size_t)q * plane + (size_t)co * Cp + ci] = acc[q][cb][r];
       }
 }
@@ -576,8 +597,33 @@ DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, f
   const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
   const int nb_ci = Cp / wino::WG_CI;
   const int nwg = nb_ci * (Co / wino::WG_CO) * S;
-  hipLaunchKernelGGL((wino::wino_wgrad_kernel<2>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co, Pt, L,
-                     nb_ci, (unsigned)xb, (unsigned)db);
+  // DDPX_WINO_WGRAD_VARIANT: ring depth 2|3 and wave split 0|1 (see wino_wgrad_kernel), e.g. "s3w1"; default
+  // s2w1 (VGG layers 3.55 ms vs 3.72 for s2w0; the ring depth changed nothing; profiles/r5_wino)
+  static const int variant = [] {
+    const char* e = getenv("DDPX_WINO_WGRAD_VARIANT");
+    if (!e || e[0] != 's' || !e[1] || e[2] != 'w' || !e[3]) return 21;
+    return (e[1] == '3' ? 30 : 20) + (e[3] == '1' ? 1 : 0);
+  }();
+  switch (variant) {
+    case 21:  // default
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    case 30:
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<3, 0>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    case 31:
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<3, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    case 20:
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 0>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    default:
+      return -5;
+  }
   const size_t n4 = (size_t)16 * Co * Cp / 4;
   hipLaunchKernelGGL(wino::wino_wgrad_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part, S, n4, du);
   hipLaunchKernelGGL(wino::wino_wgrad_out_kernel, dim3((Co * Ci + 255) / 256), dim3(256), 0, s, du, Co, Ci, Cp, grad,
