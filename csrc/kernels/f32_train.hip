@@ -787,6 +787,103 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
   rstd_out[c] = rs;
 }
 
+// The same merge split over chunk ranges, for few channels and many chunks (VGG conv0 / conv1: C = 64 / 128,
+// T = 2048 / 4096, one or two workgroups of the kernel above: 78 / 52 us).  Three launches: (1) per split the
+// fp64 sum of n * mean; (2) the mean from all splits' sums (split order), then per split the fp64 M2 sum;
+// (3) the M2 of all splits (split order) and the outputs.  Deterministic; within a split the same 16-group
+// interleave as bn_finalize_kernel.
+constexpr int kFinSplitMax = 32, kFinSplitMaxC = 1024;
+__device__ double g_fin_s1[kFinSplitMax * kFinSplitMaxC];
+__device__ double g_fin_s2[kFinSplitMax * kFinSplitMaxC];
+
+__device__ __forceinline__ double fin_group_tree(double v, double (*red)[64], int g, int cl) {
+  red[g][cl] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int k = 0; k < 16; ++k) r += red[k][cl];
+  return r;
+}
+
+__global__ void __launch_bounds__(1024) bn_fin_sum_kernel(const float* __restrict__ part, int T, int Ts, int R,
+                                                           int P, int C) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
+  const int t0 = sp * Ts, t1 = min(T, t0 + Ts);
+  double sm = 0.0;
+  if (c < C) {
+    int t = t0 + g;
+    for (; t + 7 * 16 < t1; t += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sm += (double)min(R, P - (t + 16 * u) * R) * v[u];
+    }
+    for (; t < t1; t += 16) sm += (double)min(R, P - t * R) * part[(size_t)t * 2 * C + c];
+  }
+  sm = fin_group_tree(sm, red, g, cl);
+  if (g == 0 && c < C) g_fin_s1[(size_t)sp * C + c] = sm;
+}
+
+__global__ void __launch_bounds__(1024) bn_fin_m2_kernel(const float* __restrict__ part, int T, int Ts, int S, int R,
+                                                          int P, int C) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
+  const int t0 = sp * Ts, t1 = min(T, t0 + Ts);
+  double m2 = 0.0;
+  if (c < C) {
+    double m = 0.0;
+    for (int k = 0; k < S; ++k) m += g_fin_s1[(size_t)k * C + c];
+    m /= P;
+    int t = t0 + g;
+    for (; t + 7 * 16 < t1; t += 8 * 16) {
+      float mv[8], qv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        mv[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+        qv[u] = part[(size_t)(t + 16 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double d = mv[u] - m;
+        m2 += qv[u] + (double)min(R, P - (t + 16 * u) * R) * d * d;
+      }
+    }
+    for (; t < t1; t += 16) {
+      const double d = part[(size_t)t * 2 * C + c] - m;
+      m2 += part[(size_t)t * 2 * C + C + c] + (double)min(R, P - t * R) * d * d;
+    }
+  }
+  m2 = fin_group_tree(m2, red, g, cl);
+  if (g == 0 && c < C) g_fin_s2[(size_t)sp * C + c] = m2;
+}
+
+__global__ void __launch_bounds__(64) bn_fin_out_kernel(int S, int P, int C, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ rmean,
+                                                         float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                                                         float momentum, float eps, float* __restrict__ a,
+                                                         float* __restrict__ b, float* __restrict__ mean_out,
+                                                         float* __restrict__ rstd_out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double m = 0.0, m2 = 0.0;
+  for (int k = 0; k < S; ++k) m += g_fin_s1[(size_t)k * C + c];
+  m /= P;
+  for (int k = 0; k < S; ++k) m2 += g_fin_s2[(size_t)k * C + c];
+  const float mu = (float)m, var = (float)(m2 / P);
+  const float unb = P > 1 ? (float)(m2 / (P - 1)) : var;
+  rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+  rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  const float rs = 1.f / sqrtf(var + eps);
+  a[c] = gamma[c] * rs;
+  b[c] = beta[c];
+  mean_out[c] = mu;
+  rstd_out[c] = rs;
+}
+
 // out = [maxpool2](relu(a*(y - mean) + b)), 4 channels per thread
 __global__ void __launch_bounds__(256) bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ a,
                                                         const float* __restrict__ b, const float* __restrict__ mean,
@@ -1482,6 +1579,21 @@ DDPX_API int ddpx_f32_bn_stats(const float* y, int P, int C, int R, float* part,
 DDPX_API int ddpx_f32_bn_finalize(const float* part, int T, int R, int P, int C, const float* gamma, const float* beta,
                                   float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
                                   float* a, float* b, float* mean, float* rstd, hipStream_t s) {
+  // few channel groups and many chunks: the split merge (DDPX_F32_BN_SPLIT=0 keeps the one-kernel merge)
+  static const bool split_ok = [] {
+    const char* e = getenv("DDPX_F32_BN_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (split_ok && training && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
+    const int S = min(kFinSplitMax, (T + 127) / 128);
+    const int Ts = (T + S - 1) / S;
+    const int Sr = (T + Ts - 1) / Ts;  // splits with a chunk range
+    hipLaunchKernelGGL(bn_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, R, P, C);
+    hipLaunchKernelGGL(bn_fin_m2_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, Sr, R, P, C);
+    hipLaunchKernelGGL(bn_fin_out_kernel, dim3(nblk(C, 64)), dim3(64), 0, s, Sr, P, C, gamma, beta, rmean, rvar, nbt,
+                       momentum, eps, a, b, mean, rstd);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, R, P, C, gamma, beta, rmean, rvar,
                      nbt, momentum, eps, training, a, b, mean, rstd);
   return (int)hipGetLastError();

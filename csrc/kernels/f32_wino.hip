@@ -322,8 +322,8 @@ constexpr int WSLOT = WX_BYTES + WD_BYTES;        // 25 KiB
 // WS (wave split): 0 = wave w owns output channels 16w.. and both input-channel halves (each wave transforms
 // all 32 channels' patches); 1 = wave w owns output channels 32(w/2).. and input channels 16(w%2).. (two dy
 // transforms, one patch transform per MFMA k-step: a third fewer LDS reads)
-template <int STAGES, int WS>
-__global__ void __launch_bounds__(NT, 2)
+template <int STAGES, int WS, int OCC = 2>
+__global__ void __launch_bounds__(NT, OCC)  // OCC workgroups (waves per SIMD) per CU
 wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int H,
                   int W, int Cp, int Co, int Pt, int L, int nb_ci, unsigned x_bytes, unsigned dy_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * WSLOT];
@@ -573,12 +573,19 @@ DDPX_API int ddpx_f32_wino_wgrad_ok(int H, int W, int Cp, int Co) {
           W % 2 == 0) ? 1 : 0;
 }
 
-// Splits of the tile range: enough workgroups for two rounds of the chip (2 per CU), >= 16 K-steps each.
+// Splits of the tile range: enough workgroups for one round of the chip (3 per CU), >= 16 K-steps each.
 DDPX_API int ddpx_f32_wino_wgrad_splits(int N, int H, int W, int Cp, int Co) {
   const int Pt = N * (H / 2) * (W / 2);
   const int nblk = (Cp / wino::WG_CI) * (Co / wino::WG_CO);
   const int maxS = Pt / (16 * wino::WKT) > 1 ? Pt / (16 * wino::WKT) : 1;
-  int S = (2 * 256 * 2 + nblk - 1) / nblk;
+  // DDPX_WINO_WGRAD_SLOTS: workgroups aimed for; default 768 = one round at three per CU (VGG layers 3.25 ms,
+  // 1024: 3.40, 1536: 3.38; profiles/r5_wino)
+  static const int slots = [] {
+    const char* e = getenv("DDPX_WINO_WGRAD_SLOTS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 768;
+  }();
+  int S = (slots + nblk - 1) / nblk;
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
   const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
@@ -597,15 +604,17 @@ DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, f
   const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
   const int nb_ci = Cp / wino::WG_CI;
   const int nwg = nb_ci * (Co / wino::WG_CO) * S;
-  // DDPX_WINO_WGRAD_VARIANT: ring depth 2|3 and wave split 0|1 (see wino_wgrad_kernel), e.g. "s3w1"; default
-  // s2w1 (VGG layers 3.55 ms vs 3.72 for s2w0; the ring depth changed nothing; profiles/r5_wino)
+  // DDPX_WINO_WGRAD_VARIANT: ring depth 2|3, wave split 0|1 (see wino_wgrad_kernel), "o3" = held to 168 VGPRs for
+  // three workgroups per CU, e.g. "s3w1"; default s2w1o3 (VGG layers 3.42 ms; s2w1 3.55-3.60, s2w0 3.72; the ring
+  // depth changed nothing; profiles/r5_wino)
   static const int variant = [] {
     const char* e = getenv("DDPX_WINO_WGRAD_VARIANT");
-    if (!e || e[0] != 's' || !e[1] || e[2] != 'w' || !e[3]) return 21;
+    if (!e || e[0] != 's' || !e[1] || e[2] != 'w' || !e[3]) return 121;
+    if (e[4] == 'o' && e[5] == '3') return 121 + (e[3] == '1' ? 0 : -1);  // "s2w1o3": 3 workgroups per CU
     return (e[1] == '3' ? 30 : 20) + (e[3] == '1' ? 1 : 0);
   }();
   switch (variant) {
-    case 21:  // default
+    case 21:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
                          Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
       break;
@@ -616,6 +625,14 @@ DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, f
     case 31:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<3, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
                          Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    case 120:
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 0, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp,
+                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+      break;
+    case 121:  // default
+      hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 1, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp,
+                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
       break;
     case 20:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 0>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,

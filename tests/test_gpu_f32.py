@@ -71,7 +71,8 @@ def test_conv_fwd_dgrad_wgrad(gpu, N, H, Ci, Co):
 
 
 @pytest.mark.parametrize("pool", [False, True])
-@pytest.mark.parametrize("N,H,C", [(16, 8, 128), (8, 4, 512), (4, 32, 64)])
+@pytest.mark.parametrize("N,H,C", [(16, 8, 128), (8, 4, 512), (4, 32, 64),
+                                   (256, 32, 64)])  # 1024 chunks of 64 channels: the split statistics merge
 def test_bn_relu_pool_fwd_bwd(gpu, pool, N, H, C):
     from ddpx.ops import f32
     torch.manual_seed(1)
