@@ -175,7 +175,7 @@ static int pick_fwd(int P, int C, int Co) {
   // 64-channel outputs at 32x32 (VGG conv0, DeepNN 128->64): 256x64, 2-deep (47.9 vs 53.4 us, 120.7 vs 159.9 us)
   if (Co <= 64 && P >= 524288 && !picks_r4()) return 23;
   if (Co <= 64) return 7;     // DeepNN's 64/32-channel layers at 16x16: 64x64, 3 stages
-  if (P <= 8192) return 5;    // 4x4 layers: 64x128, 3 stages
+  if (P <= 8192) return picks_r4() ? 5 : 14;  // 4x4 layers: 128x128 / 8 waves / 3 stages (55.1 vs 61.7 us for cfg 5)
   if (picks_r4()) return P >= 524288 ? 8 : 13;
   if (C <= 128) return 22;    // K <= 1152 (VGG conv1 @32, conv2 @16): 115.6 vs 149.3 us (cfg 8) on conv1
   return 13;                  // 256x256, 8 waves
