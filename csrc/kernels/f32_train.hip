@@ -1448,6 +1448,28 @@ __global__ void __launch_bounds__(256) nchw_flatten_kernel(const float* __restri
   else out[f] = x[i];
 }
 
+// bf16 version for the native DeepNN's classifier input (2048 = 32 channels x 8 x 8 features per image): one
+// workgroup per image stages the image's S x C values in LDS, so both the NHWC side and the (C, H, W) side are
+// read / written contiguously (2-byte elements).  S * C <= kFlatLds.
+constexpr int kFlatLds = 16384;
+__global__ void __launch_bounds__(256) nchw_flatten_bf16_kernel(const unsigned short* __restrict__ x, int S, int C,
+                                                                 int backward, unsigned short* __restrict__ out) {
+  __shared__ unsigned short img[kFlatLds];
+  const int SC = S * C;
+  const size_t base = (size_t)blockIdx.x * SC;
+  for (int i = threadIdx.x; i < SC; i += 256) img[i] = x[base + i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < SC; j += 256) {
+    if (backward) {  // out NHWC j = s * C + c  <-  x (C, S) order c * S + s
+      const int sp = j / C, c = j - sp * C;
+      out[base + j] = img[c * S + sp];
+    } else {         // out (C, S) order j = c * S + s  <-  x NHWC s * C + c
+      const int c = j / S, sp = j - c * S;
+      out[base + j] = img[sp * C + c];
+    }
+  }
+}
+
 // 0 = 128x128, 1 = 128x64, 2 = 64x64, 3 = 64x128.  Thin operands get the tile that does not compute padding:
 // M <= 64 (the weight gradients of 64-channel layers: M = Co) takes 64-row tiles.
 static int auto_tile(int M, int N, int splits) {
@@ -1695,6 +1717,13 @@ DDPX_API int ddpx_f32_colsum(const float* x, int M, int N, float* out, int accum
 
 DDPX_API int ddpx_f32_nchw_flatten(const float* x, int N, int S, int C, int backward, float* out, hipStream_t s) {
   hipLaunchKernelGGL(nchw_flatten_kernel, dim3(nblk((long)N * S * C)), dim3(256), 0, s, x, N, S, C, backward, out);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_bf16_nchw_flatten(const void* x, int N, int S, int C, int backward, void* out, hipStream_t s) {
+  if (S * C > kFlatLds || N <= 0) return -1;
+  hipLaunchKernelGGL(nchw_flatten_bf16_kernel, dim3(N), dim3(256), 0, s, (const unsigned short*)x, S, C, backward,
+                     (unsigned short*)out);
   return (int)hipGetLastError();
 }
 

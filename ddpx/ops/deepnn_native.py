@@ -108,6 +108,24 @@ def bias_act_backward(gout, y, bias, N, H, W, C, pool, plan, dbias, accumulate=F
     return dy
 
 
+def _nchw_flatten(x, nhwc=None):
+    """NHWC [N,H,W,C] -> [N, C*H*W] in torch's (C, H, W) flatten order; with ``nhwc`` = (N, H, W, C) the inverse
+    (the gradient of [N, C*H*W] back to NHWC).  One native launch (csrc/kernels/f32_train.hip)."""
+    lib = native.kernels()
+    if nhwc is None:
+        N, H, W, C = x.shape
+        out = torch.empty((N, C * H * W), dtype=x.dtype, device=x.device)
+        back = 0
+    else:
+        N, H, W, C = nhwc
+        out = torch.empty((N, H, W, C), dtype=x.dtype, device=x.device)
+        back = 1
+    K._req(x.dtype == torch.bfloat16 and x.is_contiguous(), "flatten: contiguous bf16 expected")
+    native.check(lib.ddpx_bf16_nchw_flatten(x.data_ptr(), N, H * W, C, back, out.data_ptr(), native.stream_handle()),
+                 "ddpx_bf16_nchw_flatten")
+    return out
+
+
 def _forward(model, x, targets, want_logits, want_grad, training):
     plan = plan_of(model)
     flat = plan.lin0.weight._ddpx_flat
@@ -122,7 +140,7 @@ def _forward(model, x, targets, want_logits, want_grad, training):
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co
     # torch.flatten(x, 1) of the NCHW tensor: features in (C, H, W) order
-    feat = x.permute(0, 3, 1, 2).reshape(N, C * H * W).contiguous()
+    feat = _nchw_flatten(x)
     a0 = G.linear_fwd(feat, flat.shadow_of(plan.lin0.weight), plan.lin0.bias, relu=True)
     p = float(plan.drop.p)
     drop = training and p > 0.0
@@ -167,7 +185,7 @@ def _backward(model, saved, last, dl, grad_out):
         G.linear_wgrad(dd0, feat, dW0, accumulate=acc)
         flat.grad_done(l0.weight)
     N, Hf, Wf, Cf = xshape
-    g = dfeat.view(N, Cf, Hf, Wf).permute(0, 2, 3, 1).contiguous()
+    g = _nchw_flatten(dfeat, (N, Hf, Wf, Cf))
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, pool = plan.blocks[bi]
         x, y, (N, H, W, C, Co), _ = saved[bi]

@@ -90,6 +90,7 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_bn_bwd_tail", I, P, P, P, P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, I, I, P, P, P, P, P, P, F, F,
          P)
     _sig(lib, "ddpx_bias_act_bwd", I, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, I, I, P, P)
+    _sig(lib, "ddpx_bf16_nchw_flatten", I, P, I, I, I, I, P, P)
     _sig(lib, "ddpx_dropout_fwd", I, P, P, I64, F, P, P, P)
     _sig(lib, "ddpx_avgpool", I, P, I, I, I, P, P)
     _sig(lib, "ddpx_avgpool_bwd", I, P, I, I, I, P, P)

@@ -103,6 +103,17 @@ def test_dropout_kernel_statistics_and_graph(gpu):
     assert rows.min().item() > 0.8 and rows.max().item() < 0.97
 
 
+@pytest.mark.parametrize("shape", [(512, 8, 8, 32), (3, 5, 7, 24)])
+def test_bf16_nchw_flatten_both_ways(gpu, shape):
+    """The native classifier-input flatten: NHWC -> torch's (C, H, W) order and back, bit for bit."""
+    from ddpx.ops.deepnn_native import _nchw_flatten
+    N, H, W, C = shape
+    x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
+    f = _nchw_flatten(x)
+    assert torch.equal(f, x.permute(0, 3, 1, 2).reshape(N, C * H * W))
+    assert torch.equal(_nchw_flatten(f, (N, H, W, C)), x)
+
+
 def test_deepnn_native_matches_torch(gpu):
     """Whole native DeepNN (bf16) vs torch fp32 with dropout disabled (p = 0 on both), error budget set by
     torch's own bf16 autocast error on the same batch."""
