@@ -36,10 +36,25 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // each thread gathers its 8 source bytes (L2/Infinity-Cache hits) and writes
 // 8 contiguous outputs with one 16-B (bf16) or two 16-B (fp32) stores.
 // NHWC layouts: one thread per (sample, row, pixel), C channels each.
+// Per-sample crop offsets and flip, from the counter-based hash (the CPU twin draws the same).
+__device__ __forceinline__ void sample_params(uint64_t seed, int b, int pad, int train, int& dy, int& dx, int& flip) {
+  dy = pad;
+  dx = pad;
+  flip = 0;
+  if (train) {
+    const uint64_t r = splitmix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(b + 1)));
+    dy = (int)mod64(r, 2 * pad + 1);
+    dx = (int)mod64(r >> 16, 2 * pad + 1);
+    flip = (int)((r >> 40) & 1);
+  }
+}
+
+// prm (optional, LDS): [dy, dx, flip] of samples b0, b0 + 1, ... drawn once per workgroup (the hash and its
+// 64-bit remainders cost more VALU than the rest of a thread's work, and up to 384 threads share a sample)
 __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images, const int64_t* __restrict__ labels,
                                              const int64_t* __restrict__ idx, int B, int C, int H, int W, int pad,
                                              uint64_t seed, int train, int layout, void* __restrict__ out,
-                                             int64_t* __restrict__ tgt_out) {
+                                             int64_t* __restrict__ tgt_out, const int* prm = nullptr, int b0 = 0) {
   const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
                      layout == OUT_NHWC4_F32);
   const int G = W / 8;  // 8-pixel groups per row (W % 8 == 0 checked on the host)
@@ -58,12 +73,13 @@ __device__ __forceinline__ void augment_body(const uint8_t* __restrict__ images,
     b = t / (G * H * C);
   }
   const int64_t src = idx ? idx[b] : b;
-  int dy = pad, dx = pad, flip = 0;
-  if (train) {
-    const uint64_t r = splitmix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(b + 1)));
-    dy = (int)mod64(r, 2 * pad + 1);
-    dx = (int)mod64(r >> 16, 2 * pad + 1);
-    flip = (int)((r >> 40) & 1);
+  int dy, dx, flip;
+  if (prm) {
+    dy = prm[(b - b0) * 3];
+    dx = prm[(b - b0) * 3 + 1];
+    flip = prm[(b - b0) * 3 + 2];
+  } else {
+    sample_params(seed, b, pad, train, dy, dx, flip);
   }
   if (tgt_out && y == 0 && c == 0 && xg == 0 && xo == 0) tgt_out[b] = labels[src];
   const int sy = y + dy - pad;
@@ -152,7 +168,28 @@ augment_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ l
     idx += (size_t)(k % nbatch) * B;
     seed += (uint64_t)k;
   }
-  augment_body(images, labels, idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);
+  constexpr int kMaxSamples = 8;
+  __shared__ int prm[kMaxSamples * 3];
+  const bool nhwc = (layout == OUT_NHWC_BF16 || layout == OUT_NHWC_F32 || layout == OUT_NHWC8_BF16 ||
+                     layout == OUT_NHWC4_F32);
+  const int per = nhwc ? H * W : C * H * (W / 8);  // threads per sample
+  const int total = B * per;
+  const int t0 = blockIdx.x * blockDim.x;
+  const int t1 = min(total, t0 + (int)blockDim.x) - 1;
+  const int b0 = t0 / per, nb = t1 >= t0 ? t1 / per - b0 + 1 : 0;
+  if (nb > kMaxSamples) {  // tiny images: every thread draws its own sample's parameters
+    augment_body(images, labels, idx, B, C, H, W, pad, seed, train, layout, out, tgt_out);
+    return;
+  }
+  if ((int)threadIdx.x < nb) {
+    int dy, dx, flip;
+    sample_params(seed, b0 + (int)threadIdx.x, pad, train, dy, dx, flip);
+    prm[threadIdx.x * 3] = dy;
+    prm[threadIdx.x * 3 + 1] = dx;
+    prm[threadIdx.x * 3 + 2] = flip;
+  }
+  __syncthreads();
+  augment_body(images, labels, idx, B, C, H, W, pad, seed, train, layout, out, tgt_out, prm, b0);
 }
 
 }  // namespace ddpx
