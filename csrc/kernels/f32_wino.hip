@@ -39,6 +39,25 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)lds_wave_base, 16, voff, 0, 0, 0);
 }
 
+// n / d for 0 <= n < 2^31 by multiply-high: s = ceil(log2 d), magic = ceil(2^(31+s) / d), n / d = umulhi(n, magic)
+// >> (s - 1); d == 1: magic 0 (identity)
+struct WDiv {
+  unsigned magic;
+  int shift;
+};
+static inline WDiv make_wdiv(int d) {
+  WDiv f{0u, 0};
+  if (d <= 1) return f;
+  int s = 0;
+  while ((1ll << s) < d) ++s;
+  f.shift = s - 1;
+  f.magic = (unsigned)(((1ull << (31 + s)) + (unsigned long long)d - 1) / (unsigned long long)d);
+  return f;
+}
+__device__ __forceinline__ int wdiv(int n, WDiv f) {
+  return f.magic ? (int)(__umulhi((unsigned)n, f.magic) >> f.shift) : n;
+}
+
 // y (+ stats) = conv3x3(x) through F(2,3).  x: NHWC [N][H][W][C]; U: [16][C][K]; y: [N*H*W][K].
 template <int STAGES, int WAVES_PER_SIMD>
 __global__ void __launch_bounds__(NT, WAVES_PER_SIMD)  // 2: <= 256 VGPR + AGPR (128 are accumulators); 3: <= 168
@@ -325,7 +344,8 @@ constexpr int WSLOT = WX_BYTES + WD_BYTES;        // 25 KiB
 template <int STAGES, int WS, int OCC = 2>
 __global__ void __launch_bounds__(NT, OCC)  // OCC workgroups (waves per SIMD) per CU
 wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int H,
-                  int W, int Cp, int Co, int Pt, int L, int nb_ci, unsigned x_bytes, unsigned dy_bytes) {
+                  int W, int Cp, int Co, int Pt, int L, int nb_ci, unsigned x_bytes, unsigned dy_bytes, WDiv d_thw,
+                  WDiv d_tw) {
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * WSLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -338,38 +358,35 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, dy_bytes, 0x00020000);
 
-  // DMA roles (per K-step): patch instruction j = 4*wave + u (u < 4): tile j/2, patch rows 2(j%2), 2(j%2)+1
-  // (lane = (pixel q%8 of the half, 16-B chunk c of the 32 channels)); dy instruction u < 2: tile 2*wave + u,
-  // lane = (pixel q = lane/16, 16-B chunk lane%16 of the 64 channels)
+  // DMA roles (per K-step): wave w fetches tiles 2w and 2w + 1: each tile's patch in two instructions of 8
+  // pixels (lane = (pixel q%8 of the half, 16-B chunk c of the 32 channels)) and its dy in one (lane = (pixel q =
+  // lane/16, 16-B chunk lane%16 of the 64 channels)).  A tile's (n, th, tw) by multiply-high division, once per
+  // K-step (the v_rcp-based divisions per instruction were 4.6 VALU per MFMA, PMC in profiles/r5_wino)
   auto issue = [&](int k) {
     char* slot = smem + (k % STAGES) * WSLOT;
     const int tb = t_beg + k * WKT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 4 * wave + u, t = j >> 1, half = j & 1;
-      const int q = half * 8 + (lane >> 3), c = lane & 7;
-      const int p = tb + t;
-      unsigned off = kOOB;
-      if (p < t_end) {
-        const int n = p / (TH * TW), r = p - n * (TH * TW);
-        const int th = r / TW, tw = r - th * TW;
-        const int h = 2 * th - 1 + (q >> 2), w = 2 * tw - 1 + (q & 3);
-        if (h >= 0 && h < H && w >= 0 && w < W) off = (unsigned)(((((size_t)n * H + h) * W + w) * Cp + ci0 + 4 * c) * 4);
-      }
-      dma16(rx, slot + (t * XS_T + half * 8 * WG_CI) * 4, off);
-    }
-#pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int t = 2 * wave + u, q = lane >> 4, c = lane & 15;
-      const int p = tb + t;
-      unsigned off = kOOB;
-      if (p < t_end) {
-        const int n = p / (TH * TW), r = p - n * (TH * TW);
-        const int th = r / TW, tw = r - th * TW;
-        const size_t pix = ((size_t)n * H + 2 * th + (q >> 1)) * W + 2 * tw + (q & 1);
-        off = (unsigned)((pix * Co + co0 + 4 * c) * 4);
+      const int t = 2 * wave + u, p = tb + t;
+      const bool pv = p < t_end;
+      int n = 0, th = 0, tw = 0;
+      if (pv) {
+        n = wdiv(p, d_thw);
+        const int r = p - n * (TH * TW);
+        th = wdiv(r, d_tw);
+        tw = r - th * TW;
       }
-      dma16(rd, slot + WX_BYTES + t * DS_T * 4, off);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int q = half * 8 + (lane >> 3), c = lane & 7;
+        const int h = 2 * th - 1 + (q >> 2), w = 2 * tw - 1 + (q & 3);
+        const bool ok = pv && h >= 0 && h < H && w >= 0 && w < W;
+        dma16(rx, slot + (t * XS_T + half * 8 * WG_CI) * 4,
+              ok ? (unsigned)(((((size_t)n * H + h) * W + w) * Cp + ci0 + 4 * c) * 4) : kOOB);
+      }
+      const int q = lane >> 4, c = lane & 15;
+      const size_t pix = ((size_t)n * H + 2 * th + (q >> 1)) * W + 2 * tw + (q & 1);
+      dma16(rd, slot + WX_BYTES + t * DS_T * 4, pv ? (unsigned)((pix * Co + co0 + 4 * c) * 4) : kOOB);
     }
   };
 
@@ -604,6 +621,7 @@ DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, f
   const int L = ((Pt + S - 1) / S + wino::WKT - 1) / wino::WKT * wino::WKT;
   const int nb_ci = Cp / wino::WG_CI;
   const int nwg = nb_ci * (Co / wino::WG_CO) * S;
+  const wino::WDiv dthw = wino::make_wdiv((H / 2) * (W / 2)), dtw = wino::make_wdiv(W / 2);
   // DDPX_WINO_WGRAD_VARIANT: ring depth 2|3, wave split 0|1 (see wino_wgrad_kernel), "o3" = held to 168 VGPRs for
   // three workgroups per CU, e.g. "s3w1"; default s2w1o3 (VGG layers 3.42 ms; s2w1 3.55-3.60, s2w0 3.72; the ring
   // depth changed nothing; profiles/r5_wino)
@@ -616,27 +634,27 @@ DDPX_API int ddpx_f32_wino_wgrad(const float* x, const float* dy, float* part, f
   switch (variant) {
     case 21:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
-                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     case 30:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<3, 0>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
-                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     case 31:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<3, 1>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
-                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     case 120:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 0, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp,
-                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     case 121:  // default
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 1, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp,
-                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Co, Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     case 20:
       hipLaunchKernelGGL((wino::wino_wgrad_kernel<2, 0>), dim3(nwg), dim3(wino::NT), 0, s, x, dy, part, H, W, Cp, Co,
-                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db);
+                         Pt, L, nb_ci, (unsigned)xb, (unsigned)db, dthw, dtw);
       break;
     default:
       return -5;

@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out/r5bf
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_f32.py -k "wino_wgrad" > gpurun_out/r5bf/tests.log 2>&1
+echo tests rc=$?
+timeout -k 10 200 python benchmarks/wino_bench.py --only wgrad --out gpurun_out/r5bf/wgrad.json > gpurun_out/r5bf/wgrad.log 2>&1
+echo bench rc=$?
+timeout -k 10 300 python bench.py --model vgg --dtype fp32 --steps 20 --warmup 3 --stock_ref 0 > gpurun_out/r5bf/vgg32.log 2>&1
+echo b1 rc=$?
