@@ -949,6 +949,7 @@ gemm_pipe_kernel(Params p) {
   float* red = T + BMH * TLD;
   float* colres = red + (NT / (BN / 4)) * BN;
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;  // EPI_BNSTAT: the tile's statistics merged over its row parts
 #pragma unroll
   for (int h = 0; h < EH; ++h) {
     if (h == 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the last LDS slot
@@ -1005,8 +1006,9 @@ gemm_pipe_kernel(Params p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) cs[q] += ch[q];
     if (LW == 0 && p.colsum && p.epi == EPI_BNSTAT_BF16) {
-      // BatchNorm statistics of the stored (bf16-rounded) values per BMH-row stat tile (tm*EH + h):
-      // tile mean, then M2 = sum (y - mean)^2 over this half's rows.
+      // BatchNorm statistics of the stored (bf16-rounded) values of the BMH-row part: its mean, then M2 = sum
+      // (y - mean)^2 over its rows; the parts are Chan-merged in order in registers and the tile writes ONE
+      // statistics row (tm): a quarter / half of the tiles to merge for the 256x256 / 2-deep 128x128 tiles
       __syncthreads();
       quad_colsum<BN, NT>(red, ch, tid, colres);
       const int rows_valid = min(BMH, p.M - mh);
@@ -1030,10 +1032,25 @@ gemm_pipe_kernel(Params p) {
         }
         quad_colsum<BN, NT>(red, m2, tid, colres);
       }
-      const size_t st = (size_t)tm * EH + h;
-      if (tid < BN && n0 + tid < p.N) {
-        p.colsum[(st * 2) * p.N + n0 + tid] = tmean[tid];
-        p.colsum[(st * 2 + 1) * p.N + n0 + tid] = colres[tid];
+      if (tid < BN) {
+        const float nb = (float)max(rows_valid, 0);
+        if (nb > 0.f) {
+          const float mb = tmean[tid], qb = colres[tid];
+          if (st_n == 0.f) {
+            st_n = nb;
+            st_mean = mb;
+            st_m2 = qb;
+          } else {
+            const float nn = st_n + nb, d = mb - st_mean;
+            st_mean += d * (nb / nn);
+            st_m2 += qb + d * d * (st_n * nb / nn);
+            st_n = nn;
+          }
+        }
+        if (h == EH - 1 && n0 + tid < p.N) {
+          p.colsum[((size_t)tm * 2) * p.N + n0 + tid] = st_mean;
+          p.colsum[((size_t)tm * 2 + 1) * p.N + n0 + tid] = st_m2;
+        }
       }
     }
   }
@@ -1100,7 +1117,8 @@ constexpr int kNumCfgs = 24;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
 static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
 
-// Row-parts the epilogue stages the tile in (BatchNorm statistics come out per part).
+// Row-parts the epilogue stages the tile in (the data gradient's BatchNorm backward sums come out per part; the
+// forward statistics are merged to one row per tile).
 static inline int epilogue_halves(int cfg) { return cfg == 13 ? 4 : (cfg == 21 || cfg == 22) ? 2 : 1; }
 
 static inline void tile_of(int cfg, int* bm, int* bn) {

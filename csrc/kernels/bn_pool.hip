@@ -141,10 +141,10 @@ static inline int merge_mode() {
   }
   return g_merge_mode;
 }
-// forward statistics: the default mode still splits the merge when the tile count is large (T >= 4096: VGG conv1
-// with the 128x128 forward tile's 64-row statistics, 8192 tiles: the per-channel kernel's strided loads took
-// 25.5 us there, profiles/r5_conv/NOTES.md)
-static inline bool merge_legacy(int T = 0) { return merge_mode() == 1 || (merge_mode() == 2 && T < 4096); }
+// forward statistics: the default mode still splits the merge when the tile count is large (T > 4096: the
+// per-channel kernel's strided loads took 25.5 us at T = 8192, profiles/r5_conv/NOTES.md; the conv epilogue now
+// writes one statistics row per row tile, so VGG's largest is conv1's 4096)
+static inline bool merge_legacy(int T = 0) { return merge_mode() == 1 || (merge_mode() == 2 && T <= 4096); }
 static inline bool merge_legacy_bwd() { return merge_mode() == 1; }    // backward sums
 __device__ int g_merge_tickets[2][kMergeMaxC / 64];
 __device__ float g_fin_scratch[kFinMaxS * 3 * kMergeMaxC];

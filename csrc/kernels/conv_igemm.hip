@@ -228,14 +228,14 @@ DDPX_API int ddpx_conv_fwd_tiles_m(int P, int C, int Co, int tile_cfg) {
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
   int bm, bn;
   tile_of(cfg, &bm, &bn);
-  return (P + bm - 1) / bm * epilogue_halves(cfg);
+  return (P + bm - 1) / bm;  // one statistics row per row tile (the epilogue merges its row parts)
 }
 
 DDPX_API int ddpx_conv_fwd_tile_rows(int P, int C, int Co, int tile_cfg) {
   const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
   int bm, bn;
   tile_of(cfg, &bm, &bn);
-  return bm / epilogue_halves(cfg);
+  return bm;
 }
 
 // y[P][Co] = conv(x, W).  x NHWC [N][H][W][C] bf16 (C % 8 == 0), wf [Co][9][C].
