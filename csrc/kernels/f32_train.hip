@@ -796,6 +796,21 @@ constexpr int kFinSplitMax = 32, kFinSplitMaxC = 1024;
 __device__ double g_fin_s1[kFinSplitMax * kFinSplitMaxC];
 __device__ double g_fin_s2[kFinSplitMax * kFinSplitMaxC];
 
+// sum_{k < S} v[k * C + c] in k order, 8 loads in flight (the fp64 adds stay in order: deterministic)
+__device__ __forceinline__ double fin_split_sum(const double* v, int S, int C, int c) {
+  double r = 0.0;
+  int k = 0;
+  for (; k + 8 <= S; k += 8) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = v[(size_t)(k + u) * C + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r += t[u];
+  }
+  for (; k < S; ++k) r += v[(size_t)k * C + c];
+  return r;
+}
+
 __device__ __forceinline__ double fin_group_tree(double v, double (*red)[64], int g, int cl) {
   red[g][cl] = v;
   __syncthreads();
@@ -834,9 +849,7 @@ __global__ void __launch_bounds__(1024) bn_fin_m2_kernel(const float* __restrict
   const int t0 = sp * Ts, t1 = min(T, t0 + Ts);
   double m2 = 0.0;
   if (c < C) {
-    double m = 0.0;
-    for (int k = 0; k < S; ++k) m += g_fin_s1[(size_t)k * C + c];
-    m /= P;
+    const double m = fin_split_sum(g_fin_s1, S, C, c) / P;
     int t = t0 + g;
     for (; t + 7 * 16 < t1; t += 8 * 16) {
       float mv[8], qv[8];
@@ -869,10 +882,8 @@ __global__ void __launch_bounds__(64) bn_fin_out_kernel(int S, int P, int C, con
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  double m = 0.0, m2 = 0.0;
-  for (int k = 0; k < S; ++k) m += g_fin_s1[(size_t)k * C + c];
-  m /= P;
-  for (int k = 0; k < S; ++k) m2 += g_fin_s2[(size_t)k * C + c];
+  const double m = fin_split_sum(g_fin_s1, S, C, c) / P;
+  const double m2 = fin_split_sum(g_fin_s2, S, C, c);
   const float mu = (float)m, var = (float)(m2 / P);
   const float unb = P > 1 ? (float)(m2 / (P - 1)) : var;
   rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
