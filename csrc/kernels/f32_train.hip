@@ -1028,6 +1028,60 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s1 : (float)s1;
 }
 
+// The same sums split over chunk ranges for few channel groups and many chunks (BN0's 64 channels x 2048 chunks
+// took 29 us in one workgroup): per split, the 16-group interleave and tree of bn_bwd_finalize_kernel into the
+// split scratch; then the splits in order (bn_bwd_fin_out_kernel).  Deterministic.
+__global__ void __launch_bounds__(1024) bn_bwd_fin_sum_kernel(const float* __restrict__ part, int T, int Ts, int C) {
+  __shared__ double red[2][16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
+  const int t0 = sp * Ts, t1 = min(T, t0 + Ts);
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    int t = t0 + g;
+    for (; t + 7 * 16 < t1; t += 8 * 16) {
+      float v1[8], v2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v1[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+        v2[u] = part[(size_t)(t + 16 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += v1[u];
+        s2 += v2[u];
+      }
+    }
+    for (; t < t1; t += 16) {
+      s1 += part[(size_t)t * 2 * C + c];
+      s2 += part[(size_t)t * 2 * C + C + c];
+    }
+  }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  s1 = s2 = 0.0;
+  for (int k = 0; k < 16; ++k) {
+    s1 += red[0][k][cl];
+    s2 += red[1][k][cl];
+  }
+  g_fin_s1[(size_t)sp * C + c] = s1;
+  g_fin_s2[(size_t)sp * C + c] = s2;
+}
+
+__global__ void __launch_bounds__(64) bn_bwd_fin_out_kernel(int S, int P, int C, float* __restrict__ c1,
+                                                             float* __restrict__ c2, float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  const double s1 = fin_split_sum(g_fin_s1, S, C, c), s2 = fin_split_sum(g_fin_s2, S, C, c);
+  c1[c] = (float)(s1 / P);
+  c2[c] = (float)(s2 / P);
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s2 : (float)s2;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s1 : (float)s1;
+}
+
 // dy = a * (gz - c1 - xhat * c2)
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ y,
                                                             const float* __restrict__ a, const float* __restrict__ b,
@@ -1667,6 +1721,19 @@ DDPX_API int ddpx_f32_bn_bwd_sums(const float* g, const float* y, const float* a
 
 DDPX_API int ddpx_f32_bn_bwd_finalize(const float* part, int T, int P, int C, float* c1, float* c2, float* dgamma,
                                       float* dbeta, int accumulate, hipStream_t s) {
+  static const bool split_ok = [] {
+    const char* e = getenv("DDPX_F32_BN_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (split_ok && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
+    const int S = min(kFinSplitMax, (T + 127) / 128);
+    const int Ts = (T + S - 1) / S;
+    const int Sr = (T + Ts - 1) / Ts;
+    hipLaunchKernelGGL(bn_bwd_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, C);
+    hipLaunchKernelGGL(bn_bwd_fin_out_kernel, dim3(nblk(C, 64)), dim3(64), 0, s, Sr, P, C, c1, c2, dgamma, dbeta,
+                       accumulate);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, P, C, c1, c2, dgamma, dbeta,
                      accumulate);
   return (int)hipGetLastError();
