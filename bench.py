@@ -45,6 +45,7 @@ import subprocess
 import sys
 import time
 
+_PF_SEQ = __import__("itertools").count()
 BASELINE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
 LAUNCHER_ENV = "DDPX_BENCH_LAUNCHER"
 
@@ -109,7 +110,8 @@ def parse(argv=None):
                    help="ZeRO-1 only: all-gathers issued at the start of the next step, waited per chunk")
     p.add_argument("--side_optimizer", type=int, default=None,
                    help="replicated plan with optimizer overlap: each bucket's SGD update on a side stream behind its "
-                        "all-reduce and its weights' last read in backward, one join per step (default 1)")
+                        "all-reduce and its weights' last read in backward, one join per step (default 0: measured "
+                        "slower at world size 1, profiles/r5_ddp1; DDPX_SIDE_OPTIMIZER=1 flips it)")
     p.add_argument("--comm_side_optimizer", type=int, default=None,
                    help="ZeRO-1 only: shard updates on the RCCL stream behind each reduce-scatter")
     p.add_argument("--first_bucket_mb", type=float, default=None)
@@ -137,9 +139,12 @@ def parse(argv=None):
     p.add_argument("--stock_first", type=int, default=None,
                    help="1: time the stock recipe BEFORE the ddpx warm-up instead of after the ddpx timing "
                         "(default 0)")
-    p.add_argument("--stock_between", type=int, default=1,
+    p.add_argument("--stock_between", type=int, default=None,
                    help="1: time the stock recipe after the ddpx graph capture, before the last ddpx warm-up steps "
-                        "(the timed window then starts on a GPU at sustained-load clocks); 0: after the timed steps")
+                        "(the timed window then starts on a GPU at sustained-load clocks; default for one process); "
+                        "0: after the timed steps (default with DDP: N > 1 or --ddp_single).  With DDP and 0 the ddpx "
+                        "JSON line is printed BEFORE the stock recipe starts (its result goes to stderr and "
+                        "--json_out), so nothing in the optional comparison can cost the job its headline line")
     p.add_argument("--seed", type=int, default=0, help="model init seed (identical replicas are also enforced by DDP)")
     return p.parse_args(argv)
 
@@ -280,6 +285,10 @@ def resolve_defaults(args, world):
     if args.stock_ref is None:
         args.stock_ref = int(args.impl == "ddpx" and (not args.ddp_single or bool(args.stock_ddp))
                              and args.comm == "rccl")
+    if args.stock_between is None:
+        # N > 1: the stock torch-DDP run opens a second NCCL communicator next to ddpx's own; it runs only after the
+        # ddpx line is out
+        args.stock_between = int(not multi)
     if args.stock_first is None:
         # measured (profiles/r3_val): stock-first gives the stock recipe a cold GPU (0.88-0.90 vs 0.62-0.73 ms) and
         # ddpx no clear gain, so the baseline runs last unless asked
@@ -427,6 +436,7 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
     cpu = device.type == "cpu"
     bs = args.batch_size
     runner = None
+    closers = []
     if args.impl == "ddpx" and not cpu:
         from ddpx.runtime.graphs import (CapturedCycle, CapturedStep, GraphedSteps, agree_all_ranks,
                                          pingpong_signature_of, restore_after_failed_capture, step_state_snapshot)
@@ -466,8 +476,10 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
             # buffer from its own device cursor (batch index = augments issued so far)
             bufs = [(static_x, static_y), (torch.empty_like(static_x), torch.empty_like(static_y))]
             side = torch.cuda.Stream(device)
-            from ddpx.runtime.graphs import register_side_stream
-            register_side_stream(side, f"prefetch stream #{id(side)}")  # joined back / reset by a failed capture
+            from ddpx.runtime.graphs import register_side_stream, unregister_side_stream
+            pf_name = f"prefetch stream #{next(_PF_SEQ)}"
+            register_side_stream(side, pf_name)  # joined back / reset by a failed capture
+            closers.append(lambda: unregister_side_stream(pf_name))
             data_ctr = counter.clone()
             loader.cursor_batch(idx_dev, nfull, *bufs[0], counter=data_ctr)  # batch of the first step
             data_ctr.add_(1)
@@ -575,13 +587,16 @@ def make_runner(args, device, world, loader, idx_all, full, comm=None):
             runner.graphs = None
         if net is not model and hasattr(net, "close"):
             net.close()
+        for c in closers:
+            c()
+        closers.clear()
 
     return argparse.Namespace(model=model, net=net, opt=opt, sched=sched, run=run, runner=runner,
                               close=close)
 
 
 
-def calibrate_plan(args, device, world, loader, idx_all, full, comm):
+def calibrate_plan(args, device, world, loader, idx_all, full, comm, rank=0):
     """Start-up calibration (``ddpx.parallel.calibrate``): build every candidate gradient-communication plan for
     real (its own model copy, DDP buckets and optimizer, graph-captured like the timed run), time a few
     training steps of each, and set ``args``' bucket caps / ZeRO-1 choice to the fastest.  Collective."""
@@ -590,6 +605,7 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
     import torch
     from ddpx.models import build_model
     from ddpx.parallel.calibrate import calibrate_by_step, candidate_plans
+    from ddpx.utils.faults import maybe_inject
     from ddpx.runtime.flat_params import flat_of
     from ddpx.runtime.setup import prepare_model
     cpu = device.type == "cpu"
@@ -641,6 +657,8 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
         k = [0]
 
         def step():
+            if k[0] == 0:
+                maybe_inject("calib", plan["name"], rank)  # tests: a candidate failing in its first step
             eng.run(k[0], 1)
             k[0] += 1
 
@@ -653,55 +671,119 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm):
                 torch.cuda.empty_cache()
         return step, close
 
-    chosen, table = calibrate_by_step(plans, make_trial, sync=sync, warm=3, reps=3 if cpu else 5,
-                                      rounds=1 if cpu else 3)
+    try:
+        chosen, table = calibrate_by_step(plans, make_trial, sync=sync, warm=3, reps=3 if cpu else 5,
+                                          rounds=1 if cpu else 3)
+    except RuntimeError as e:
+        # every candidate failed on some rank (agreed): torch's default plan, replicated optimizer
+        args.bucket_cap_mb = 25.0 if args.bucket_cap_mb is None else args.bucket_cap_mb
+        args.first_bucket_mb = 1.0 if args.first_bucket_mb is None else args.first_bucket_mb
+        if args.shard_optimizer is None:
+            args.shard_optimizer = 0
+        resolve_zero_defaults(args)
+        args.calibration = {"chosen": None, "error": str(e)[:600], "fallback": "torch default caps (25/1 MiB)"}
+        return
     apply(args, chosen)
+    dropped = sorted(k for k, v in table.items() if isinstance(v, dict))
     args.calibration = {"chosen": chosen["name"], "objective": "training step ms (max over ranks)",
-                        "step_ms": table}
+                        "step_ms": table, "dropped": dropped or None}
 
 
 def measure_stock_same_run(args, device, world, rank, idx_all, full):
-    """The stock PyTorch-ROCm recipe timed in this job (after the ddpx timing unless --stock_first 1), on the
-    same data:
-    torch.nn model + bf16 autocast (fp32 when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its
-    own RCCL process group (the reference's ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same
-    timing rule as the ddpx line: barrier + synchronize on both sides, max over ranks.  Collective."""
+    """The stock PyTorch-ROCm recipe timed in this job, on the same data: torch.nn model + bf16 autocast (fp32
+    when --dtype fp32) + foreach SGD, and at N > 1 torch DDP over its own RCCL process group (the reference's
+    ``DDP(model, device_ids=[gpu_id])``, multigpu.py:89).  Same timing rule as the ddpx line: barrier +
+    synchronize on both sides, max over ranks.  Collective.
+
+    Never raises: any failure on any rank is agreed over the CPU group at the phase boundaries and returned as
+    ``{"error": ...}`` on every rank (an optional comparison must not cost the job its line).
+    Phase 1 (local: data, fault injection) is always met by every rank; a rank failing later, inside the stock
+    DDP's own collectives, is covered by the bounded tail (:func:`_arm_tail_watchdog`) when the stock run comes
+    after the ddpx line."""
     import torch
     import torch.distributed as dist
+    from ddpx.runtime.graphs import agree_all_ranks
+    from ddpx.utils.faults import maybe_inject
     a = argparse.Namespace(**vars(args))
     a.impl, a.torch_amp = "torch", args.dtype != "fp32"
     cuda = device.type == "cuda"
-    loader = make_data(a, device, rank, world)  # the stock model's own (NCHW / flat fp32) input layout
     use_ddp = world > 1 or bool(getattr(args, "stock_ddp", 0))
-    group = dist.new_group(backend="nccl" if cuda else "gloo") if use_ddp else None
-    _, _, _, _, run = torch_runner(a, device, world, loader, idx_all, full, group=group)
+    err, group, loader = None, None, None
+
+    def fail(e):
+        return f"{type(e).__name__}: {e}"[:400]
 
     def sync():
         if cuda:
             torch.cuda.synchronize()
 
-    run(0, 5)
-    sync()
+    try:  # phase 1: local only
+        maybe_inject("stock", rank=rank)
+        loader = make_data(a, device, rank, world)  # the stock model's own (NCHW / flat fp32) input layout
+    except Exception as e:  # noqa: BLE001
+        err = fail(e)
+    if not agree_all_ranks(err is None):
+        return {"error": err or "another rank failed the stock recipe"}
+    dt = None
+    try:  # phase 2: the stock process group, model, DDP and its warm-up steps
+        if use_ddp:
+            import datetime
+            group = dist.new_group(backend="nccl" if cuda else "gloo", timeout=datetime.timedelta(seconds=120))
+        _, _, _, _, run = torch_runner(a, device, world, loader, idx_all, full, group=group)
+        maybe_inject("stock_run", rank=rank)
+        run(0, 5)
+        sync()
+    except Exception as e:  # noqa: BLE001
+        err = fail(e)
+    ok = agree_all_ranks(err is None)
+    if ok:
+        try:  # phase 3: the timed steps
+            sync()
+            t0 = time.perf_counter()
+            run(5, args.stock_steps)
+            sync()
+            dt = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            err = fail(e)
+        ok = agree_all_ranks(err is None)
+    if group is not None and ok:  # a failed group is left alone: tearing it down could block on its peers
+        try:
+            dist.destroy_process_group(group)
+        except Exception:  # noqa: BLE001
+            pass
+    if not ok:
+        return {"error": err or "another rank failed the stock recipe"}
     if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    run(5, args.stock_steps)
-    sync()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    if group is not None:
-        dist.destroy_process_group(group)
     dt /= args.stock_steps
     recipe = "torch.nn + " + ("fp32" if args.dtype == "fp32" or not cuda else "bf16 autocast") + " + foreach SGD"
     if use_ddp:
         recipe += " + torch DDP (" + ("RCCL" if cuda else "gloo") + ", 25/1 MiB buckets)"
     return {"ms_per_step": round(dt * 1000.0, 4), "samples_per_sec": round(world * args.batch_size / dt, 2),
             "recipe": recipe, "steps": args.stock_steps}
+
+
+def _vs_stock(value, stock):
+    return round(value / stock["samples_per_sec"], 4) if (stock and "samples_per_sec" in stock) else None
+
+
+def _arm_tail_watchdog(seconds: float):
+    """After the headline line is out: end this rank with status 0 if the optional tail (the stock torch-DDP
+    comparison, teardown) has not finished within ``seconds`` — a stuck stock collective must not turn a
+    measured job into a failed one."""
+    import threading
+
+    def fire():
+        print(f"bench.py: optional tail (stock comparison / teardown) exceeded {seconds:.0f} s; exiting 0 "
+              "(the ddpx line was already printed)", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(0)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def replica_digest(net, flat=None):
@@ -747,7 +829,7 @@ def main(argv=None):
 
     comm = make_comm(args, device, world)
     if getattr(args, "calibrate", False):
-        calibrate_plan(args, device, world, loader, idx_all, full, comm)
+        calibrate_plan(args, device, world, loader, idx_all, full, comm, rank=rank)
     if not cpu:
         from ddpx.runtime.graphs import assert_no_capture
         assert_no_capture("before building the timed engine")
@@ -821,8 +903,10 @@ def main(argv=None):
     if args.digest and args.impl == "ddpx":
         from ddpx.runtime.flat_params import flat_of
         digest = allck[rank] if ddpx_ddp else replica_digest(None, flat=flat_of(model))
-    if args.stock_ref and not args.stock_first and not args.stock_between:
+    stock_after = bool(args.stock_ref and not args.stock_first and not args.stock_between)
+    if stock_after and not multi:  # one process: no second communicator, the line can carry the comparison
         stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
+        stock_after = False
     value = world * bs * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
     metric = "samples_per_sec_whole_node"
@@ -884,8 +968,9 @@ def main(argv=None):
                    "master_digest": digest,
                    "comm_ms_per_step": round(cstats["comm_ms"], 4) if cstats else None,
                    "comm_exposed_ms_per_step": round(cstats["comm_exposed_ms"], 4) if cstats else None,
-                   "stock_same_run": stock,
-                   "vs_stock_same_run": (round(value / stock["samples_per_sec"], 4) if stock else None)},
+                   "stock_same_run": (stock if not stock_after else
+                                      {"placement": "after this line (DDP job): result on stderr / --json_out"}),
+                   "vs_stock_same_run": _vs_stock(value, stock)},
     }
     if rank == 0:
         line = json.dumps(rec)
@@ -893,6 +978,17 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "a") as f:
                 f.write(line + "\n")
+    if stock_after:
+        # the headline line is out; the stock torch-DDP comparison (a second NCCL communicator) runs now, bounded
+        _arm_tail_watchdog(float(os.environ.get("DDPX_BENCH_TAIL_S", "300")))
+        stock = measure_stock_same_run(args, device, world, rank, idx_all, full)
+        if rank == 0:
+            tail = json.dumps({"stock_same_run": stock, "vs_stock_same_run": _vs_stock(value, stock),
+                               "for_metric": metric, "n_gpus": world})
+            print("STOCK " + tail, file=sys.stderr, flush=True)
+            if args.json_out:
+                with open(args.json_out, "a") as f:
+                    f.write(tail + "\n")
     if multi:
         if args.impl == "ddpx" and hasattr(net, "close"):
             net.close()

@@ -18,7 +18,9 @@ CASES = ["fwd1_t7", "fwd1_t0", "fwd1_t8", "dgrad1_t3", "wgrad1_t5", "wgrad1_t8",
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", required=True, choices=CASES)
+    ap.add_argument("--case", required=True,
+                    help="one of CASES, or KIND_tT with KIND in fwd0 (fc0: K = 3072) / fwd1 / dgrad1 / wgrad1 / "
+                         "wgrad1sgd and T a dispatch tile (-1: the default plan)")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -42,13 +44,14 @@ def main():
         else:
             fn = lambda: G.linear_fwd(x, w, b, relu=True)  # noqa: E731
     else:
-        x = torch.randn(M, H, device=dev).to(torch.bfloat16)
-        w = (torch.randn(H, H, device=dev) * 0.02).to(torch.bfloat16)
-        b = torch.randn(H, device=dev)
-        dy = torch.randn(M, H, device=dev).to(torch.bfloat16)
         kind, tile = c.split("_t")
         tile = int(tile)
-        if kind == "fwd1":
+        K = 3072 if kind == "fwd0" else H
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(H, K, device=dev) * 0.02).to(torch.bfloat16)
+        b = torch.randn(H, device=dev)
+        dy = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        if kind in ("fwd0", "fwd1"):
             # tile -1: the default plan (in-launch split-K on 128x128 tiles for this shape)
             fn = lambda: G.linear_fwd(x, w, b, relu=True, tile=tile)  # noqa: E731
         elif kind == "dgrad1":

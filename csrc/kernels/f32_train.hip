@@ -791,10 +791,10 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
 // T = 2048 / 4096, one or two workgroups of the kernel above: 78 / 52 us).  Three launches: (1) per split the
 // fp64 sum of n * mean; (2) the mean from all splits' sums (split order), then per split the fp64 M2 sum;
 // (3) the M2 of all splits (split order) and the outputs.  Deterministic; within a split the same 16-group
-// interleave as bn_finalize_kernel.
+// interleave as bn_finalize_kernel.  The per-split partials live in a caller-allocated fp64 workspace
+// ws[2][kFinSplitMax][C] (stream-ordered by the caller's allocator: two merges in flight on different streams
+// cannot overwrite each other's partials).
 constexpr int kFinSplitMax = 32, kFinSplitMaxC = 1024;
-__device__ double g_fin_s1[kFinSplitMax * kFinSplitMaxC];
-__device__ double g_fin_s2[kFinSplitMax * kFinSplitMaxC];
 
 // sum_{k < S} v[k * C + c] in k order, 8 loads in flight (the fp64 adds stay in order: deterministic)
 __device__ __forceinline__ double fin_split_sum(const double* v, int S, int C, int c) {
@@ -820,7 +820,7 @@ __device__ __forceinline__ double fin_group_tree(double v, double (*red)[64], in
 }
 
 __global__ void __launch_bounds__(1024) bn_fin_sum_kernel(const float* __restrict__ part, int T, int Ts, int R,
-                                                           int P, int C) {
+                                                           int P, int C, double* __restrict__ fin_s1) {
   __shared__ double red[16][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
@@ -838,18 +838,19 @@ __global__ void __launch_bounds__(1024) bn_fin_sum_kernel(const float* __restric
     for (; t < t1; t += 16) sm += (double)min(R, P - t * R) * part[(size_t)t * 2 * C + c];
   }
   sm = fin_group_tree(sm, red, g, cl);
-  if (g == 0 && c < C) g_fin_s1[(size_t)sp * C + c] = sm;
+  if (g == 0 && c < C) fin_s1[(size_t)sp * C + c] = sm;
 }
 
 __global__ void __launch_bounds__(1024) bn_fin_m2_kernel(const float* __restrict__ part, int T, int Ts, int S, int R,
-                                                          int P, int C) {
+                                                          int P, int C, const double* __restrict__ fin_s1,
+                                                          double* __restrict__ fin_s2) {
   __shared__ double red[16][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
   const int t0 = sp * Ts, t1 = min(T, t0 + Ts);
   double m2 = 0.0;
   if (c < C) {
-    const double m = fin_split_sum(g_fin_s1, S, C, c) / P;
+    const double m = fin_split_sum(fin_s1, S, C, c) / P;
     int t = t0 + g;
     for (; t + 7 * 16 < t1; t += 8 * 16) {
       float mv[8], qv[8];
@@ -870,7 +871,7 @@ __global__ void __launch_bounds__(1024) bn_fin_m2_kernel(const float* __restrict
     }
   }
   m2 = fin_group_tree(m2, red, g, cl);
-  if (g == 0 && c < C) g_fin_s2[(size_t)sp * C + c] = m2;
+  if (g == 0 && c < C) fin_s2[(size_t)sp * C + c] = m2;
 }
 
 __global__ void __launch_bounds__(64) bn_fin_out_kernel(int S, int P, int C, const float* __restrict__ gamma,
@@ -878,12 +879,14 @@ __global__ void __launch_bounds__(64) bn_fin_out_kernel(int S, int P, int C, con
                                                          float* __restrict__ rvar, int64_t* __restrict__ nbt,
                                                          float momentum, float eps, float* __restrict__ a,
                                                          float* __restrict__ b, float* __restrict__ mean_out,
-                                                         float* __restrict__ rstd_out) {
+                                                         float* __restrict__ rstd_out,
+                                                         const double* __restrict__ fin_s1,
+                                                         const double* __restrict__ fin_s2) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  const double m = fin_split_sum(g_fin_s1, S, C, c) / P;
-  const double m2 = fin_split_sum(g_fin_s2, S, C, c);
+  const double m = fin_split_sum(fin_s1, S, C, c) / P;
+  const double m2 = fin_split_sum(fin_s2, S, C, c);
   const float mu = (float)m, var = (float)(m2 / P);
   const float unb = P > 1 ? (float)(m2 / (P - 1)) : var;
   rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
@@ -1031,7 +1034,9 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
 // The same sums split over chunk ranges for few channel groups and many chunks (BN0's 64 channels x 2048 chunks
 // took 29 us in one workgroup): per split, the 16-group interleave and tree of bn_bwd_finalize_kernel into the
 // split scratch; then the splits in order (bn_bwd_fin_out_kernel).  Deterministic.
-__global__ void __launch_bounds__(1024) bn_bwd_fin_sum_kernel(const float* __restrict__ part, int T, int Ts, int C) {
+__global__ void __launch_bounds__(1024) bn_bwd_fin_sum_kernel(const float* __restrict__ part, int T, int Ts, int C,
+                                                               double* __restrict__ fin_s1,
+                                                               double* __restrict__ fin_s2) {
   __shared__ double red[2][16][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
@@ -1066,16 +1071,18 @@ __global__ void __launch_bounds__(1024) bn_bwd_fin_sum_kernel(const float* __res
     s1 += red[0][k][cl];
     s2 += red[1][k][cl];
   }
-  g_fin_s1[(size_t)sp * C + c] = s1;
-  g_fin_s2[(size_t)sp * C + c] = s2;
+  fin_s1[(size_t)sp * C + c] = s1;
+  fin_s2[(size_t)sp * C + c] = s2;
 }
 
 __global__ void __launch_bounds__(64) bn_bwd_fin_out_kernel(int S, int P, int C, float* __restrict__ c1,
                                                              float* __restrict__ c2, float* __restrict__ dgamma,
-                                                             float* __restrict__ dbeta, int accumulate) {
+                                                             float* __restrict__ dbeta, int accumulate,
+                                                             const double* __restrict__ fin_s1,
+                                                             const double* __restrict__ fin_s2) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= C) return;
-  const double s1 = fin_split_sum(g_fin_s1, S, C, c), s2 = fin_split_sum(g_fin_s2, S, C, c);
+  const double s1 = fin_split_sum(fin_s1, S, C, c), s2 = fin_split_sum(fin_s2, S, C, c);
   c1[c] = (float)(s1 / P);
   c2[c] = (float)(s2 / P);
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s2 : (float)s2;
@@ -1665,20 +1672,22 @@ DDPX_API int ddpx_f32_bn_stats(const float* y, int P, int C, int R, float* part,
 
 DDPX_API int ddpx_f32_bn_finalize(const float* part, int T, int R, int P, int C, const float* gamma, const float* beta,
                                   float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
-                                  float* a, float* b, float* mean, float* rstd, hipStream_t s) {
+                                  float* a, float* b, float* mean, float* rstd, double* ws, hipStream_t s) {
   // few channel groups and many chunks: the split merge (DDPX_F32_BN_SPLIT=0 keeps the one-kernel merge)
   static const bool split_ok = [] {
     const char* e = getenv("DDPX_F32_BN_SPLIT");
     return !(e && e[0] == '0');
   }();
-  if (split_ok && training && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
+  if (split_ok && ws && training && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
     const int S = min(kFinSplitMax, (T + 127) / 128);
     const int Ts = (T + S - 1) / S;
     const int Sr = (T + Ts - 1) / Ts;  // splits with a chunk range
-    hipLaunchKernelGGL(bn_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, R, P, C);
-    hipLaunchKernelGGL(bn_fin_m2_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, Sr, R, P, C);
+    double* s1 = ws;
+    double* s2 = ws + (size_t)kFinSplitMax * C;
+    hipLaunchKernelGGL(bn_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, R, P, C, s1);
+    hipLaunchKernelGGL(bn_fin_m2_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, Sr, R, P, C, s1, s2);
     hipLaunchKernelGGL(bn_fin_out_kernel, dim3(nblk(C, 64)), dim3(64), 0, s, Sr, P, C, gamma, beta, rmean, rvar, nbt,
-                       momentum, eps, a, b, mean, rstd);
+                       momentum, eps, a, b, mean, rstd, s1, s2);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, R, P, C, gamma, beta, rmean, rvar,
@@ -1720,18 +1729,20 @@ DDPX_API int ddpx_f32_bn_bwd_sums(const float* g, const float* y, const float* a
 }
 
 DDPX_API int ddpx_f32_bn_bwd_finalize(const float* part, int T, int P, int C, float* c1, float* c2, float* dgamma,
-                                      float* dbeta, int accumulate, hipStream_t s) {
+                                      float* dbeta, int accumulate, double* ws, hipStream_t s) {
   static const bool split_ok = [] {
     const char* e = getenv("DDPX_F32_BN_SPLIT");
     return !(e && e[0] == '0');
   }();
-  if (split_ok && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
+  if (split_ok && ws && C <= kFinSplitMaxC && T >= 1024 && nblk(C, 64) < 8) {
     const int S = min(kFinSplitMax, (T + 127) / 128);
     const int Ts = (T + S - 1) / S;
     const int Sr = (T + Ts - 1) / Ts;
-    hipLaunchKernelGGL(bn_bwd_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, C);
+    double* s1 = ws;
+    double* s2 = ws + (size_t)kFinSplitMax * C;
+    hipLaunchKernelGGL(bn_bwd_fin_sum_kernel, dim3(nblk(C, 64), Sr), dim3(1024), 0, s, part, T, Ts, C, s1, s2);
     hipLaunchKernelGGL(bn_bwd_fin_out_kernel, dim3(nblk(C, 64)), dim3(64), 0, s, Sr, P, C, c1, c2, dgamma, dbeta,
-                       accumulate);
+                       accumulate, s1, s2);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C, 64)), dim3(1024), 0, s, part, T, P, C, c1, c2, dgamma, dbeta,

@@ -27,10 +27,10 @@ for _sig in (
         ("ddpx_f32_conv_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_conv_wgrad_reduce", _I, _P, _I, _I, _I, _I, _P, _I, _P),
         ("ddpx_f32_bn_stats", _I, _P, _I, _I, _I, _P, _P),
-        ("ddpx_f32_bn_finalize", _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _I, _P, _P, _P, _P, _P),
+        ("ddpx_f32_bn_finalize", _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _I, _P, _P, _P, _P, _P, _P),
         ("ddpx_f32_bn_apply", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_bn_bwd_sums", _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
-        ("ddpx_f32_bn_bwd_finalize", _I, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P),
+        ("ddpx_f32_bn_bwd_finalize", _I, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P),
         ("ddpx_f32_bn_bwd_apply", _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_avgpool", _I, _P, _I, _I, _I, _P, _I, _P),
         ("ddpx_f32_head_fwd", _I, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P),
@@ -398,12 +398,24 @@ def bn_forward(y, N, H, W, C, bn, training, pool, stats=None, comm=None):
     nbt = bn.num_batches_tracked if (training and bn.num_batches_tracked is not None) else None
     _call("ddpx_f32_bn_finalize", part.data_ptr(), T, R, Ptot, C, bn.weight.data_ptr(), bn.bias.data_ptr(),
           bn.running_mean.data_ptr(), bn.running_var.data_ptr(), native.ptr(nbt), float(bn.momentum),
-          float(bn.eps), int(training), a.data_ptr(), b.data_ptr(), mean.data_ptr(), rstd.data_ptr())
+          float(bn.eps), int(training), a.data_ptr(), b.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+          native.ptr(_fin_ws(T, C, dev)))
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)
     out = torch.empty((N, Ho, Wo, C), dtype=torch.float32, device=dev)
     _call("ddpx_f32_bn_apply", y.data_ptr(), a.data_ptr(), b.data_ptr(), mean.data_ptr(), N, H, W, C, 1, int(pool),
           out.data_ptr())
     return out, a, b, mean, rstd
+
+
+_FIN_SPLIT_MAX, _FIN_SPLIT_MAX_C = 32, 1024  # f32_train.hip kFinSplitMax / kFinSplitMaxC
+
+
+def _fin_ws(T, C, dev):
+    """fp64 workspace [2][32][C] of the split BatchNorm merges (f32_train.hip bn_fin_*), from the caching allocator
+    on the current stream, or None where the merge does not split (the kernels then take the one-pass merge)."""
+    if T < 1024 or C > _FIN_SPLIT_MAX_C:
+        return None
+    return torch.empty(2 * _FIN_SPLIT_MAX * C, dtype=torch.float64, device=dev)
 
 
 def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumulate=False, comm=None):
@@ -422,7 +434,7 @@ def bn_backward(g, y, a, b, mean, rstd, N, H, W, C, pool, dgamma, dbeta, accumul
     cc = torch.empty(2 * C, dtype=torch.float32, device=y.device)
     c1, c2 = cc[:C], cc[C:]
     _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), native.ptr(dgamma),
-          native.ptr(dbeta), int(accumulate))
+          native.ptr(dbeta), int(accumulate), native.ptr(_fin_ws(T, C, y.device)))
     if comm is not None:
         comm.allreduce_(cc, op="sum")
         native.check(native.kernels().ddpx_scale_f32(cc.data_ptr(), 2 * C, 1.0 / comm.world_size,
@@ -574,7 +586,7 @@ def _vgg_backward(model, saved, last, dl, grad_out):
         flat.grad_done(bn.bias)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
-            if plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
+            if wino and plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
                 g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
             else:
                 g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
@@ -670,7 +682,7 @@ def bias_act_backward(g, y, N, H, W, C, pool, plan, dbias, accumulate=False):
           one.data_ptr(), N, H, W, C, int(pool), R, part.data_ptr())
     c1, c2 = plan.scratch[:C], plan.scratch[C:2 * C]
     _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), None, dbias.data_ptr(),
-          int(accumulate))
+          int(accumulate), native.ptr(_fin_ws(T, C, y.device)))
     dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
     _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
           one.data_ptr(), zero.data_ptr(), zero.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
@@ -684,14 +696,16 @@ def _deepnn_forward(model, x, targets, training):
     for bi, (conv, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
         P = N * H * W
-        if plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co):
+        # the data-gradient algorithm follows THIS forward's branch (saved below); the plan is never changed, so
+        # one forward at another input size (an eval) does not demote later 32x32 steps to the direct dgrad
+        wino = plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co)
+        if wino:
             wino_wprep(conv.weight, plan.uf[bi], plan.ud[bi])
             if bi > 0 and plan.ud[bi] is None:  # data gradient on the direct GEMM
                 conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
             y = wino_conv(x, plan.uf[bi], Co, bias=conv.bias, relu=True)
         else:
-            conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
-            plan.ud[bi] = None  # this input size takes the direct path: so does the data gradient
+            conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])  # this input size: direct forward and data gradient
             y = torch.empty((P, Co), dtype=torch.float32, device=x.device)
             gemm(IM2COL_KC, x, 0, DENSE_OC, plan.wf[bi], Co, P, Co, 9 * C, y, geom=(C, H, W, 1), bias=conv.bias,
                  relu=True)
@@ -701,7 +715,7 @@ def _deepnn_forward(model, x, targets, training):
                   plan.zeros.data_ptr(), N, H, W, Co, 1, 1, xn.data_ptr())
         else:
             xn = y.view(N, H, W, Co)
-        saved.append((x, y, (N, H, W, C, Co), pool))
+        saved.append((x, y, (N, H, W, C, Co), pool, wino))
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co
     feat = nchw_flatten(x)
@@ -731,7 +745,7 @@ def _deepnn_backward(model, saved, last, dl, grad_out):
     g = nchw_unflatten(linear_dgrad(dd0, l0.weight), *xshape)
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, pool = plan.blocks[bi]
-        x, y, (N, H, W, C, Co), _ = saved[bi]
+        x, y, (N, H, W, C, Co), _, wino = saved[bi]
         dy = None
 
         def bias_grad(o, ac):
@@ -740,7 +754,7 @@ def _deepnn_backward(model, saved, last, dl, grad_out):
         _grad_write(flat, conv.bias, bias_grad)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
-            if plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
+            if wino and plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
                 g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
             else:
                 g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)

@@ -120,15 +120,35 @@ def _barrier():
         dist.barrier()
 
 
+class PeerFailed(RuntimeError):
+    """Another rank reported a failure at an agreement point of the current trial."""
+
+
+def _all_ok(ok: bool) -> bool:
+    """Agreement point: True iff ``ok`` on every rank (MIN over the CPU group; the local value without one)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def _check():
+    """A barrier that also fails the trial on every rank when one rank has already failed it."""
+    if not _all_ok(True):
+        raise PeerFailed("another rank failed this calibration trial")
+
+
 def time_trial(step, sync, warm=3, reps=5, rounds=3):
     """Median over ``rounds`` of the mean wall time (ms) of ``reps`` back-to-back ``step()`` calls, after
-    ``warm`` untimed ones; every round is bracketed by a barrier and ``sync()`` on both sides."""
+    ``warm`` untimed ones; every round is bracketed by an agreement point (barrier) and ``sync()`` on both
+    sides."""
     for _ in range(warm):
         step()
     sync()
     out = []
     for _ in range(rounds):
-        _barrier()
+        _check()
         sync()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -139,34 +159,85 @@ def time_trial(step, sync, warm=3, reps=5, rounds=3):
     return out[len(out) // 2]
 
 
+def _err(e: BaseException) -> str:
+    return f"{type(e).__name__}: {e}"[:300]
+
+
+def run_trial(plan, make_trial, sync, warm, reps, rounds):
+    """One candidate's timing, agreed over ranks: (step ms, None) or (inf, error string) on EVERY rank.
+
+    The agreement protocol makes a failed candidate cost the job nothing but its time: a rank whose trial
+    raises goes straight to an agreement point with "failed"; the other ranks meet it at their next agreement
+    point (every barrier of :func:`time_trial` is one, and so is the end of the trial), see the failure and stop
+    this trial too.  Every rank therefore leaves the trial after the same number of CPU-group collectives.  (A
+    rank failing *inside* a training step after its peers issued that step's RCCL collectives cannot be met
+    this way; the communicator watchdog reports that case.)"""
+    err = None
+    close = None
+    t = float("inf")
+    try:
+        step, close = make_trial(plan)
+        t = time_trial(step, sync, warm=warm, reps=reps, rounds=rounds)
+    except PeerFailed as e:
+        err = _err(e)
+        peer = True
+    except Exception as e:  # noqa: BLE001 - any failure of an optional candidate is survivable
+        err = _err(e)
+        peer = False
+    else:
+        peer = False
+    if close is not None:
+        try:
+            sync()
+            close()
+        except Exception as e:  # noqa: BLE001
+            err = err or _err(e)
+            peer = False
+    try:
+        # a trial's graph capture must leave no stream capturing: the next trial (or the timed engine) would
+        # otherwise have its work recorded instead of run (profiles/r5_capture/NOTES.md)
+        assert_no_capture(f"after calibration trial {plan.get('name', '?')}")
+    except Exception as e:  # noqa: BLE001
+        err = err or _err(e)
+        peer = False
+    if not peer:  # the final agreement point (a rank that saw PeerFailed already consumed it)
+        if not _all_ok(err is None):
+            err = err or "another rank failed this calibration trial"
+    if err is not None:
+        t = float("inf")
+    return t, err
+
+
 def calibrate_by_step(plans, make_trial, sync=lambda: None, warm=3, reps=5, rounds=3, tie=0.01):
     """Pick the plan whose training step is fastest on this node.  Returns (chosen plan, {name: step ms}).
 
     ``make_trial(plan) -> (step, close)``: a fresh model + DDP + optimizer for ``plan``; ``step()`` runs one
     whole training step, ``close()`` releases the trial (reducer, graphs, memory).  Collective: every rank
     calls this with the same plans.  Ties (within ``tie``) go to the earlier candidate (torch's default caps
-    come first)."""
-    local = []
-    for p in plans:
-        step, close = make_trial(p)
-        try:
-            local.append(time_trial(step, sync, warm=warm, reps=reps, rounds=rounds))
-        finally:
-            close()
-        # a trial's graph capture must leave no stream capturing: the next trial (or the timed engine) would
-        # otherwise have its work recorded instead of run (profiles/r5_capture/NOTES.md)
-        assert_no_capture(f"after calibration trial {p.get('name', '?')}")
+    come first).  A candidate that fails on any rank is dropped on every rank (:func:`run_trial`); its error is
+    the table entry.  Raises :class:`RuntimeError` only when every candidate failed."""
     if not plans:
         raise ValueError("calibrate_by_step: no candidate plans")
+    local, errors = [], {}
+    for p in plans:
+        t, err = run_trial(p, make_trial, sync, warm, reps, rounds)
+        local.append(t)
+        if err is not None:
+            errors[p["name"]] = err
     ms = _max_over_ranks(local)
     best = min(ms)
+    if best == float("inf"):
+        raise RuntimeError("calibrate_by_step: every candidate failed: " + "; ".join(
+            f"{k}: {v}" for k, v in errors.items()))
     pick = min(i for i, v in enumerate(ms) if v <= best * (1.0 + tie))
     obj = [pick]
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.broadcast_object_list(obj, src=0)
     chosen = dict(plans[obj[0]])
     chosen.pop("colls", None)
-    return chosen, {p["name"]: round(v, 4) for p, v in zip(plans, ms)}
+    table = {p["name"]: (round(v, 4) if v != float("inf") else {"error": errors.get(p["name"], "failed")})
+             for p, v in zip(plans, ms)}
+    return chosen, table
 
 
 def isolated_collective_ms(comm, plans, device, reps=3):

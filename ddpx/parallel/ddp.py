@@ -266,6 +266,8 @@ class _NativeReducer:
 
 
 class DistributedDataParallel(nn.Module):
+    _side_seq = 0  # names of registered optimizer side streams
+
     def __init__(self, module: nn.Module, device_ids=None, comm: Comm | None = None,
                  bucket_cap_mb: float = DEFAULT_BUCKET_CAP_MB, first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB,
                  broadcast_buffers: bool = True, overlap_optimizer: bool = False, verify: bool = True,
@@ -406,8 +408,10 @@ class DistributedDataParallel(nn.Module):
                 and isinstance(comm, RcclComm) and dev.type == "cuda"):
             self._opt_stream = torch.cuda.Stream(dev)
             from ..runtime.graphs import register_side_stream
-            self._side_name = f"DDP optimizer stream #{id(self)}"
-            register_side_stream(self._opt_stream, self._side_name)
+            DistributedDataParallel._side_seq += 1
+            self._side_name = f"DDP optimizer stream #{DistributedDataParallel._side_seq}"
+            # by (owner, attribute), held weakly: a dropped wrapper leaves no stale stream in the registry
+            register_side_stream(self, self._side_name, attr="_opt_stream")
         late = getattr(self.flat, "late_read", None)
         # late-read parameters per bucket; unknown read pattern (late = None): every bucket waits for backward's end
         self._late = [(sum(1 for i in self.bucket_params[b] if id(self.flat.params[i]) in late) if late is not None

@@ -270,7 +270,7 @@ def make_ddp(args, model, optimizer, comm):
                                   shard_optimizer=args.shard_optimizer, chunk_mb=args.chunk_mb,
                                   defer_gather=args.defer_gather,
                                   comm_side_optimizer=args.comm_side_optimizer,
-                                  side_stream_optimizer=bool(getattr(args, "side_optimizer", 1)))
+                                  side_stream_optimizer=bool(getattr(args, "side_optimizer", 0)))
     if args.overlap_optimizer or args.shard_optimizer:
         net.attach_optimizer(optimizer)
     return net

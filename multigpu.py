@@ -51,8 +51,13 @@ if __name__ == "__main__":
             # initialising HIP here (environment / KFD topology, ddpx.utils.devices): the ranks are fork+exec'd,
             # which must not happen from a process that touched the GPU
             from ddpx.utils.devices import visible_gpu_count
-            n = 0 if args.device == "cpu" else visible_gpu_count()
-            world_size = n if n > 0 else 2
+            if args.device == "cpu":
+                world_size = 2  # CPU/gloo rehearsal: two processes unless --nprocs says otherwise
+            else:
+                world_size = visible_gpu_count()
+                if world_size < 1:
+                    raise SystemExit("multigpu.py: no GPU is visible (the reference's torch.cuda.device_count() "
+                                     "would be 0); pass --device cpu for the gloo rehearsal or --nprocs N")
         if args.device != "cpu":
             from ddpx.utils.devices import assert_hip_uninitialised
             assert_hip_uninitialised("multigpu.py: mp.spawn")

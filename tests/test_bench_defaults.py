@@ -96,16 +96,23 @@ def test_self_launch_command_needs_no_launcher():
     assert "--master-addr=127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "5"]
 
 
-def _bench(argv, timeout=600):
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+def _bench(argv, timeout=600, env_extra=None, stock_tail=False):
+    env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], cwd=ROOT, env=env,
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stdout[-3000:]
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    # the driver contract: exactly ONE JSON line on stdout
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-3000:]
-    return json.loads(lines[0])
+    rec = json.loads(lines[0])
+    if not stock_tail:
+        return rec
+    tails = [ln[len("STOCK "):] for ln in r.stderr.splitlines() if ln.startswith("STOCK ")]
+    assert len(tails) == 1, r.stderr[-3000:]
+    # the headline line is printed before the stock comparison starts
+    return rec, json.loads(tails[0])
 
 
 SMALL = ["--steps", "3", "--warmup", "1", "--batch_size", "64", "--hidden", "256", "--train_size", "1024"]
@@ -130,7 +137,42 @@ def test_bench_cpu_two_ranks_self_launched():
     assert c["bucket_plan"] == "calibrated" and c["calibration"]["chosen"].startswith("allreduce")
     assert all(v > 0 for v in c["calibration"]["step_ms"].values()) and len(c["calibration"]["step_ms"]) >= 1
     assert "step" in c["calibration"]["objective"]
-    # the stock recipe (torch DDP over gloo here, RCCL on the GPU) timed in the same job
-    st = c["stock_same_run"]
-    assert st["ms_per_step"] > 0 and "torch DDP" in st["recipe"] and c["vs_stock_same_run"] > 0
     assert c["graph"] is False and c["graph_error"] is None
+
+
+def test_bench_cpu_two_ranks_stock_after_the_line():
+    """N > 1: the stock recipe (torch DDP over gloo here, over a second RCCL communicator on the GPU) runs only
+    after the ddpx line is printed; its result is a ``STOCK`` line on stderr."""
+    rec, tail = _bench(["--gpus", "2", "--device", "cpu", *SMALL], stock_tail=True)
+    assert rec["config"]["stock_same_run"]["placement"].startswith("after this line")
+    assert rec["config"]["vs_stock_same_run"] is None
+    st = tail["stock_same_run"]
+    assert st["ms_per_step"] > 0 and "torch DDP" in st["recipe"] and tail["vs_stock_same_run"] > 0
+    assert tail["n_gpus"] == 2
+
+
+def test_bench_cpu_two_ranks_survives_optional_failures():
+    """a calibration candidate that fails is dropped on every rank, and a stock recipe failing
+    on ONE rank becomes an agreed ``error`` — the job still exits 0 with its one ddpx line.  (The candidate fails
+    on every rank, in its first training step: a failure on one rank only, after its peers issued that step's
+    collectives, cannot be met by an agreement point — the communicator watchdog owns that case.)"""
+    argv = ["--gpus", "2", "--device", "cpu", "--steps", "3", "--warmup", "1", "--batch_size", "64", "--hidden",
+            "1024", "--train_size", "1024"]
+    rec, tail = _bench(argv, stock_tail=True,
+                       env_extra={"DDPX_BENCH_INJECT": "calib:allreduce:1/25MB,stock@rank1"})
+    cal = rec["config"]["calibration"]
+    assert cal["dropped"] == ["allreduce:1/25MB"], cal
+    assert "InjectedFault" in cal["step_ms"]["allreduce:1/25MB"]["error"] or \
+        "another rank" in cal["step_ms"]["allreduce:1/25MB"]["error"]
+    assert cal["chosen"] != "allreduce:1/25MB" and cal["step_ms"][cal["chosen"]] > 0
+    assert rec["config"]["replicas_consistent"] is True and rec["value"] > 0
+    assert "error" in tail["stock_same_run"] and tail["vs_stock_same_run"] is None
+
+
+def test_bench_cpu_every_candidate_failing_falls_back_to_torch_caps():
+    rec = _bench(["--gpus", "2", "--device", "cpu", *SMALL, "--stock_ref", "0"],
+                 env_extra={"DDPX_BENCH_INJECT": "calib"})
+    c = rec["config"]
+    assert c["calibration"]["chosen"] is None and "every candidate failed" in c["calibration"]["error"]
+    assert c["bucket_cap_mb"] == 25.0 and c["first_bucket_mb"] == 1.0 and c["sharded_optimizer"] is False
+    assert c["replicas_consistent"] is True and rec["value"] > 0

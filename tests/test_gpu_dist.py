@@ -205,3 +205,74 @@ def test_capture_aborted_after_rccl_collectives_then_eager(gpu, pg, shard):
         assert torch.equal(p, q)
     da.close()
     comm.close()
+
+
+@pytest.mark.parametrize("kind", ["mlp_bf16", "mlp_fp32", "deepnn_bf16"])
+def test_side_stream_optimizer_matches_in_stream(gpu, pg, kind):
+    """Replicated plan with per-bucket optimizer overlap: each bucket's SGD on a side stream behind its
+    all-reduce and the release of its weights (``side_stream_optimizer``) vs on the compute stream.  The side
+    update may rewrite W_l (and its bf16 compute copy) while backward is still running, so a missed release
+    (``flat.release`` / ``late_read_params``) or end-of-backward fallback would corrupt the data gradients that
+    read W_l.  Master weights + momentum must be bitwise equal after eager AND graph-captured steps, for the bf16
+    MLP (declares late reads), the fp32 MLP, and DeepNN (no late-read declaration: every bucket waits for the
+    end of backward)."""
+    import ddpx
+    from ddpx.models import build_model
+    from ddpx.optim.sgd import SGD
+    from ddpx.parallel.comm import RcclComm
+    from ddpx.parallel.ddp import DistributedDataParallel
+    from ddpx.runtime.flat_params import flat_of
+    from ddpx.runtime.graphs import CapturedStep
+    name, dt = kind.split("_")
+    comm = RcclComm(gpu)
+    runs = []
+    for side in (False, True):
+        torch.manual_seed(3)
+        m = build_model(name, hidden=512, layers=3, dtype=dt, device=gpu)
+        ddpx.prepare_model(m, gpu)
+        d = DistributedDataParallel(m, comm=comm, bucket_cap_mb=0.5, first_bucket_mb=0.125, reduce_single=True,
+                                    overlap_optimizer=True, side_stream_optimizer=side)
+        assert (d.update_side_stream() is not None) == side
+        assert len(d.bucket_ranges) >= 2
+        o = SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True)
+        d.attach_optimizer(o)
+        g = torch.Generator(device="cpu").manual_seed(4)
+        if name == "mlp":
+            xs = [torch.rand(128, 3072, generator=g).to(gpu) for _ in range(6)]
+            xs = [x.to(torch.bfloat16) if dt == "bf16" else x for x in xs]
+        else:
+            lay = m.input_layout(gpu) if hasattr(m, "input_layout") else "nchw_f32"
+            assert lay.startswith("nhwc8") or lay.startswith("nchw"), lay
+            xs = [torch.rand(64, 3, 32, 32, generator=g) for _ in range(6)]
+            if lay.startswith("nhwc8"):
+                xs = [torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).contiguous().to(torch.bfloat16)
+                      for x in xs]
+            xs = [x.to(gpu) for x in xs]
+        ts = [torch.randint(0, 10, (xs[0].shape[0],), generator=g).to(gpu) for _ in range(6)]
+
+        def body(x, y):
+            o.zero_grad()
+            loss, _ = d.forward_loss(x, y) if hasattr(m, "forward_loss") else (
+                torch.nn.functional.cross_entropy(d(x), y), None)
+            loss.backward()
+            o.step()
+            return loss
+
+        o.sync_lr()
+        losses = [body(xs[i], ts[i]).item() for i in range(3)]  # eager
+        cap = CapturedStep(body, xs[3], ts[3])
+        for i in range(3, 6):
+            cap.load(xs[i], ts[i])
+            losses.append(cap().item())
+        d.consolidate()
+        torch.cuda.synchronize()
+        f = flat_of(m)
+        runs.append((losses, f.master.detach().clone(),
+                     {k: v.detach().clone() for k, v in f.state_tensors.items()}))
+        cap = None
+        d.close()
+    (la, ma, sa), (lb, mb, sb) = runs
+    assert la == lb, (la, lb)
+    assert torch.equal(ma, mb)
+    assert sa.keys() == sb.keys() and all(torch.equal(sa[k], sb[k]) for k in sa)
+    comm.close()

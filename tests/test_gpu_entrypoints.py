@@ -103,8 +103,33 @@ def test_bench_n_gt_1_paths_at_world_size_1(gpu, tmp_path):
     assert any(k.startswith("zero1") for k in table) and any(k.startswith("allreduce") for k in table), table
     assert all(v > 0 for v in table.values()) and c["calibration"]["chosen"] in table
     assert c["graph"] is True and c["graph_error"] is None
-    assert c["stock_same_run"] is not None and "torch DDP" in c["stock_same_run"]["recipe"], c["stock_same_run"]
+    # the DDP job's placement: the stock torch-DDP run starts only after the ddpx line is out
+    assert c["stock_same_run"]["placement"].startswith("after this line")
+    assert out.index('{"metric"') < out.index("STOCK {")
+    tail = json.loads(out.split("STOCK ", 1)[1].splitlines()[0])
+    assert "torch DDP" in tail["stock_same_run"]["recipe"] and tail["vs_stock_same_run"] > 0, tail
     assert c["replicas_consistent"] is True and c["ddp"] is True
+
+
+def test_bench_ddp_job_survives_optional_failures(gpu, tmp_path):
+    """VERDICT r5 item 1 on the GPU (the N > 1 layout at world size 1): a failure injected into the stock
+    torch-DDP run (after its NCCL group and DDP model exist) and into every ZeRO-1 calibration trial (first
+    training step, real RcclComm, graph capture) — rc 0, the ddpx line, the ZeRO-1 candidates dropped, the stock
+    error agreed and reported."""
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3", "--ddp_single",
+                "--stock_ddp", "1", "--stock_steps", "5", "--train_size", "8192"],
+               tmp_path, extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()),
+                                    "DDPX_COMM_SKIP_IDENTITY": "0", "DDPX_BENCH_INJECT": "calib:zero1,stock_run"})
+    lines = [ln for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, out[-3000:]
+    c = json.loads(lines[0])["config"]
+    cal = c["calibration"]
+    assert cal["dropped"] and all(k.startswith("zero1") for k in cal["dropped"]), cal
+    assert cal["chosen"].startswith("allreduce") and c["sharded_optimizer"] is False
+    assert all(isinstance(v, dict) == k.startswith("zero1") for k, v in cal["step_ms"].items()), cal
+    assert c["graph"] is True and c["replicas_consistent"] is True
+    tail = json.loads(out.split("STOCK ", 1)[1].splitlines()[0])
+    assert "InjectedFault" in tail["stock_same_run"]["error"] and tail["vs_stock_same_run"] is None
 
 
 def test_bench_contract_one_gpu(gpu, tmp_path):
