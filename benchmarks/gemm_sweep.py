@@ -38,7 +38,11 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--inp", type=int, default=3072)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7", help="comma-separated tile configs")
+    ap.add_argument("--cases", default="", help="comma-separated subset of fwd1,fwd2,dgrad2,wgrad1,wgrad2")
+    ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",") if c.strip()]
     dev = torch.device("cuda", 0)
     B, H, I = a.batch, a.hidden, a.inp
 
@@ -50,6 +54,7 @@ def main():
     b = torch.randn(H, device=dev)
     dy = rnd(B, H)
     dw1, dw2 = torch.empty(H, I, device=dev), torch.empty(H, H, device=dev)
+    dyT, h1T = dy.t().contiguous(), h1.t().contiguous()
     cases = {
         "fwd1": (2 * B * H * I, lambda t: G.gemm_raw(x, w1, torch.empty(B, H, dtype=torch.bfloat16, device=dev),
                  M=B, N=H, K=I, lda=I, ldb=I, ldc=H, a_kcontig=True, b_kcontig=True, epi=G.EPI_BIAS_RELU_BF16,
@@ -64,14 +69,24 @@ def main():
                    a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t), lambda: dy.t() @ x),
         "wgrad2": (2 * B * H * H, lambda t: G.gemm_raw(dy, h1, dw2, M=H, N=H, K=B, lda=H, ldb=H, ldc=H,
                    a_kcontig=False, b_kcontig=False, epi=G.EPI_F32, tile=t), lambda: dy.t() @ h1),
+        # the same weight gradient from K-contiguous (transposed) copies of dY and X: the forward GEMMs' layout
+        "wgrad2kk": (2 * B * H * H, lambda t: G.gemm_raw(dyT, h1T, dw2, M=H, N=H, K=B, lda=B, ldb=B, ldc=H,
+                     a_kcontig=True, b_kcontig=True, epi=G.EPI_F32, tile=t), lambda: dy.t() @ h1),
     }
     res = {}
+    want = [c for c in a.cases.split(",") if c] or list(cases)
     for name, (flop, ours, ref) in cases.items():
+        if name not in want:
+            continue
         row = {}
-        t = timeit(ref)
+        t = timeit(ref, iters=a.iters)
         row["hipblaslt"] = round(t, 2)
-        for cfg in range(8):
-            row[f"pipe{cfg}"] = round(timeit(lambda: ours(cfg)), 2)
+        r = ref().float()
+        for cfg in cfgs:
+            row[f"pipe{cfg}"] = round(timeit(lambda: ours(cfg), iters=a.iters), 2)
+            err = ((ours(cfg).float() - r).norm() / r.norm()).item()
+            if err > 2e-2:
+                row[f"pipe{cfg}_ERR"] = err
         best = min((v, k) for k, v in row.items() if k != "hipblaslt")
         row["best"] = best[1]
         row["best_tflops"] = round(flop / best[0] / 1e6, 1)

@@ -878,7 +878,10 @@ gemm_pipe_kernel(Params p) {
     const int ahead = min(STAGES - 2, nk - 1 - t);
     // stages 1..STAGES-1 were issued before the prefetch (t = 0): its PFW ops are younger than them
     const bool pf_young = SGDPF && t >= 1 && t <= STAGES - 1;
-    if (ahead >= 2) { if (pf_young) wait_vmcnt<2 * LPW + PFW>(); else wait_vmcnt<2 * LPW>(); }
+    // deep rings (configs 24 / 25: 6 stages) keep up to STAGES - 2 younger stages in flight past the barrier
+    if (STAGES >= 6 && !SGDPF && ahead >= 4) wait_vmcnt<(STAGES >= 6 ? 4 : 0) * LPW>();
+    else if (STAGES >= 5 && !SGDPF && ahead >= 3) wait_vmcnt<(STAGES >= 5 ? 3 : 0) * LPW>();
+    else if (ahead >= 2) { if (pf_young) wait_vmcnt<2 * LPW + PFW>(); else wait_vmcnt<2 * LPW>(); }
     else if (ahead == 1) { if (pf_young) wait_vmcnt<LPW + PFW>(); else wait_vmcnt<LPW>(); }
     else { if (pf_young) wait_vmcnt<PFW>(); else wait_vmcnt<0>(); }
     __builtin_amdgcn_s_barrier();
@@ -1113,9 +1116,11 @@ static hipError_t launch(const Params& p, int splits, hipStream_t s) {
 }
 
 // cfg 16 - 20: warp-specialised rings (LW = 4 loader waves) for the M = 512-row products
-constexpr int kNumCfgs = 24;
+constexpr int kNumCfgs = 26;
 // 8-wave configs whose register budget has no room for the in-launch column-sum finish
-static inline bool eight_wave(int cfg) { return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15; }
+static inline bool eight_wave(int cfg) {
+  return cfg == 8 || cfg == 13 || cfg == 14 || cfg == 15 || cfg == 22 || cfg == 25;
+}
 
 // Row-parts the epilogue stages the tile in (the data gradient's BatchNorm backward sums come out per part; the
 // forward statistics are merged to one row per tile).
@@ -1125,7 +1130,7 @@ static inline void tile_of(int cfg, int* bm, int* bn) {
   static const int t[kNumCfgs][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64},  {128, 128}, {64, 128}, {128, 64},
                                      {64, 64},   {256, 128}, {64, 64},  {64, 128}, {128, 64}, {64, 64},  {256, 256},
                                      {128, 128}, {128, 128}, {256, 128}, {128, 128}, {64, 128}, {128, 64},
-                                     {64, 64},   {128, 128}, {128, 128}, {256, 64}};
+                                     {64, 64},   {128, 128}, {128, 128}, {256, 64}, {128, 64}, {128, 64}};
   const int c = (cfg >= 0 && cfg < kNumCfgs) ? cfg : 7;
   *bm = t[c][0];
   *bn = t[c][1];
@@ -1148,6 +1153,11 @@ static hipError_t dispatch(const Params& p, int cfg, int splits, hipStream_t s) 
     // narrow (N = 64) products: 256x64, 2-deep (80 KiB, 2 per CU), 4 waves of 128x32 (8 waves would need 128
     // VGPRs each and spilled)
     case 23: return launch<256, 64, 2, AK, BKc, AMODE, BMODE, 4>(p, splits, s);
+    // one 128x64 tile per CU at M = 512 (256 tiles: 25 % fewer operand bytes per CU than two 64x64 tiles) on a
+    // barrier-coupled 6 x 24 KiB ring: 5 K-steps (120 KiB) of LDS-DMA in flight per CU, against config 12's 64 KiB
+    // (PMC, profiles/r6_gemm: config 12's waves wait 53 % of their cycles with the TA path 53 % busy)
+    case 24: return launch<128, 64, 6, AK, BKc, AMODE, BMODE, 4>(p, splits, s);  // 4 waves, 64x32 each
+    case 25: return launch<128, 64, 6, AK, BKc, AMODE, BMODE, 8>(p, splits, s);  // 8 waves, 32x32 each
     case 16:  // warp-specialised (plain operands only)
       if constexpr (AMODE == MODE_PLAIN && BMODE == MODE_PLAIN)
         return launch<256, 128, 3, AK, BKc, AMODE, BMODE, 8, 1, false, false, 4>(p, splits, s);

@@ -39,18 +39,27 @@ constexpr int VPT = BM * BN / 4 / 256;  // f32x4 vectors per stream thread per t
 //   SB (single hand-off buffer): the stream waves read each gradient vector one K-step ahead, so they never touch
 //             the buffer in the K-step the math waves refill it: one fp32 tile buffer instead of two, which leaves
 //             room for a 4-stage ring with padded rows (DDPX_WSGD_SB=1, 4 stream waves).
+// Diagnostics (ddpx_gemm_set_stamps, benchmarks/pair_stamps.py): with p0.stamp set, lane 0 of wave 0 (math role)
+// and of wave 4 (stream role) write s_memrealtime (10 ns ticks) at kernel start (slot 0), on ARRIVAL at each of the
+// role's s_barriers (slots 1..), and at kernel end (last slot): stamp[(block * 2 + role) * kStampSlots + slot].  A
+// barrier's departure is the later of the two roles' arrivals, so the per-barrier wait of each role shows which
+// side sets the pace.  Off (a null pointer) it costs a scalar test per barrier.
+constexpr int kStampSlots = 256;
+
 template <int STAGES, int XTRA = 0, bool SB = false>
 struct Cfg {
   static constexpr int ALD = (STAGES >= 4 && !SB) ? BN : BN + 4;
   static constexpr int ACC_BYTES = BM * ALD * 4;
-  static constexpr int LDS_BYTES = STAGES * SLOT + (SB ? 1 : 2) * ACC_BYTES + (XTRA >= 2 ? SLOT : 0);
+  static constexpr int LDS_BYTES = STAGES * SLOT + (SB ? 1 : 2) * ACC_BYTES + (XTRA == 2 ? SLOT : 0);
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 // Two GEMMs may share one launch (p0's tiles, then p1's: the toy MLP's fc1 and fc0 weight gradients are
 // independent once fc1's data gradient ran): one fill and one drain iteration instead of two, one launch
 // boundary fewer.  Single GEMM: p1 = p0 and nt1 = 0.  Both must have the same K, lr, momentum, wd, alpha.
-// XTRA (measurement only, DDPX_WSGD_XTRA): 1 = every K-step runs its MFMAs twice (the second set into a
+// XTRA (measurement only, DDPX_WSGD_XTRA): 3 = math only (the stream waves keep the barrier sequence but load,
+// update and store nothing), 4 = stream only (the math waves issue no DMA and no MFMA: zero gradients);
+// 1 = every K-step runs its MFMAs twice (the second set into a
 // dead accumulator kept live), 2 = also a second operand stage of LDS-DMA per K-step into a dummy ring — the
 // math and L2->LDS load a fused data-gradient GEMM would add beside the weight-gradient tiles.
 template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false>
@@ -90,6 +99,17 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     return sel;
   };
   const pipe::Params& p = p0;  // K, alpha, lr, momentum, wd: shared by both GEMMs
+  long long* const stp = (p0.stamp && (tid == 0 || tid == 256))
+                             ? p0.stamp + ((size_t)blockIdx.x * 2 + (wave < 4 ? 0 : 1)) * kStampSlots
+                             : nullptr;
+  int nstamp = 1;
+  auto mark = [&]() {  // arrival at the role's next barrier
+    if (stp) {
+      stp[nstamp < kStampSlots - 1 ? nstamp : kStampSlots - 2] = (long long)__builtin_amdgcn_s_memrealtime();
+      ++nstamp;
+    }
+  };
+  if (stp) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
 
   if (wave < 4) {
     // ------------------------------------------------------------------ math waves
@@ -104,6 +124,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     // nk = 8 K-steps: a per-tile refill cost ~2 of every 10 K-steps of L2 latency).
     const int G = nt * nk;
     auto issue = [&](int g) {
+      if constexpr (XTRA == 4) return;  // measurement: stream only
       int m0, n0;
       const int sel = tile_origin(g / nk, m0, n0);
       const int kt = g % nk;
@@ -114,7 +135,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, kt * 64, p.K, wave, lane);
       pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, kt * 64, p.K, wave,
                                                        lane);
-      if constexpr (XTRA >= 2) {  // dummy second stage (same operands, other k rows) into the extra ring
+      if constexpr (XTRA == 2) {  // dummy second stage (same operands, other k rows) into the extra ring
         char* x = smem + STAGES * SLOT + 2 * ACC_BYTES;  // one dummy slot (its contents are never used)
         const int kx = ((kt + 3) % (p.K / 64)) * 64;
         pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, x, p.conv, lda, m0, Mg, kx, p.K, wave, lane);
@@ -126,7 +147,10 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
       if (s < G) issue(s);
     for (int i = 0; i <= nt; ++i) {
       if (i == nt) {  // drain iteration: the stream waves finish the last tile
-        for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < nk; ++t) {
+          mark();
+          __builtin_amdgcn_s_barrier();
+        }
       } else {
         f32x4 acc[FM][FN], acc2[FM][FN];
 #pragma unroll
@@ -136,19 +160,20 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
         for (int t = 0; t < nk; ++t) {
           const int g = i * nk + t;
           const int ahead = min(STAGES - 2, G - 1 - g);
-          constexpr int LW = XTRA >= 2 ? 2 * LPW : LPW;
+          constexpr int LW = XTRA == 2 ? 2 * LPW : LPW;
           // stage g landed: everything but the (up to STAGES - 2) younger stages' DMAs
           if (STAGES >= 5 && ahead >= 3) pipe::wait_vmcnt<3 * LW>();
           else if (STAGES >= 4 && ahead >= 2) pipe::wait_vmcnt<2 * LW>();
           else if (ahead >= 1) pipe::wait_vmcnt<LW>();
           else pipe::wait_vmcnt<0>();
+          mark();
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
           if (g + STAGES - 1 < G) issue(g + STAGES - 1);
           const char* sa = smem + (g % STAGES) * SLOT;
           const char* sb = sa + A_SUB;
 #pragma unroll
-          for (int kk = 0; kk < 64; kk += 32) {
+          for (int kk = 0; kk < (XTRA == 4 ? 0 : 64); kk += 32) {
             bf16x8 af[FM], bfr[FN];
             pipe::load_frags<BM, false, FM, BN, false, FN>(sa, wm * 32, sb, wn * 64, kk, lane, af, bfr);
 #pragma unroll
@@ -156,8 +181,8 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
 #pragma unroll
               for (int b = 0; b < FN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
-            if constexpr (XTRA >= 1) {
-              const char* xa = XTRA >= 2 ? smem + STAGES * SLOT + 2 * ACC_BYTES : sa;
+            if constexpr (XTRA == 1 || XTRA == 2) {
+              const char* xa = XTRA == 2 ? smem + STAGES * SLOT + 2 * ACC_BYTES : sa;
               bf16x8 af2[FM], bf2[FN];
               pipe::load_frags<BM, false, FM, BN, false, FN>(xa, wm * 32, xa + A_SUB, wn * 64, kk, lane, af2, bf2);
 #pragma unroll
@@ -168,7 +193,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
             }
           }
         }
-        if constexpr (XTRA >= 1) {
+        if constexpr (XTRA == 1 || XTRA == 2) {
 #pragma unroll
           for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -185,8 +210,10 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
             for (int r = 0; r < 4; ++r) T[(mr + a * 16 + r) * ALD + nc + b * 16] = acc[a][b][r] * p.alpha;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mark();
       __builtin_amdgcn_s_barrier();  // hand-off: tile i's buffer complete, tile i-1's buffer released
     }
+    if (stp) stp[kStampSlots - 1] = (long long)__builtin_amdgcn_s_memrealtime();
   } else {
     // ---------------------------------------------------------------- stream waves
     // Vector v of tile i-1 (row row0 + 8 v, columns col..col+3 of the tile) is updated in K-step v of
@@ -273,8 +300,13 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
 #pragma unroll
-    for (int v = 0; v < DIST; ++v) load_vec(0, v, rp[v], rm[v]);
-    for (int t = 0; t < nk; ++t) __builtin_amdgcn_s_barrier();
+    for (int v = 0; v < DIST; ++v)
+      if constexpr (XTRA != 3) load_vec(0, v, rp[v], rm[v]);
+    for (int t = 0; t < nk; ++t) {
+      mark();
+      __builtin_amdgcn_s_barrier();
+    }
+    mark();
     __builtin_amdgcn_s_barrier();
     // trip r = DIST K-steps: iteration i = 1 + r / TPI updates tile i - 1, vectors (r % TPI) * DIST .. + DIST - 1;
     // the first trip is peeled so the loop is entered with the same memory operations in flight as on its back
@@ -287,15 +319,20 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
 #pragma unroll
       for (int u = 0; u < DIST; ++u) {
         // sched_barrier: keep each update's register work (which waits for its ring slot) inside its K-step
+        mark();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        update_vec(i - 1, t + u, T, rp[u], rm[u]);
+        if constexpr (XTRA != 3) update_vec(i - 1, t + u, T, rp[u], rm[u]);  // (3: measurement, math only)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int k = 1; k < KPU; ++k) __builtin_amdgcn_s_barrier();
+        for (int k = 1; k < KPU; ++k) {
+          mark();
+          __builtin_amdgcn_s_barrier();
+        }
       }
       if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mark();
         __builtin_amdgcn_s_barrier();
       }
     };
@@ -335,6 +372,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
 #pragma unroll 1
       for (int r = 1; r < TPI * nt; ++r) trip(r);
     }
+    if (stp) stp[kStampSlots - 1] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -399,6 +437,12 @@ template <int STAGES, bool FP8>
 static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1,
                                int nsw) {
   const bool no = n_order();
+  if constexpr (!FP8 && STAGES == 3) {
+    // measurement variants: DDPX_WSGD_XTRA=3 math only, 4 stream only (benchmarks/pair_stamps.py)
+    const int x = xtra();
+    if (x == 3 && nsw == 4) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 3>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
+    if (x == 4 && nsw == 4) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 4>), grid, dim3(512), 0, s, p0, p1, nt1); return; }
+  }
   if constexpr (!FP8 && STAGES == 2) {
     // measurement variants (DDPX_WSGD_XTRA=1|2, 2-stage ring so the dummy ring fits the LDS)
     const int x = xtra();

@@ -852,6 +852,26 @@ DDPX_API int ddpx_bn_bwd_apply(const void* gout, const void* y, const float* a, 
   return (int)hipGetLastError();
 }
 
+DDPX_API int ddpx_bias_act_bwd_sgd(const void* gout, const void* y, const float* bias, const float* ones,
+                                   const float* zeros, int N, int H, int W, int C, int pool, int relu, float* part,
+                                   float* c1, float* c2, void* dbias, int out_bf16, int accumulate, void* dy,
+                                   float* sb_p, float* sb_buf, void* sb_shadow, const float* lr, float mom, float wd,
+                                   hipStream_t s) {
+  // sb_p (optional): the bias gradient is applied as its fused SGD update in the merge (no gradient stored)
+  if (C % 8 || C > 512 || (pool && (H % 2 || W % 2)) || (sb_p && !lr) || (!sb_p && !dbias)) return -1;
+  const int B = ddpx_bn_bwd_blocks(N, H, W, C);
+  hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
+  launch_bwd_finalize(part, B, C, N * H * W, c1, c2, nullptr, dbias, out_bf16, accumulate,
+                      SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
+                      SgdArgs{sb_p, sb_buf, (unsigned short*)sb_shadow, lr, mom, wd}, s);
+  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
+  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
+                     (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,
+                     (unsigned short*)dy);
+  return (int)hipGetLastError();
+}
+
 DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bias, const float* ones,
                                const float* zeros, int N, int H, int W, int C, int pool, int relu, float* part,
                                float* c1, float* c2, void* dbias, int out_bf16, int accumulate, void* dy,

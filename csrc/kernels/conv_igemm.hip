@@ -263,6 +263,109 @@ DDPX_API int ddpx_conv_fwd(const void* x, const void* wf, void* y, float* stats,
   return (int)dispatch_conv_fwd(p, cfg, s);
 }
 
+// DeepNN's conv blocks (no BatchNorm, /root/reference/singlegpu.py:18-44): act[P][Co] = relu(conv(x, W) + bias) in
+// the GEMM epilogue (EPI_BIAS_RELU_BF16), so no separate bias/ReLU pass reads the conv output back.
+DDPX_API int ddpx_conv_fwd_act(const void* x, const void* wf, void* act, const float* bias, int N, int H, int W, int C,
+                               int Co, int tile_cfg, hipStream_t s) {
+  if (C % 8 || Co % 8 || !bias) return -1;
+  if (!chk16(x) || !chk16(wf) || !chk16(act)) return -3;
+  const int P = N * H * W, K = 9 * C;
+  Params p{};
+  p.A = (const unsigned short*)x;
+  p.B = (const unsigned short*)wf;
+  p.C = act;
+  p.bias = bias;
+  p.M = P; p.N = Co; p.K = K;
+  p.lda = C; p.ldb = K; p.ldc = Co;
+  p.epi = EPI_BIAS_RELU_BF16;
+  p.alpha = 1.f;
+  p.im_slow = im_slow();
+  const size_t ab = (size_t)P * C * 2, bb = (size_t)Co * K * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = make_geom(H, W, C, P);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_fwd(P, C, Co);
+  return (int)dispatch_conv_fwd(p, cfg, s);
+}
+
+// Row tiles of the data-gradient GEMM (rows of ddpx_conv_dgrad_act's column-sum partials).
+DDPX_API int ddpx_conv_dgrad_tiles_m(int N, int H, int W, int C, int Co, int tile_cfg) {
+  const int P = N * H * W;
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
+  int bm, bn;
+  tile_of(cfg, &bm, &bn);
+  return (P + bm - 1) / bm;
+}
+
+// Data gradient straight into the pre-activation gradient of the (un-pooled) ReLU block below:
+// dz[P][C] = dgrad(dy, W) * (act[P][C] > 0) (EPI_RELUMASK_BF16, act = relu(conv + bias) of that block), plus
+// colsum[T][C] = per-row-tile column sums of the stored dz (its bias gradient, finished in fixed order by
+// ddpx_colsum_finish).  One launch replaces the plain data gradient and a reduce + apply pass over dz.
+DDPX_API int ddpx_conv_dgrad_act(const void* dy, const void* wd, void* dz, int N, int H, int W, int C, int Co,
+                                 int tile_cfg, const void* act, float* colsum, hipStream_t s) {
+  if (C % 8 || Co % 8 || !act || !colsum) return -1;
+  if (!chk16(dy) || !chk16(wd) || !chk16(dz) || !chk16(act)) return -3;
+  const int P = N * H * W, K = 9 * Co;
+  Params p{};
+  p.A = (const unsigned short*)dy;
+  p.B = (const unsigned short*)wd;
+  p.C = dz;
+  p.aux = (const unsigned short*)act;
+  p.ldaux = C;
+  p.colsum = colsum;
+  p.M = P; p.N = C; p.K = K;
+  p.lda = Co; p.ldb = C; p.ldc = C;
+  p.epi = EPI_RELUMASK_BF16;
+  p.alpha = 1.f;
+  p.im_slow = im_slow();
+  const size_t ab = (size_t)P * Co * 2, bb = (size_t)K * C * 2;
+  if (ab >= 0x80000000ull || bb >= 0x80000000ull) return -4;
+  p.a_bytes = (unsigned)ab; p.b_bytes = (unsigned)bb;
+  p.conv = make_geom(H, W, Co, P);
+  const int cfg = tile_cfg >= 0 ? tile_cfg : conv::pick_dgrad(P, C, Co);
+  return (int)dispatch_conv_dgrad(p, cfg, s);
+}
+
+namespace ddpx {
+namespace conv {
+// out[c] (=|+=) sum_t part[t][c] in t order (8 loads in flight), or the fused SGD of the parameter out points at
+__global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restrict__ part, int T, int C,
+                                                            void* __restrict__ out, int out_bf16, int accumulate,
+                                                            SgdArgs sgd) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  int t = 0;
+  for (; t + 8 <= T; t += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(t + u) * C + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; t < T; ++t) s += part[(size_t)t * C + c];
+  if (sgd.p) {
+    sgd_apply(sgd, c, s, *sgd.lr);
+  } else if (out_bf16) {
+    unsigned short* d = reinterpret_cast<unsigned short*>(out) + c;
+    *d = f2bf(accumulate ? s + bf2f(*d) : s);
+  } else {
+    float* d = reinterpret_cast<float*>(out) + c;
+    *d = accumulate ? s + *d : s;
+  }
+}
+}  // namespace conv
+}  // namespace ddpx
+
+DDPX_API int ddpx_colsum_finish(const float* part, int T, int C, void* out, int out_bf16, int accumulate, float* sgd_p,
+                                float* sgd_buf, void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd,
+                                hipStream_t s) {
+  if (T < 1 || C < 1 || (!out && !sgd_p) || (sgd_p && !sgd_lr)) return -1;
+  hipLaunchKernelGGL(conv::colsum_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, T, C, out, out_bf16,
+                     accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
+  return (int)hipGetLastError();
+}
+
 // dx[P][C] = dgrad(dy, W) (optionally times relu mask of aux — unused by VGG, whose
 // ReLU sits behind BN).  dy [P][Co] bf16, wd [9][Co][C] bf16.
 DDPX_API int ddpx_conv_dgrad(const void* dy, const void* wd, void* dx, int N, int H, int W, int C, int Co,

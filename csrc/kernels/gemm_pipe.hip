@@ -235,8 +235,9 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
   };
   if (K <= 0 || lda0 % 8 || ldb0 % 8 || lda1 % 8 || ldb1 % 8 || M0 % 8 || N0 % 8 || M1 % 8 || N1 % 8) return -20;
   if (((uintptr_t)A0 | (uintptr_t)B0 | (uintptr_t)A1 | (uintptr_t)B1) & 15) return -20;
-  const pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80);
+  pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80);
   const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81);
+  q0.stamp = g_stamp;  // diagnostics: per-role barrier arrival stamps (ddpx_wgrad_sgd.h kStampSlots)
   if ((size_t)q0.a_bytes != ((size_t)(K - 1) * lda0 + M0) * 2 || (size_t)q1.b_bytes != ((size_t)(K - 1) * ldb1 + N1) * 2)
     return -20;  // 32-bit buffer offsets
   if (!wsgd::eligible(q0, false, false) || !wsgd::eligible(q1, false, false) || !wsgd::pair_compatible(q0, q1))

@@ -54,6 +54,47 @@ def conv_fwd(x, wf, Co, stats=True, tile=-1):
     return y, st, T, BM
 
 
+def conv_fwd_act(x, wf, Co, bias, tile=-1):
+    """act [N*H*W, Co] bf16 = relu(conv(x) + bias), bias + ReLU in the GEMM epilogue (DeepNN's conv blocks)."""
+    N, H, W, C = x.shape
+    _nhwc(x, "x")
+    _req(C % 8 == 0 and wf.numel() == Co * 9 * C, "conv_fwd_act: weight/input channel mismatch")
+    _req(bias.dtype == torch.float32 and bias.numel() == Co and bias.is_contiguous(), "conv_fwd_act: bias fp32 [Co]")
+    act = torch.empty((N * H * W, Co), dtype=torch.bfloat16, device=x.device)
+    native.check(native.kernels().ddpx_conv_fwd_act(x.data_ptr(), wf.data_ptr(), act.data_ptr(), bias.data_ptr(),
+                                                    N, H, W, C, Co, tile, native.stream_handle()), "ddpx_conv_fwd_act")
+    return act
+
+
+def conv_dgrad_act(dy, wd, N, H, W, C, Co, act, tile=-1):
+    """(dz [N*H*W, C] bf16, (part [T, C] fp32, T)): the data gradient masked by the ReLU of the block below
+    (``act`` = its relu(conv + bias) output, [N*H*W, C]) in the GEMM epilogue, with per-row-tile column sums of
+    dz (that block's bias gradient, finished by :func:`colsum_finish`)."""
+    _nhwc(dy, "dy", Co)
+    _nhwc(act, "act", C)
+    _req(act.numel() == N * H * W * C, "conv_dgrad_act: act must be [N*H*W, C]")
+    _req(wd.numel() == 9 * Co * C, "conv_dgrad_act: bad weight buffer")
+    lib = native.kernels()
+    T = lib.ddpx_conv_dgrad_tiles_m(N, H, W, C, Co, tile)
+    part = torch.empty((T, C), dtype=torch.float32, device=dy.device)
+    dz = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dy.device)
+    native.check(lib.ddpx_conv_dgrad_act(dy.data_ptr(), wd.data_ptr(), dz.data_ptr(), N, H, W, C, Co, tile,
+                                         act.data_ptr(), part.data_ptr(), native.stream_handle()), "ddpx_conv_dgrad_act")
+    return dz, (part, T)
+
+
+def colsum_finish(part, T, C, out=None, accumulate=False, sgd=None):
+    """out (=|+=) Σ_t part[t] in row-tile order, or applied as ``sgd``'s update (fused optimizer)."""
+    _req(out is not None or sgd is not None, "colsum_finish: out or sgd")
+    if out is not None:
+        _req(out.numel() == C and out.is_contiguous() and out.dtype in (torch.float32, torch.bfloat16),
+             "colsum_finish: bad out")
+    native.check(native.kernels().ddpx_colsum_finish(part.data_ptr(), T, C, native.ptr(out),
+                                                     int(out is not None and out.dtype == torch.bfloat16),
+                                                     int(accumulate), *native.sgd_args(sgd), native.stream_handle()),
+                 "ddpx_colsum_finish")
+
+
 def conv_dgrad(dy, wd, N, H, W, C, Co, tile=-1):
     """dx [N,H,W,C] bf16 = dgrad(dy [N*H*W, Co], wd [9,Co,C])."""
     _nhwc(dy, "dy", Co)

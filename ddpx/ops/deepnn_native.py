@@ -7,8 +7,8 @@
 
 Schedule:
 
-    forward : y  = conv3x3(x, W)                  implicit-GEMM MFMA (no BN statistics)
-              x' = [maxpool2](relu(y + bias))     fused elementwise pass (BN apply kernel, a = 1, b = bias)
+    forward : act = relu(conv3x3(x, W) + bias)    implicit-GEMM MFMA, bias + ReLU in its epilogue
+              x'  = maxpool2(act) (pooled blocks) one pass; un-pooled blocks feed act on as is
               f  = flatten in torch's (C,H,W) order (NHWC → NCHW view of 2048 features)
               a0 = relu(f W0ᵀ + b0)               MFMA GEMM, bias+ReLU epilogue
               d0 = dropout(a0)                    Philox kernel, device-resident (seed, offset)
@@ -16,12 +16,18 @@ Schedule:
     backward: dd0, dW1, db1, db0 = head_bwd(...)  dropout+ReLU backward folded in: mask = d0 > 0,
                                                   scale 1/(1-p); db0 = Σ dd0 from the same kernel
               dW0 = dd0ᵀ f,  df = dd0 W0          MFMA GEMMs
-              per conv block (reverse): dy, dbias = bias_act_bwd(g, y)  (pool routing + ReLU mask
-              recomputed from y); dW = wgrad(dy, x) (split-K MFMA); g = dgrad(dy, W)
+              per conv block (reverse):
+                pooled: dz, dbias = bias_act_bwd(g, act)   (pool routing + ReLU mask from act)
+                un-pooled: dz = dgrad(dz', W') * (act > 0) and its bias-gradient column sums, both in the
+                           epilogue of the block above's data-gradient GEMM (EPI_RELUMASK_BF16), finished
+                           in fixed order (or applied as the bias's fused SGD)
+                dW = wgrad(dz, x) (split-K MFMA); the fused update rewrites the bf16 GEMM layouts of W, so
+                the next forward runs no weight_prep pass
 
 Gradients land in the flat store (DDP buckets) in grad-ready order, or — single process with
 ``SGD(fused_backward=True)`` — weights are updated inside the kernels that produce their
-gradients (conv weights, Linear weights, classifier); conv biases are stepped by the optimizer.
+gradients (conv weights and the un-pooled blocks' biases, Linear weights, classifier); the pooled blocks'
+conv biases are stepped by the optimizer.
 """
 from __future__ import annotations
 
@@ -60,6 +66,9 @@ class _Plan:
             n = Co * 9 * K.padded_channels(Ci)
             self.wf.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
             self.wd.append(torch.empty(n, dtype=torch.bfloat16, device=dev))
+        # FlatParams version each block's prepared layouts were made from (vgg_native's scheme): the fused update
+        # rewrites them, any other update makes them stale
+        self.wver = [None] * len(self.blocks)
         cmax = max(c.weight.shape[0] for c, _ in self.blocks)
         self.ones = torch.ones(cmax, dtype=torch.float32, device=dev)
         self.zeros = torch.zeros(cmax, dtype=torch.float32, device=dev)
@@ -89,22 +98,33 @@ def dropout_(x, p, plan, out=None):
     return out
 
 
-def bias_act_backward(gout, y, bias, N, H, W, C, pool, plan, dbias, accumulate=False):
-    """dy [N*H*W, C] bf16 and dbias (=|+=) Σ dy for out = [pool](relu(y + bias))."""
+# (gout, y, bias, ones, zeros, N, H, W, C, pool, relu, part, c1, c2, dbias, out_bf16, accumulate, dy,
+#  sgd p, buf, shadow, lr, mom, wd, stream)
+native.register_kernel_sig("ddpx_bias_act_bwd_sgd", native.c_int, *([native.c_void_p] * 5 + [native.c_int] * 6
+                                                                     + [native.c_void_p] * 4 + [native.c_int] * 2
+                                                                     + [native.c_void_p] * 5 + [native.c_float] * 2
+                                                                     + [native.c_void_p]))
+
+
+def bias_act_backward(gout, act, N, H, W, C, pool, plan, dbias=None, accumulate=False, sgd=None):
+    """dz [N*H*W, C] bf16 and dbias (=|+=) Σ dz — or, with ``sgd``, that sum applied as the bias's fused SGD
+    update — for out = [pool](act), act = relu(conv + bias): the pool routing (first maximum) and the ReLU mask
+    recomputed from act (bn_pool.hip's backward with a = 1, b = 0)."""
     K._nhwc(gout, "gout", C)
-    K._nhwc(y, "y", C)
+    K._nhwc(act, "act", C)
     lib = native.kernels()
     B = lib.ddpx_bn_bwd_blocks(N, H, W, C)
-    dev = y.device
+    dev = act.device
     part = torch.empty((B, 2, C), dtype=torch.float32, device=dev)
     c1 = torch.empty(C, dtype=torch.float32, device=dev)
     c2 = torch.empty(C, dtype=torch.float32, device=dev)
     dy = torch.empty((N * H * W, C), dtype=torch.bfloat16, device=dev)
-    native.check(lib.ddpx_bias_act_bwd(gout.data_ptr(), y.data_ptr(), bias.data_ptr(), plan.ones.data_ptr(),
-                                       plan.zeros.data_ptr(), N, H, W, C, int(pool), 1, part.data_ptr(),
-                                       c1.data_ptr(), c2.data_ptr(), dbias.data_ptr(),
-                                       int(dbias.dtype == torch.bfloat16), int(accumulate), dy.data_ptr(),
-                                       native.stream_handle()), "ddpx_bias_act_bwd")
+    native.check(lib.ddpx_bias_act_bwd_sgd(gout.data_ptr(), act.data_ptr(), plan.zeros.data_ptr(),
+                                           plan.ones.data_ptr(), plan.zeros.data_ptr(), N, H, W, C, int(pool), 1,
+                                           part.data_ptr(), c1.data_ptr(), c2.data_ptr(), native.ptr(dbias),
+                                           int(dbias is not None and dbias.dtype == torch.bfloat16), int(accumulate),
+                                           dy.data_ptr(), *native.sgd_args(sgd), native.stream_handle()),
+                 "ddpx_bias_act_bwd_sgd")
     return dy
 
 
@@ -133,10 +153,16 @@ def _forward(model, x, targets, want_logits, want_grad, training):
     saved = []
     for bi, (conv, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
-        K.weight_prep(conv.weight, plan.wf[bi], plan.wd[bi])
-        y, _, _, _ = K.conv_fwd(x, plan.wf[bi], Co, stats=False)
-        xn = K.bn_apply(y, plan.ones, conv.bias, N, H, W, Co, relu=True, pool=pool)
-        saved.append((x, y, (N, H, W, C, Co), pool))
+        ver = flat.version_of(conv.weight)
+        if plan.wver[bi] != ver:
+            K.weight_prep(conv.weight, plan.wf[bi], plan.wd[bi])
+            plan.wver[bi] = ver
+        act = K.conv_fwd_act(x, plan.wf[bi], Co, conv.bias)
+        if pool:
+            xn = K.bn_apply(act, plan.ones, plan.zeros, N, H, W, Co, relu=False, pool=True)
+        else:
+            xn = act.view(N, H, W, Co)
+        saved.append((x, act, (N, H, W, C, Co), pool))
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co
     # torch.flatten(x, 1) of the NCHW tensor: features in (C, H, W) order
@@ -186,23 +212,59 @@ def _backward(model, saved, last, dl, grad_out):
         flat.grad_done(l0.weight)
     N, Hf, Wf, Cf = xshape
     g = _nchw_flatten(dfeat, (N, Hf, Wf, Cf))
+    dz_next = None  # (dz, (part, T)) of the current block, made by the data gradient of the block above
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, pool = plan.blocks[bi]
-        x, y, (N, H, W, C, Co), _ = saved[bi]
-        dbias, accb = flat.grad_target(conv.bias)
-        dy = bias_act_backward(g, y, conv.bias, N, H, W, Co, pool, plan, dbias, accumulate=accb)
-        flat.grad_done(conv.bias)
+        x, act, (N, H, W, C, Co), _ = saved[bi]
+        if dz_next is None:
+            # pooled block (or the last one): routing + ReLU mask + bias gradient (or its fused SGD) from g and act
+            sb = flat.fused_spec(conv.bias)
+            if sb is not None:
+                dy = bias_act_backward(g, act, N, H, W, Co, pool, plan, sgd=sb)
+                flat.mark_updated(conv.bias)
+            else:
+                dbias, accb = flat.grad_target(conv.bias)
+                dy = bias_act_backward(g, act, N, H, W, Co, pool, plan, dbias, accumulate=accb)
+                flat.grad_done(conv.bias)
+        else:
+            dy, (part, T) = dz_next
+            sb = flat.fused_spec(conv.bias)
+            if sb is not None:
+                K.colsum_finish(part, T, Co, sgd=sb)
+                flat.mark_updated(conv.bias)
+            else:
+                dbias, accb = flat.grad_target(conv.bias)
+                K.colsum_finish(part, T, Co, out=dbias, accumulate=accb)
+                flat.grad_done(conv.bias)
+        dz_next = None
+        below_pooled = bi > 0 and plan.blocks[bi - 1][1]
+
+        def dgrad():
+            """the gradient for the block below: its pre-activation gradient (+ bias sums) straight from the GEMM
+            epilogue when no pool sits between, else the gradient of its pooled output"""
+            nonlocal g, dz_next
+            if below_pooled:
+                g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            else:
+                dz_next = K.conv_dgrad_act(dy, plan.wd[bi], N, H, W, C, Co, saved[bi - 1][1])
         Cr = conv.weight.shape[1]
         sc = flat.fused_spec(conv.weight)
         if sc is not None:
-            K.conv_wgrad(dy, x, Co, Cr, sgd=sc)
+            # layouts current before this update (the forward made or kept them): the reduce rewrites them with the
+            # updated weight, after this block's data gradient below has read wd (stream order)
+            prep = plan.wver[bi] == flat.version_of(conv.weight)
+            if bi > 0:
+                dgrad()
+            K.conv_wgrad(dy, x, Co, Cr, sgd=sc, prepared=(plan.wf[bi], plan.wd[bi]) if prep else None)
             flat.mark_updated(conv.weight)
-        else:
-            dw, accw = flat.grad_target(conv.weight)
-            K.conv_wgrad(dy, x, Co, Cr, out=dw, accumulate=accw)
-            flat.grad_done(conv.weight)
+            if prep:
+                plan.wver[bi] = flat.version_of(conv.weight)
+            continue
+        dw, accw = flat.grad_target(conv.weight)
+        K.conv_wgrad(dy, x, Co, Cr, out=dw, accumulate=accw)
+        flat.grad_done(conv.weight)
         if bi > 0:
-            g = K.conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+            dgrad()
 
 
 class _DeepNNLoss(torch.autograd.Function):

@@ -205,7 +205,7 @@ def linear_dgrad(dy, w, relu_mask_of=None, out=None, tile=-1, bias_grad=None, bi
     return out
 
 
-_EIGHT_WAVE_TILES = (8, 13, 14, 15)
+_EIGHT_WAVE_TILES = (8, 13, 14, 15, 22, 25)  # ddpx_pipe.h eight_wave()
 
 
 def linear_wgrad(dy, x, out, accumulate=False, tile=-1, sgd=None):

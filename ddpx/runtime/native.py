@@ -74,6 +74,10 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_fwd_tile_rows", I, I, I, I, I)
     _sig(lib, "ddpx_conv_fwd", I, P, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad", I, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_fwd_act", I, P, P, P, P, I, I, I, I, I, I, P)
+    _sig(lib, "ddpx_conv_dgrad_tiles_m", I, I, I, I, I, I, I)
+    _sig(lib, "ddpx_conv_dgrad_act", I, P, P, P, I, I, I, I, I, I, P, P, P)
+    _sig(lib, "ddpx_colsum_finish", I, P, I, I, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_conv_dgrad_parts", I, I, I, I, I, I, I)
     _sig(lib, "ddpx_conv_dgrad_bn", I, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, P, P)
     _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I, I)

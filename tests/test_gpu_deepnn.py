@@ -34,6 +34,8 @@ def _pair(gpu, seed=0, p=None):
 
 @pytest.mark.parametrize("pool", [False, True])
 def test_bias_relu_pool_backward(gpu, pool):
+    """dz, dbias of out = [pool](act), act = relu(y + bias) stored bf16 (the conv epilogue's output): routing and
+    ReLU mask from act alone, vs torch autograd through relu(y + bias) [+ max_pool2d]."""
     from ddpx.ops import conv as K
     from ddpx.ops.deepnn_native import bias_act_backward
 
@@ -46,20 +48,64 @@ def test_bias_relu_pool_backward(gpu, pool):
     plan.zeros = torch.zeros(C, device=gpu)
     y = _bf(torch.randn(N * H * H, C, device=gpu))
     bias = torch.randn(C, device=gpu) * 0.3
-    out = K.bn_apply(y.to(torch.bfloat16).contiguous(), plan.ones, bias, N, H, H, C, relu=True, pool=pool)
+    act = torch.relu(y + bias).to(torch.bfloat16).contiguous()
+    out = K.bn_apply(act, plan.ones, plan.zeros, N, H, H, C, relu=False, pool=True) if pool else act
     yn = y.view(N, H, H, C).permute(0, 3, 1, 2).clone().requires_grad_(True)
     br = bias.clone().requires_grad_(True)
-    z = F.relu(yn + br.view(1, C, 1, 1))
+    zr = F.relu(yn + br.view(1, C, 1, 1))
+    # the pool routes on the STORED bf16 activation (as torch's autocast pool does): straight-through rounding
+    z = zr + (zr.to(torch.bfloat16).float() - zr).detach()
     if pool:
         z = F.max_pool2d(z, 2)
-    assert _rel(out.permute(0, 3, 1, 2), z) < 1e-2
+    assert _rel(out.view(N, *z.shape[2:], C).permute(0, 3, 1, 2), z) < 1e-2
     g = _bf(torch.randn_like(z))
     z.backward(g)
     db = torch.empty(C, device=gpu)
-    dy = bias_act_backward(g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), y.to(torch.bfloat16).contiguous(),
-                           bias, N, H, H, C, pool, plan, db)
+    dy = bias_act_backward(g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), act, N, H, H, C, pool, plan, db)
     assert _rel(db, br.grad) < 1e-2
     assert _rel(dy.view(N, H, H, C).permute(0, 3, 1, 2), yn.grad) < 1e-2
+    # the same sum applied as the bias's fused SGD update (no momentum history: p -= lr * (g + wd p))
+    p0 = torch.randn(C, device=gpu)
+    p1, buf = p0.clone(), torch.zeros(C, device=gpu)
+    lr = torch.full((), 0.1, device=gpu)
+    bias_act_backward(g.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), act, N, H, H, C, pool, plan,
+                      sgd=(p1, buf, None, lr, 0.9, 5e-4))
+    d = db + 5e-4 * p0
+    assert torch.allclose(p1, p0 - 0.1 * d, atol=1e-6) and torch.allclose(buf, d, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(8, 16, 16, 64, 32), (4, 32, 32, 8, 128), (2, 8, 8, 64, 64)])
+def test_conv_bias_relu_epilogue_and_masked_dgrad(gpu, shape):
+    """DeepNN's fused conv epilogues vs torch fp32: act = relu(conv(x) + b) (EPI_BIAS_RELU_BF16), and the data
+    gradient masked by the ReLU of the block below with its bias-gradient column sums (EPI_RELUMASK_BF16 +
+    per-tile partials finished in fixed order, stored or applied as SGD)."""
+    from ddpx.ops import conv as K
+    N, H, W, C, Co = shape
+    torch.manual_seed(7)
+    x = _bf(torch.randn(N, C, H, W, device=gpu))
+    w = torch.randn(Co, C, 3, 3, device=gpu) * (1.0 / (9 * C) ** 0.5)
+    b = torch.randn(Co, device=gpu) * 0.2
+    wf = torch.empty(Co * 9 * C, dtype=torch.bfloat16, device=gpu)
+    wd = torch.empty_like(wf)
+    K.weight_prep(w.contiguous(), wf, wd)
+    xh = x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    act = K.conv_fwd_act(xh, wf, Co, b)
+    ref = torch.relu(F.conv2d(x, _bf(w), b, padding=1))
+    assert _rel(act.view(N, H, W, Co).permute(0, 3, 1, 2), ref) < 1e-2
+    # data gradient of this conv, masked by the ReLU of a block below whose activation is `below`
+    below = torch.relu(_bf(torch.randn(N, H, W, C, device=gpu))).to(torch.bfloat16).contiguous()
+    dy = _bf(torch.randn(N * H * W, Co, device=gpu)).to(torch.bfloat16)
+    dz, (part, T) = K.conv_dgrad_act(dy, wd, N, H, W, C, Co, below.view(N * H * W, C))
+    dyn = dy.float().view(N, H, W, Co).permute(0, 3, 1, 2)
+    dx = torch.nn.grad.conv2d_input((N, C, H, W), _bf(w), dyn, padding=1)
+    mask = (below.float().permute(0, 3, 1, 2) > 0).float()
+    refz = dx * mask
+    assert _rel(dz.view(N, H, W, C).permute(0, 3, 1, 2), refz) < 1e-2
+    db = torch.empty(C, device=gpu)
+    K.colsum_finish(part, T, C, out=db)
+    assert _rel(db, dz.float().sum(0)) < 1e-5
+    K.colsum_finish(part, T, C, out=db, accumulate=True)
+    assert _rel(db, 2 * dz.float().sum(0)) < 1e-5
 
 
 def test_dropout_kernel_statistics_and_graph(gpu):

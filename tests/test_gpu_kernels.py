@@ -13,7 +13,7 @@ def _rand_bf16(*shape, dev):
     return (torch.randn(*shape, device=dev) * 0.5).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("tile", list(range(-1, 14)) + [16, 17, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("tile", list(range(-1, 14)) + [16, 17, 18, 19, 20, 21, 22, 23, 24, 25])
 @pytest.mark.parametrize("layout", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("MNK", [(512, 4096, 3072), (336, 256, 512), (128, 128, 64), (106, 64, 200), (64, 192, 72),
                                  (200, 136, 1000), (2048, 4096, 512)])
