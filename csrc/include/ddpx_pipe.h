@@ -431,18 +431,18 @@ __device__ __forceinline__ void lds_signal(int* c, int lane) {
 template <int E>
 __device__ __forceinline__ float epi_one(const Params& p, void* Cbase, size_t off, int n, float v, float lr,
                                          float cin, unsigned short auxv, float pv, float bv, float* p_out,
-                                         float* b_out) {
+                                         float* b_out, float bias_n) {
   float stored;
   if constexpr (E == EPI_F32) {
     stored = v * p.alpha + cin;
   } else if constexpr (E == EPI_BF16 || E == EPI_BNSTAT_BF16) {
     stored = bf2f(f2bf(v * p.alpha + cin));
   } else if constexpr (E == EPI_BIAS_BF16) {  // alpha: dequant scale of the fp8 GEMMs (1 for bf16)
-    stored = bf2f(f2bf(fmaf(v, p.alpha, p.bias[n])));
+    stored = bf2f(f2bf(fmaf(v, p.alpha, bias_n)));
   } else if constexpr (E == EPI_BIAS_RELU_BF16) {
-    stored = bf2f(f2bf(fmaxf(fmaf(v, p.alpha, p.bias[n]), 0.f)));
+    stored = bf2f(f2bf(fmaxf(fmaf(v, p.alpha, bias_n), 0.f)));
   } else if constexpr (E == EPI_BIAS_F32) {
-    stored = fmaf(v, p.alpha, p.bias[n]);
+    stored = fmaf(v, p.alpha, bias_n);
   } else if constexpr (E == EPI_SGD) {
     stored = v * p.alpha;
     float d = fmaf(p.sgd.wd, pv, stored);
@@ -470,6 +470,20 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
   const bool vec = (n + 3 < p.N) && ((p.ldc & 3) == 0);
   float lr = 0.f;
   if constexpr (E == EPI_SGD) lr = *p.sgd.lr;
+  // the thread's 4 columns are fixed: their bias is loaded once, not per row (the stores to C may alias p.bias
+  // as far as the compiler knows, so it re-loaded bias[n] for every element)
+  constexpr bool HAS_BIAS = E == EPI_BIAS_BF16 || E == EPI_BIAS_RELU_BF16 || E == EPI_BIAS_F32;
+  float bq[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (HAS_BIAS) {
+    if (vec && !(reinterpret_cast<uintptr_t>(p.bias + n) & 15)) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bq[q] = b4[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bq[q] = n + q < p.N ? p.bias[n + q] : 0.f;
+    }
+  }
   // vectors whose loads are in flight together: the fused-SGD epilogue is a pure stream (p, momentum
   // in; p, momentum, shadow out) and needs every byte in flight it can get; the others stay at 4
   constexpr int CH = E == EPI_SGD ? (NV < 8 ? NV : 8) : (NV < 4 ? NV : 4);
@@ -524,7 +538,8 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const unsigned short av = (unsigned short)((q & 1) ? (ain[i][q >> 1] >> 16) : (ain[i][q >> 1] & 0xffffu));
-        st[q] = epi_one<E>(p, Cbase, off + q, n + q, v[q], lr, cin[i][q], av, pin[i][q], bin[i][q], &po[q], &bo[q]);
+        st[q] = epi_one<E>(p, Cbase, off + q, n + q, v[q], lr, cin[i][q], av, pin[i][q], bin[i][q], &po[q], &bo[q],
+                           bq[q]);
         csum[q] += st[q];
       }
       if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
@@ -557,7 +572,7 @@ __device__ __forceinline__ void epilogue_vec(const Params& p, void* Cbase, const
         if constexpr (E == EPI_RELUMASK_BF16) av = p.aux[(size_t)m * p.ldaux + n + q];
         if constexpr (E == EPI_SGD) { pv = p.sgd.p[o]; if (p.sgd.mom != 0.f) bv = p.sgd.buf[o]; }
         float po = 0.f, bo = 0.f;
-        const float st = epi_one<E>(p, Cbase, o, n + q, v[q], lr, c0, av, pv, bv, &po, &bo);
+        const float st = epi_one<E>(p, Cbase, o, n + q, v[q], lr, c0, av, pv, bv, &po, &bo, bq[q]);
         csum[q] += st;
         if constexpr (E == EPI_F32 || E == EPI_BIAS_F32) {
           reinterpret_cast<float*>(Cbase)[o] = st;

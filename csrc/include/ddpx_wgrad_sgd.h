@@ -62,12 +62,17 @@ struct Cfg {
 // 1 = every K-step runs its MFMAs twice (the second set into a
 // dead accumulator kept live), 2 = also a second operand stage of LDS-DMA per K-step into a dummy ring — the
 // math and L2->LDS load a fused data-gradient GEMM would add beside the weight-gradient tiles.
-template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false>
-__global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
+// NMW: math waves, 4 (2 x 2 waves of 32 x 64) or 8 (2 x 4 waves of 32 x 32: two MFMA waves per SIMD, so one wave's
+// fragment reads, DMA issue and barrier wait run under the other's MFMAs — the 4-wave math side ran its K-steps at
+// 11 % MFMA busy with its waves waiting 62 % of their cycles, profiles/r6_pair).
+template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false, int NMW = 4>
+__global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
   constexpr int ALD = Cfg<STAGES, XTRA, SB>::ALD, ACC_BYTES = Cfg<STAGES, XTRA, SB>::ACC_BYTES;
   constexpr int LDS_BYTES = Cfg<STAGES, XTRA, SB>::LDS_BYTES;
-  constexpr int FM = 2, FN = 4;                  // math wave tile 32 x 64
-  constexpr int LPW = (BM + BN) / (8 * 4);       // LDS-DMA instructions per math wave per stage
+  static_assert(NMW == 4 || NMW == 8, "math waves");
+  constexpr int WN = NMW / 2;                    // math waves along N
+  constexpr int FM = 2, FN = BN / WN / 16;       // math wave tile 32 x (BN / WN)
+  constexpr int LPW = (BM + BN) / (8 * NMW);     // LDS-DMA instructions per math wave per stage
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   float* const accb = reinterpret_cast<float*>(smem + STAGES * SLOT);
 
@@ -99,8 +104,8 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     return sel;
   };
   const pipe::Params& p = p0;  // K, alpha, lr, momentum, wd: shared by both GEMMs
-  long long* const stp = (p0.stamp && (tid == 0 || tid == 256))
-                             ? p0.stamp + ((size_t)blockIdx.x * 2 + (wave < 4 ? 0 : 1)) * kStampSlots
+  long long* const stp = (p0.stamp && (tid == 0 || tid == 64 * NMW))
+                             ? p0.stamp + ((size_t)blockIdx.x * 2 + (wave < NMW ? 0 : 1)) * kStampSlots
                              : nullptr;
   int nstamp = 1;
   auto mark = [&]() {  // arrival at the role's next barrier
@@ -111,9 +116,9 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
   };
   if (stp) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
 
-  if (wave < 4) {
+  if (wave < NMW) {
     // ------------------------------------------------------------------ math waves
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p0.A, 0, p0.a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rb0 = __builtin_amdgcn_make_buffer_rsrc((void*)p0.B, 0, p0.b_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)p1.A, 0, p1.a_bytes, 0x00020000);
@@ -123,23 +128,27 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     // the next tile, so the ring never drains and refills at a tile boundary (with K = 512 a tile is only
     // nk = 8 K-steps: a per-tile refill cost ~2 of every 10 K-steps of L2 latency).
     const int G = nt * nk;
+    // the issuer walks g = 0, 1, 2, ... in order: the tile origin (integer divisions) is computed once per tile
+    int iss_i = -1, iss_kt = nk - 1, iss_m0 = 0, iss_n0 = 0, iss_sel = 0;
     auto issue = [&](int g) {
       if constexpr (XTRA == 4) return;  // measurement: stream only
-      int m0, n0;
-      const int sel = tile_origin(g / nk, m0, n0);
-      const int kt = g % nk;
+      if (++iss_kt >= nk) {
+        iss_kt = 0;
+        iss_sel = tile_origin(++iss_i, iss_m0, iss_n0);
+      }
+      const int m0 = iss_m0, n0 = iss_n0, sel = iss_sel, kt = iss_kt;
       const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0, rb = sel ? rb1 : rb0;
       const int lda = sel ? p1.lda : p0.lda, ldb = sel ? p1.ldb : p0.ldb;
       const int Mg = sel ? p1.M : p0.M, Ng = sel ? p1.N : p0.N;
       char* slot = smem + (g % STAGES) * SLOT;
-      pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, slot, p.conv, lda, m0, Mg, kt * 64, p.K, wave, lane);
-      pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, kt * 64, p.K, wave,
-                                                       lane);
+      pipe::stage_tile<BM, false, pipe::MODE_PLAIN, NMW>(ra, slot, p.conv, lda, m0, Mg, kt * 64, p.K, wave, lane);
+      pipe::stage_tile<BN, false, pipe::MODE_PLAIN, NMW>(rb, slot + A_SUB, p.conv, ldb, n0, Ng, kt * 64, p.K, wave,
+                                                         lane);
       if constexpr (XTRA == 2) {  // dummy second stage (same operands, other k rows) into the extra ring
         char* x = smem + STAGES * SLOT + 2 * ACC_BYTES;  // one dummy slot (its contents are never used)
         const int kx = ((kt + 3) % (p.K / 64)) * 64;
-        pipe::stage_tile<BM, false, pipe::MODE_PLAIN, 4>(ra, x, p.conv, lda, m0, Mg, kx, p.K, wave, lane);
-        pipe::stage_tile<BN, false, pipe::MODE_PLAIN, 4>(rb, x + A_SUB, p.conv, ldb, n0, Ng, kx, p.K, wave, lane);
+        pipe::stage_tile<BM, false, pipe::MODE_PLAIN, NMW>(ra, x, p.conv, lda, m0, Mg, kx, p.K, wave, lane);
+        pipe::stage_tile<BN, false, pipe::MODE_PLAIN, NMW>(rb, x + A_SUB, p.conv, ldb, n0, Ng, kx, p.K, wave, lane);
       }
     };
 #pragma unroll
@@ -175,7 +184,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
 #pragma unroll
           for (int kk = 0; kk < (XTRA == 4 ? 0 : 64); kk += 32) {
             bf16x8 af[FM], bfr[FN];
-            pipe::load_frags<BM, false, FM, BN, false, FN>(sa, wm * 32, sb, wn * 64, kk, lane, af, bfr);
+            pipe::load_frags<BM, false, FM, BN, false, FN>(sa, wm * 32, sb, wn * (BN / WN), kk, lane, af, bfr);
 #pragma unroll
             for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -184,7 +193,8 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
             if constexpr (XTRA == 1 || XTRA == 2) {
               const char* xa = XTRA == 2 ? smem + STAGES * SLOT + 2 * ACC_BYTES : sa;
               bf16x8 af2[FM], bf2[FN];
-              pipe::load_frags<BM, false, FM, BN, false, FN>(xa, wm * 32, xa + A_SUB, wn * 64, kk, lane, af2, bf2);
+              pipe::load_frags<BM, false, FM, BN, false, FN>(xa, wm * 32, xa + A_SUB, wn * (BN / WN), kk, lane, af2,
+                                                             bf2);
 #pragma unroll
               for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -201,7 +211,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
         }
         // accumulators -> tile buffer i&1 (C/D map: row 4*(lane>>4)+r, col lane&15 of each 16x16 block)
         float* T = accb + (SB ? 0 : (i & 1) * (ACC_BYTES / 4));
-        const int mr = wm * 32 + 4 * (lane >> 4), nc = wn * 64 + (lane & 15);
+        const int mr = wm * 32 + 4 * (lane >> 4), nc = wn * (BN / WN) + (lane & 15);
 #pragma unroll
         for (int a = 0; a < FM; ++a)
 #pragma unroll
@@ -229,7 +239,7 @@ __global__ void __launch_bounds__(256 + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Para
     constexpr int KPU = VPT / SV;                 // K-steps per update: 1 or 2
     constexpr int RSTEP = NSW * 2;                // tile rows between a thread's consecutive vectors
     static_assert(SV % DIST == 0 && VPT % SV == 0, "ring");
-    const int st = tid - 256;
+    const int st = tid - 64 * NMW;
     const int row0 = st >> 5, col = 4 * (st & 31);  // row0 < RSTEP
     const float lr = *p.sgd.lr;
     const float mom = p.sgd.mom, wd = p.sgd.wd;
@@ -433,10 +443,32 @@ static inline int xtra() {
   return v;
 }
 
+// Math waves: DDPX_WSGD_MATH_WAVES=4|8 (default 8: profiles/r6_pair).
+static inline int math_waves() {
+  static const int v = [] {
+    const char* e = getenv("DDPX_WSGD_MATH_WAVES");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  return v;
+}
+
 template <int STAGES, bool FP8>
 static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1,
                                int nsw) {
   const bool no = n_order();
+  if constexpr (STAGES == 3 || STAGES == 4) {
+    if (math_waves() == 8 && nsw == 4 && no && (FP8 || single_buffer() == 0)) {
+      const int x = FP8 ? 0 : xtra();
+      if constexpr (!FP8 && STAGES == 3) {  // measurement: math only / stream only (benchmarks/pair_stamps.py)
+        if (x == 3) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 3, false, 8>), grid, dim3(768), 0, s, p0, p1, nt1); return; }
+        if (x == 4) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 4, false, 8>), grid, dim3(768), 0, s, p0, p1, nt1); return; }
+      }
+      if (x == 0) {
+        hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true, 0, false, 8>), grid, dim3(768), 0, s, p0, p1, nt1);
+        return;
+      }
+    }
+  }
   if constexpr (!FP8 && STAGES == 3) {
     // measurement variants: DDPX_WSGD_XTRA=3 math only, 4 stream only (benchmarks/pair_stamps.py)
     const int x = xtra();

@@ -328,22 +328,48 @@ DDPX_API int ddpx_conv_dgrad_act(const void* dy, const void* wd, void* dz, int N
 
 namespace ddpx {
 namespace conv {
-// out[c] (=|+=) sum_t part[t][c] in t order (8 loads in flight), or the fused SGD of the parameter out points at
-__global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restrict__ part, int T, int C,
+// out[c] (=|+=) sum_t part[t][c], or the fused SGD of the parameter out points at.  Two fixed-order levels (the
+// partials can be 4096 rows: one thread per channel walking them all took 237 us): split sp of S sums rows
+// [sp * RS, (sp + 1) * RS) as 4 interleaved row groups merged in group order, then one thread per channel adds
+// the S split sums in split order.  Deterministic.
+constexpr int kColsumRows = 64;  // rows per split
+__global__ void __launch_bounds__(256) colsum_split_kernel(const float* __restrict__ part, int T, int C,
+                                                           float* __restrict__ ws) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, sp = blockIdx.y;
+  const int t0 = sp * kColsumRows, t1 = min(T, t0 + kColsumRows);
+  float s = 0.f;
+  if (c < C) {
+    float v[kColsumRows / 4];
+#pragma unroll
+    for (int u = 0; u < kColsumRows / 4; ++u) {
+      const int t = t0 + g + 4 * u;
+      v[u] = t < t1 ? part[(size_t)t * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kColsumRows / 4; ++u) s += v[u];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < C) ws[(size_t)sp * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
+__global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restrict__ ws, int S, int C,
                                                             void* __restrict__ out, int out_bf16, int accumulate,
                                                             SgdArgs sgd) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
   int t = 0;
-  for (; t + 8 <= T; t += 8) {
+  for (; t + 8 <= S; t += 8) {
     float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(t + u) * C + c];
+    for (int u = 0; u < 8; ++u) v[u] = ws[(size_t)(t + u) * C + c];
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
-  for (; t < T; ++t) s += part[(size_t)t * C + c];
+  for (; t < S; ++t) s += ws[(size_t)t * C + c];
   if (sgd.p) {
     sgd_apply(sgd, c, s, *sgd.lr);
   } else if (out_bf16) {
@@ -357,11 +383,18 @@ __global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restr
 }  // namespace conv
 }  // namespace ddpx
 
-DDPX_API int ddpx_colsum_finish(const float* part, int T, int C, void* out, int out_bf16, int accumulate, float* sgd_p,
-                                float* sgd_buf, void* sgd_shadow, const float* sgd_lr, float sgd_mom, float sgd_wd,
-                                hipStream_t s) {
-  if (T < 1 || C < 1 || (!out && !sgd_p) || (sgd_p && !sgd_lr)) return -1;
-  hipLaunchKernelGGL(conv::colsum_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, T, C, out, out_bf16,
+// Workspace floats ddpx_colsum_finish needs for T partial rows of C columns.
+DDPX_API long long ddpx_colsum_ws_floats(int T, int C) {
+  return (long long)((T + conv::kColsumRows - 1) / conv::kColsumRows) * C;
+}
+
+DDPX_API int ddpx_colsum_finish(const float* part, int T, int C, float* ws, void* out, int out_bf16, int accumulate,
+                                float* sgd_p, float* sgd_buf, void* sgd_shadow, const float* sgd_lr, float sgd_mom,
+                                float sgd_wd, hipStream_t s) {
+  if (T < 1 || C < 1 || !ws || (!out && !sgd_p) || (sgd_p && !sgd_lr)) return -1;
+  const int S = (T + conv::kColsumRows - 1) / conv::kColsumRows;
+  hipLaunchKernelGGL(conv::colsum_split_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, part, T, C, ws);
+  hipLaunchKernelGGL(conv::colsum_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, out, out_bf16,
                      accumulate, SgdArgs{sgd_p, sgd_buf, (unsigned short*)sgd_shadow, sgd_lr, sgd_mom, sgd_wd});
   return (int)hipGetLastError();
 }

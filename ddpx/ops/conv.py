@@ -89,7 +89,9 @@ def colsum_finish(part, T, C, out=None, accumulate=False, sgd=None):
     if out is not None:
         _req(out.numel() == C and out.is_contiguous() and out.dtype in (torch.float32, torch.bfloat16),
              "colsum_finish: bad out")
-    native.check(native.kernels().ddpx_colsum_finish(part.data_ptr(), T, C, native.ptr(out),
+    lib = native.kernels()
+    ws = torch.empty(lib.ddpx_colsum_ws_floats(T, C), dtype=torch.float32, device=part.device)
+    native.check(lib.ddpx_colsum_finish(part.data_ptr(), T, C, ws.data_ptr(), native.ptr(out),
                                                      int(out is not None and out.dtype == torch.bfloat16),
                                                      int(accumulate), *native.sgd_args(sgd), native.stream_handle()),
                  "ddpx_colsum_finish")

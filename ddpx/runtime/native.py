@@ -77,7 +77,8 @@ def _declare_kernels(lib):
     _sig(lib, "ddpx_conv_fwd_act", I, P, P, P, P, I, I, I, I, I, I, P)
     _sig(lib, "ddpx_conv_dgrad_tiles_m", I, I, I, I, I, I, I)
     _sig(lib, "ddpx_conv_dgrad_act", I, P, P, P, I, I, I, I, I, I, P, P, P)
-    _sig(lib, "ddpx_colsum_finish", I, P, I, I, P, I, I, P, P, P, P, F, F, P)
+    _sig(lib, "ddpx_colsum_ws_floats", ctypes.c_longlong, I, I)
+    _sig(lib, "ddpx_colsum_finish", I, P, I, I, P, P, I, I, P, P, P, P, F, F, P)
     _sig(lib, "ddpx_conv_dgrad_parts", I, I, I, I, I, I, I)
     _sig(lib, "ddpx_conv_dgrad_bn", I, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, P, P)
     _sig(lib, "ddpx_conv_wgrad_splits", I, I, I, I, I)
