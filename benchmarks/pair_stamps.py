@@ -39,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--time_only", action="store_true")
+    ap.add_argument("--xwg", action="store_true", help="two-workgroup pair: placement + per-role spans")
     a = ap.parse_args()
     native.register_kernel_sig("ddpx_gemm_set_stamps", None, native.c_void_p)
     lib = native.kernels()
@@ -65,6 +67,47 @@ def main():
     for _ in range(3):
         run()
     torch.cuda.synchronize()
+    # plain timing: 20 back-to-back launches (every variant, stamped or not)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"pair_us_per_launch": round(e0.elapsed_time(e1) * 1000 / 20, 2),
+                      "xwg_poll_timeouts": G.xwg_poll_timeouts(dev)}), flush=True)
+    if a.time_only:
+        return
+    if a.xwg:
+        # two-workgroup pair: per workgroup [HW_ID, XCC_ID, start, end] -> placement of the roles and their spans
+        st = torch.zeros((1024, 4), dtype=torch.int64, device=dev)
+        lib.ddpx_gemm_set_stamps(st.data_ptr())
+        run()
+        torch.cuda.synchronize()
+        lib.ddpx_gemm_set_stamps(None)
+        s = st.cpu().numpy()
+        n = int((s[:, 2] != 0).sum())
+        G2 = n // 2
+        t0 = s[:n, 2].min()
+
+        def cu_key(hw, xcc):  # (xcc, se, sh, cu) from HW_ID: cu [11:8], sh [12], se [15:13]
+            return (int(xcc) & 0xf, (int(hw) >> 13) & 7, (int(hw) >> 12) & 1, (int(hw) >> 8) & 0xf)
+        where = {}
+        for b in range(n):
+            where.setdefault(cu_key(s[b, 0], s[b, 1]), []).append("M" if b < G2 else "S")
+        kinds = {}
+        for v in where.values():
+            k = "".join(sorted(v))
+            kinds[k] = kinds.get(k, 0) + 1
+        math_span = [(s[b, 3] - s[b, 2]) / 100.0 for b in range(G2)]
+        strm_span = [(s[b, 3] - s[b, 2]) / 100.0 for b in range(G2, n)]
+        end = (s[:n, 3].max() - t0) / 100.0
+        print(json.dumps({"workgroups": n, "cus_used": len(where), "cu_role_mix": kinds,
+                          "math_span_med": med(math_span), "math_span_max": max(math_span),
+                          "stream_span_med": med(strm_span), "stream_span_max": max(strm_span),
+                          "stream_start_med": med([(s[b, 2] - t0) / 100.0 for b in range(G2, n)]),
+                          "kernel_span": end}), flush=True)
+        return
     st = torch.zeros((256 * 2, SLOTS), dtype=torch.int64, device=dev)
     out = {"reps": []}
     for _ in range(a.reps):

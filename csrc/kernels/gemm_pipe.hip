@@ -36,6 +36,7 @@
 #include "ddpx_gemm_dispatch.h"
 #include "ddpx_pipe.h"
 #include "ddpx_wgrad_sgd.h"
+#include "ddpx_wgrad_sgd_xwg.h"
 #include "ddpx_wsgd_dgrad.h"
 
 namespace ddpx {
@@ -94,6 +95,27 @@ static int plan(int M, int N, int K, bool ak, bool bk, int epi, int* cfg) {
 using namespace ddpx;
 
 static long long* g_stamp = nullptr;
+
+// Scratch of the two-workgroup wgrad + SGD pair (ddpx_wgrad_sgd_xwg.h): gradient tile slots [cap][2][64x128] fp32 and
+// counters [2 cap + 1] int (zeroed once; every launch leaves them zero); cap = workgroup pairs it holds.
+static float* g_xwg_T = nullptr;
+static int* g_xwg_cnt = nullptr;
+static int g_xwg_cap = 0;
+DDPX_API void ddpx_wsgd_set_xwg_scratch(float* T, int* counters, int cap) {
+  g_xwg_T = T;
+  g_xwg_cnt = counters;
+  g_xwg_cap = (T && counters) ? cap : 0;
+}
+// DDPX_WSGD_XWG=1 (measurement): the two-workgroup pair.  Measured slower (profiles/r6_pair/NOTES.md: 178-186 vs
+// 123 us back to back): unpaced, the optimizer stream's HBM traffic stalls the CU's texture-address path that the
+// MFMA side's operand DMA shares, and the math side runs at half speed; the one-workgroup lock-step paces it.
+static bool xwg_on() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_WSGD_XWG");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 // Diagnostics: every following ddpx_gemm_pipe launch writes per-workgroup timestamps into buf
 // ([workgroups][8] int64, s_memrealtime); nullptr turns it off (benchmarks/gemm_stamps.py).
@@ -237,7 +259,7 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
   if (((uintptr_t)A0 | (uintptr_t)B0 | (uintptr_t)A1 | (uintptr_t)B1) & 15) return -20;
   pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80);
   const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81);
-  q0.stamp = g_stamp;  // diagnostics: per-role barrier arrival stamps (ddpx_wgrad_sgd.h kStampSlots)
+  q0.stamp = g_stamp;  // diagnostics: per-role barrier arrival stamps (ddpx_wgrad_sgd.h kStampSlots) / xwg placement
   if ((size_t)q0.a_bytes != ((size_t)(K - 1) * lda0 + M0) * 2 || (size_t)q1.b_bytes != ((size_t)(K - 1) * ldb1 + N1) * 2)
     return -20;  // 32-bit buffer offsets
   if (!wsgd::eligible(q0, false, false) || !wsgd::eligible(q1, false, false) || !wsgd::pair_compatible(q0, q1))
@@ -247,6 +269,12 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
+  if (xwg_on() && g_xwg_cap > 0 && !q80 && wsgd::xwg::launch_pair(q0, q1, cus,
+                                                                  wsgd::xwg::Scratch{g_xwg_T, g_xwg_cnt,
+                                                                                     g_xwg_cnt + g_xwg_cap,
+                                                                                     g_xwg_cnt + 2 * g_xwg_cap},
+                                                                  g_xwg_cap, stream) == hipSuccess)
+    return 0;
   return (int)wsgd::launch_pair(q0, q1, cus, stream);
 }
 

@@ -15,6 +15,8 @@ wgrad      dW[N,K] = dY[M,N]ᵀ · X[M,K]   M-contig     N-contig
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..runtime import native
@@ -252,6 +254,34 @@ native.register_kernel_sig("ddpx_wgrad_sgd_pair", native.c_int, *([native.c_void
                            native.c_int, native.c_void_p, native.c_float, native.c_float, native.c_void_p)
 
 
+native.register_kernel_sig("ddpx_wsgd_set_xwg_scratch", None, native.c_void_p, native.c_void_p, native.c_int)
+_XWG = {}
+# DDPX_WSGD_XWG=1: the two-workgroup pair (measurement variant, measured slower: profiles/r6_pair/NOTES.md)
+_XWG_ON = os.environ.get("DDPX_WSGD_XWG", "0") == "1"
+
+
+def _xwg_scratch(dev):
+    """Persistent scratch of the two-workgroup pair (csrc/include/ddpx_wgrad_sgd_xwg.h), made once per device and
+    handed to the library: gradient tile slots [CUs][2][64x128] fp32 + counters [2 CUs + 1] int32 (zero; every
+    launch leaves them zero; the last word counts poll timeouts)."""
+    if dev.index in _XWG:
+        return _XWG[dev.index]
+    cap = torch.cuda.get_device_properties(dev).multi_processor_count
+    T = torch.empty(cap * 2 * 64 * 128, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(2 * cap + 1, dtype=torch.int32, device=dev)
+    native.kernels().ddpx_wsgd_set_xwg_scratch(T.data_ptr(), cnt.data_ptr(), cap)
+    _XWG[dev.index] = (T, cnt, cap)
+    return _XWG[dev.index]
+
+
+def xwg_poll_timeouts(dev) -> int:
+    """Poll timeouts of the two-workgroup pair on ``dev`` since its scratch was made (0 = every hand-off healthy)."""
+    if dev.index not in _XWG:
+        return 0
+    _, cnt, cap = _XWG[dev.index]
+    return int(cnt[2 * cap].item())
+
+
 def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
     """Both fused weight-gradient + SGD updates (dW_i = dy_iᵀ x_i applied to sgd_i's parameter) in ONE
     warp-specialised launch.  False (nothing launched) when the pair is not eligible; the caller then
@@ -277,6 +307,8 @@ def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
                  native.ptr(sg[1]), native.ptr(sg[2]), native.ptr(mx[0] if mx else None),
                  native.ptr(mx[1] if mx else None)]
     lr = sg[3]
+    if _XWG_ON:
+        _xwg_scratch(dy0.device)
     rc = native.kernels().ddpx_wgrad_sgd_pair(*args, K, lr.data_ptr(), float(sgd0[4]), float(sgd0[5]),
                                               native.stream_handle())
     if rc == -20:
