@@ -119,6 +119,10 @@ def parse(argv=None):
     p.add_argument("--json_out", default=None)
     p.add_argument("--ddp_single", action="store_true",
                    help="N=1: still run the DDP machinery (RCCL reducer at world size 1) to measure its overhead")
+    p.add_argument("--sim_world", type=int, default=None,
+                   help="diagnostics, with --ddp_single: present world size N to DDP (the N-rank bucket plan, ZeRO-1 "
+                        "shards of 1/N, this rank's 1/N optimizer stream) on a one-rank communicator whose collectives "
+                        "are skipped: the per-rank compute of an N-GPU step without its wire time (docs/SCALING.md)")
     p.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                    help="host: gloo-staged collectives so several ranks can share one GPU (logic rehearsal on a "
                         "1-GPU box; not graph-capturable, not a performance path)")
@@ -318,7 +322,8 @@ def make_comm(args, device, world):
     if args.comm == "host":
         return HostStagedComm()
     set_rccl_protocol(args.rccl_proto)
-    return RcclComm(device, channels=args.rccl_channels)
+    return RcclComm(device, channels=args.rccl_channels,
+                    sim_world=args.sim_world if (args.ddp_single and args.sim_world) else None)
 
 
 def build_ddpx(args, device, world, comm=None):
@@ -620,7 +625,8 @@ def calibrate_plan(args, device, world, loader, idx_all, full, comm, rank=0):
     del probe, f
     allow = (args.shard_optimizer is None and any(shadow_only) and args.comm == "rccl" and not cpu) or \
         bool(args.shard_optimizer)
-    plans = candidate_plans(numels, shadow_only, max(world, 2) if args.ddp_single else world, allow_shard=allow,
+    cand_world = (args.sim_world or max(world, 2)) if args.ddp_single else world
+    plans = candidate_plans(numels, shadow_only, cand_world, allow_shard=allow,
                             shapes=None if args.chunk_explicit else shapes)
     if args.shard_optimizer is not None:
         plans = [p for p in plans if p["shard"] == bool(args.shard_optimizer)]
@@ -939,6 +945,7 @@ def main(argv=None):
                    "comm": (args.comm if ddpx_ddp else None),
                    "rccl": ({"channels": args.rccl_channels, "proto": os.environ.get("NCCL_PROTO")}
                             if (ddpx_ddp and args.comm == "rccl") else None),
+                   "sim_world": (args.sim_world if (args.ddp_single and args.sim_world) else None),
                    "graph": bool(runner is not None and runner.use_graph),
                    "graph_steps": (args.graph_steps if (runner is not None and runner.use_graph) else None),
                    "graph_schedule": (runner.schedule(args.steps) if (runner is not None and runner.use_graph)

@@ -219,16 +219,32 @@ class RcclComm(Comm):
     """Native RCCL communicator for one process per MI355X."""
 
     def __init__(self, device: torch.device, timeout_s: float | None = None, high_priority: bool = True,
-                 channels=None):
+                 channels=None, sim_world: int | None = None):
         """``channels``: None (RCCL's choice), N, or (min, max) channel / CTA bounds for THIS communicator
         (``ncclConfig_t.minCTAs/maxCTAs``); default from ``DDPX_RCCL_CHANNELS`` ("N" or "MIN:MAX").  The
-        protocol is process-wide in RCCL: set ``NCCL_PROTO`` (``--rccl_proto``) before the first communicator."""
+        protocol is process-wide in RCCL: set ``NCCL_PROTO`` (``--rccl_proto``) before the first communicator.
+
+        ``sim_world`` (diagnostics, ``bench.py --ddp_single --sim_world N``): a one-process job that PRESENTS world
+        size N, rank 0, to DDP — the N-rank bucket plan, ZeRO-1 shards of 1/N, the deferred gathers and this rank's
+        1/N optimizer stream are built and run exactly as on rank 0 of N ranks — while the communicator itself has
+        one rank: every collective DDP issues is then the in-place identity and is skipped
+        (``DDPX_COMM_SKIP_IDENTITY=1``), so a step times the per-rank compute of an N-GPU job without its wire
+        time.  Not a training mode: the gradients are this rank's own, not averages."""
         if not dist.is_initialized():
             raise RuntimeError("RcclComm bootstraps through the default c10d store: init_process_group first")
         self.channels = parse_channels(os.environ.get("DDPX_RCCL_CHANNELS") if channels is None else channels)
         rt = native.runtime()
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
+        nranks = self.world_size
+        self.sim_world = None
+        if sim_world is not None and int(sim_world) > 1:
+            if self.world_size != 1:
+                raise ValueError("sim_world needs a one-process job")
+            if os.environ.get("DDPX_COMM_SKIP_IDENTITY") != "1":
+                raise ValueError("sim_world needs DDPX_COMM_SKIP_IDENTITY=1 (collectives must not run)")
+            self.sim_world = int(sim_world)
+            self.world_size = self.sim_world
         self.device = torch.device(device)
         self.native = True
         store = dist.distributed_c10d._get_default_store()
@@ -243,7 +259,7 @@ class RcclComm(Comm):
         err = native.ctypes.c_int(0)
         torch.cuda.set_device(self.device)
         lo, hi = self.channels or (0, 0)
-        self.handle = rt.ddpx_comm_create2(uid, self.world_size, self.rank, self.device.index or 0,
+        self.handle = rt.ddpx_comm_create2(uid, nranks, self.rank, self.device.index or 0,
                                            int(high_priority), float(timeout_s), lo, hi, native.ctypes.byref(err))
         if not self.handle:
             raise RuntimeError(f"ncclCommInitRank failed (code {err.value})")

@@ -132,6 +132,18 @@ def test_bench_ddp_job_survives_optional_failures(gpu, tmp_path):
     assert "InjectedFault" in tail["stock_same_run"]["error"] and tail["vs_stock_same_run"] is None
 
 
+def test_bench_sim_world_builds_the_n_rank_layout(gpu, tmp_path):
+    """``--ddp_single --sim_world 4 --shard_optimizer 1``: the 4-rank ZeRO-1 layout (1/4 shards, shadow gathers) on a
+    one-rank communicator with every collective skipped — the per-rank compute table of docs/SCALING.md."""
+    out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3", "--ddp_single",
+                "--sim_world", "4", "--shard_optimizer", "1", "--bucket_plan", "default", "--stock_ref", "0"],
+               tmp_path, extra_env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port())})
+    rec = json.loads([ln for ln in out.splitlines() if ln.startswith('{"metric"')][0])
+    c = rec["config"]
+    assert c["sim_world"] == 4 and c["sharded_optimizer"] is True and c["graph"] is True
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+
+
 def test_bench_contract_one_gpu(gpu, tmp_path):
     out = _run([os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10", "--warmup", "3"], tmp_path)
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
