@@ -58,8 +58,86 @@ __device__ __forceinline__ int wdiv(int n, WDiv f) {
   return f.magic ? (int)(__umulhi((unsigned)n, f.magic) >> f.shift) : n;
 }
 
+// One K-step of the forward's product with LDS reads the compiler does not see (inline asm, settled by explicit
+// lgkmcnt waits that redefine their outputs, as frag_tr/frag_settle in ddpx_pipe.h).  With ordinary C++ loads
+// hipcc (ROCm 7.2) takes the U-slab reads for possible readers of the LDS-DMA just issued for step t + 1 and puts
+// an `s_waitcnt vmcnt(0)` in front of them: every K-step then waited out the whole global->LDS latency of the
+// NEXT stage and the 2-stage ring (the one that fits 3 workgroups per CU) ran as a 1-stage one.  Here the ring's
+// own vmcnt + barrier order reads against DMA; the U pairs are double-buffered (read of pair i + 1 in flight
+// during pair i's four MFMAs) and the patch transform runs while the first U pair is in flight.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#define WINO_RD_D(out, a, o0, o1) \
+  asm volatile("ds_read2st64_b32 %0, %1 offset0:" #o0 " offset1:" #o1 : "=v"(out) : "v"(a) : "memory")
+#define WINO_RD_B(out, a, o0, o1) \
+  asm volatile("ds_read2st64_b64 %0, %1 offset0:" #o0 " offset1:" #o1 : "=v"(out) : "v"(a) : "memory")
+
+// U rows q = 2i, 2i + 1 of this lane's channel: (b[2i].x, b[2i].y, b[2i+1].x, b[2i+1].y); row stride 512 B
+__device__ __forceinline__ void rd_upair(f32x4& o, const LDS_AS char* a, int i) {
+  switch (i) {
+    case 0: WINO_RD_B(o, a, 0, 1); break;
+    case 1: WINO_RD_B(o, a, 2, 3); break;
+    case 2: WINO_RD_B(o, a, 4, 5); break;
+    case 3: WINO_RD_B(o, a, 6, 7); break;
+    case 4: WINO_RD_B(o, a, 8, 9); break;
+    case 5: WINO_RD_B(o, a, 10, 11); break;
+    case 6: WINO_RD_B(o, a, 12, 13); break;
+    default: WINO_RD_B(o, a, 14, 15); break;
+  }
+}
+
+__device__ __forceinline__ void step_asm(const float* dp, const float* bp, f32x4 (&acc)[16][2]) {
+  const LDS_AS char* da = (const LDS_AS char*)(const char*)dp;  // patch pixel q at +256 q B
+  const LDS_AS char* ba = (const LDS_AS char*)(const char*)bp;  // U row q at +512 q B
+  f32x2 dd[8];
+  WINO_RD_D(dd[0], da, 0, 1);
+  WINO_RD_D(dd[1], da, 2, 3);
+  WINO_RD_D(dd[2], da, 4, 5);
+  WINO_RD_D(dd[3], da, 6, 7);
+  WINO_RD_D(dd[4], da, 8, 9);
+  WINO_RD_D(dd[5], da, 10, 11);
+  WINO_RD_D(dd[6], da, 12, 13);
+  WINO_RD_D(dd[7], da, 14, 15);
+  f32x4 bb[2];
+  rd_upair(bb[0], ba, 0);
+  asm volatile("s_waitcnt lgkmcnt(1)"
+               : "+v"(dd[0]), "+v"(dd[1]), "+v"(dd[2]), "+v"(dd[3]), "+v"(dd[4]), "+v"(dd[5]), "+v"(dd[6]),
+                 "+v"(dd[7])::"memory");
+  float tmp[16], v[16];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {  // the same B^T d B as the compiler-read path below
+    const float d0 = dd[c >> 1][c & 1], d1 = dd[(4 + c) >> 1][c & 1];
+    const float d2 = dd[(8 + c) >> 1][c & 1], d3 = dd[(12 + c) >> 1][c & 1];
+    tmp[0 * 4 + c] = d0 - d2;
+    tmp[1 * 4 + c] = d1 + d2;
+    tmp[2 * 4 + c] = d2 - d1;
+    tmp[3 * 4 + c] = d1 - d3;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r * 4 + 0] = tmp[r * 4 + 0] - tmp[r * 4 + 2];
+    v[r * 4 + 1] = tmp[r * 4 + 1] + tmp[r * 4 + 2];
+    v[r * 4 + 2] = tmp[r * 4 + 2] - tmp[r * 4 + 1];
+    v[r * 4 + 3] = tmp[r * 4 + 1] - tmp[r * 4 + 3];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f32x4& b = bb[i & 1];
+    if (i < 7) {
+      rd_upair(bb[(i + 1) & 1], ba, i + 1);
+      asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(b)::"memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b)::"memory");
+    }
+    acc[2 * i][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[2 * i], b.x, acc[2 * i][0], 0, 0, 0);
+    acc[2 * i][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[2 * i], b.y, acc[2 * i][1], 0, 0, 0);
+    acc[2 * i + 1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[2 * i + 1], b.z, acc[2 * i + 1][0], 0, 0, 0);
+    acc[2 * i + 1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[2 * i + 1], b.w, acc[2 * i + 1][1], 0, 0, 0);
+  }
+}
+
 // y (+ stats) = conv3x3(x) through F(2,3).  x: NHWC [N][H][W][C]; U: [16][C][K]; y: [N*H*W][K].
-template <int STAGES, int WAVES_PER_SIMD>
+// ASMRD: K-step reads through step_asm (default); false = compiler-visible LDS loads (DDPX_WINO_STAGES=2c).
+template <int STAGES, int WAVES_PER_SIMD, bool ASMRD = true>
 __global__ void __launch_bounds__(NT, WAVES_PER_SIMD)  // 2: <= 256 VGPR + AGPR (128 are accumulators); 3: <= 168
 wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                 float* __restrict__ stats, const float* __restrict__ bias, int relu, int N, int H, int W, int C, int K,
@@ -93,24 +171,26 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
     }
   }
   // U slab DMA: 8 wave-instructions per K-step, 2 per wave; chunk q = row (xi*4 + ci) * 8 + 16-B column
-  unsigned uoff[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int q = (j * 4 + wave) * 64 + lane;
+  // (instruction j = 1 is 32 rows = 8 xi further: a uniform 8 C K floats past instruction 0's lane offset)
+  unsigned uoff;
+  {
+    const int q = wave * 64 + lane;
     const int row = q >> 3, ch = q & 7;
     const int xi = row >> 2, ci = row & 3;
-    uoff[j] = (unsigned)((((size_t)xi * C + ci) * K + k0 + ch * 4) * 4);
+    uoff = (unsigned)((((size_t)xi * C + ci) * K + k0 + ch * 4) * 4);
   }
+  const unsigned u_j1 = (unsigned)((size_t)8 * C * K * 4);
   const int nk = C >> 2;
   auto issue = [&](int t) {
     char* slot = smem + (t % STAGES) * SLOT;
     const unsigned cx = (unsigned)(t * 16);  // 4 channels = 16 B further along every pixel
     char* raw = slot + wave * (RAW_BYTES / 4);
+    // an out-of-image pixel's kOOB + cx (< 2^31 + 4C) stays past the buffer (x_bytes < 2^31): still reads 0
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(rx, raw + j * 1024, poff[j] == kOOB ? kOOB : poff[j] + cx);
+    for (int j = 0; j < 4; ++j) dma16(rx, raw + j * 1024, poff[j] + cx);
     const unsigned cu = (unsigned)((size_t)t * 4 * K * 4);  // 4 channels = 4 rows of K further
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(ru, slot + RAW_BYTES + (j * 4 + wave) * 1024, uoff[j] + cu);
+    for (int j = 0; j < 2; ++j) dma16(ru, slot + RAW_BYTES + (j * 4 + wave) * 1024, uoff + cu + j * u_j1);
   };
 
   f32x4 acc[16][2];
@@ -133,6 +213,10 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
     const char* slot = smem + (t % STAGES) * SLOT;
     const float* raw = reinterpret_cast<const float*>(slot + wave * (RAW_BYTES / 4));
     const float* us = reinterpret_cast<const float*>(slot + RAW_BYTES);
+    if constexpr (ASMRD) {
+      step_asm(raw + tl * 4 + ci, us + ci * TK + 2 * tl, acc);
+      continue;
+    }
     float d[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) d[q] = raw[(q * 16 + tl) * 4 + ci];
@@ -570,13 +654,17 @@ DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float*
   const int nwg = tiles_p * (K / wino::TK);
   // ring depth (DDPX_WINO_STAGES, default 2): 2 stages = 48 KiB, 3 workgroups per CU (8-10 % faster on every VGG
   // layer, profiles/r5_wino); 3 stages = 72 KiB, 2 per CU
+  // (2c: the 2-stage ring with compiler-visible LDS reads, the round-5 kernel; see step_asm)
   static const int stages = [] {
     const char* e = getenv("DDPX_WINO_STAGES");
-    return e && e[0] == '3' ? 3 : 2;
+    return e && e[0] == '3' ? 3 : (e && e[0] == '2' && e[1] == 'c') ? 1 : 2;
   }();
   if (stages == 2)
     hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
                        H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
+  else if (stages == 1)
+    hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3, false>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias,
+                       relu, N, H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
   else
     hipLaunchKernelGGL((wino::wino_f32_kernel<3, 2>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
                        H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);

@@ -536,7 +536,8 @@ def _vgg_forward(model, x, targets, training):
     N, H, W, C = x.shape
     for bi, (conv, bn, pool) in enumerate(plan.blocks):
         Co = conv.weight.shape[0]
-        if plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co):
+        wino = plan.uf[bi] is not None and H == W and wino_applies(H, W, C, Co)
+        if wino:
             wino_wprep(conv.weight, plan.uf[bi], plan.ud[bi])
             if plan.wd[bi] is not None:  # data gradient on the direct GEMM
                 conv_wprep(conv.weight, plan.wf[bi], plan.wd[bi])
@@ -555,7 +556,7 @@ def _vgg_forward(model, x, targets, training):
             else:
                 y, st = conv_fwd(x, plan.wf[bi], Co), None
         xn, a, b, mean, rstd = bn_forward(y, N, H, W, Co, bn, training, pool, stats=st, comm=comm)
-        saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), pool))
+        saved.append((x, y, a, b, mean, rstd, (N, H, W, C, Co), wino))
         x = xn
         H, W, C = xn.shape[1], xn.shape[2], Co
     feat = avgpool(x)
@@ -578,7 +579,7 @@ def _vgg_backward(model, saved, last, dl, grad_out):
     comm = _sync_comm(model, True)
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, bn, pool = plan.blocks[bi]
-        x, y, a, b, mean, rstd, (N, H, W, C, Co), _ = saved[bi]
+        x, y, a, b, mean, rstd, (N, H, W, C, Co), wino = saved[bi]
         dgam, accg = flat.grad_target(bn.weight)
         dbet, _ = flat.grad_target(bn.bias)
         dy = bn_backward(g, y, a, b, mean, rstd, N, H, W, Co, pool, dgam, dbet, accumulate=accg, comm=comm)
