@@ -408,14 +408,16 @@ static inline int stages(long long ntiles = 0, int num_cus = 256) {
 // Stream waves per workgroup: DDPX_WSGD_STREAM_WAVES=4|8 forces it; by default 8 once every CU owns >= 64
 // tiles (wide MLP, ~150 tiles per CU: 2.108 vs 2.175 ms/step) and 4 below (toy MLP, 14 tiles per CU: pair
 // 115.9 vs 120.4 us; profiles/r3_wsgd).
-// With the MX-FP8 copy (FP8) 4 stream waves stay faster on the wide MLP too (2.052-2.069 vs 2.072-2.082 ms).
+// With the MX-FP8 copy (FP8) too since round 6 (wide MLP --fp8 1, one box: 8 stream waves 2.055 / 2.059 ms with 8 / 4
+// math waves vs 4 stream waves 2.195 / 2.160 ms, profiles/r6_fp8; round 4 had measured 4 faster on the old pair).
 static inline int stream_waves(long long ntiles, int num_cus, bool fp8) {
+  (void)fp8;
   static const int forced = [] {
     const char* e = getenv("DDPX_WSGD_STREAM_WAVES");
     return e && e[0] == '8' ? 8 : (e && e[0] == '4' ? 4 : 0);
   }();
   if (forced) return forced;
-  return (!fp8 && ntiles >= 64LL * num_cus) ? 8 : 4;
+  return ntiles >= 64LL * num_cus ? 8 : 4;
 }
 // Tile order: DDPX_WSGD_ORDER=n (n fastest, default) | m.
 static inline bool n_order() {

@@ -519,7 +519,9 @@ __global__ void __launch_bounds__(256)
 bwd_reduce_kernel(const unsigned short* __restrict__ gout, const unsigned short* __restrict__ y,
                   const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ mean,
                   const float* __restrict__ rstd, int N, int H, int W, int C, int pool, int relu,
-                  float* __restrict__ part) {
+                  float* __restrict__ part, unsigned short* __restrict__ dyw) {
+  // dyw (bias + activation only, no normalisation): the routed, masked gradient gz IS dy and does not depend on
+  // the sums, so this pass also writes it and bwd_apply_kernel's second read of gout and y goes away
   __shared__ float red[2][256 * 8];
   const int G = C / 8;
   const int lanes = 256 / G;  // pixel lanes per block (G <= 64 => >= 4)
@@ -544,6 +546,13 @@ bwd_reduce_kernel(const unsigned short* __restrict__ gout, const unsigned short*
           s1[j] += gz[q][j];
           s2[j] = fmaf(gz[q][j], (f[q][j] - mu[j]) * rs[j], s2[j]);
         }
+      if (dyw) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int hh = 2 * ho + (q >> 1), ww = 2 * wo + (q & 1);
+          *reinterpret_cast<u32x4*>(dyw + (((size_t)n * H + hh) * W + ww) * C + g * 8) = pack8(gz[q]);
+        }
+      }
     }
   } else {
     for (int pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
@@ -556,6 +565,7 @@ bwd_reduce_kernel(const unsigned short* __restrict__ gout, const unsigned short*
         s1[j] += gz[j];
         s2[j] = fmaf(gz[j], (f[j] - mu[j]) * rs[j], s2[j]);
       }
+      if (dyw) *reinterpret_cast<u32x4*>(dyw + (size_t)pix * C + g * 8) = pack8(gz);
     }
   }
 #pragma unroll
@@ -783,7 +793,7 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
   if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
+                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part, nullptr);
   launch_bwd_finalize(part, B, C, N * H * W, c1, c2, dgamma, dbeta, out_bf16, accumulate,
                       SgdArgs{sg_p, sg_buf, nullptr, lr, mom, wd}, SgdArgs{sb_p, sb_buf, nullptr, lr, mom, wd}, s);
   const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
@@ -794,9 +804,9 @@ DDPX_API int ddpx_bn_bwd(const void* gout, const void* y, const float* a, const 
 }
 
 // Backward of  out = [maxpool2](relu(y + bias))  — a 3x3 conv WITH bias followed by ReLU (and pool),
-// no BatchNorm: the reference's DeepNN blocks (/root/reference/singlegpu.py:21-31).  Same two
-// passes as BatchNorm with a = 1, b = bias, mean = 0, rstd = 1: pass 1 yields dbias = sum gz
-// (fixed-order, deterministic), pass 2 writes dy = gz for the conv dgrad / wgrad GEMMs.
+// no BatchNorm: the reference's DeepNN blocks (/root/reference/singlegpu.py:21-31).  BatchNorm's pass 1 with
+// a = 1, b = bias, mean = 0, rstd = 1 yields dbias = sum gz (fixed-order, deterministic) and, as dy = gz needs no
+// sums, writes dy for the conv dgrad / wgrad GEMMs in the same pass (no second read of gout and y).
 // SyncBatchNorm, backward in two halves around an all-reduce of sums[2][C] = (sum dy, sum dy*xhat):
 // ddpx_bn_bwd_sums stores this rank's sums and the LOCAL dgamma / dbeta (DDP averages those, as torch's
 // SyncBatchNorm does); after the all-reduce and a 1/M_global scale, ddpx_bn_bwd_apply forms dy.
@@ -806,7 +816,7 @@ DDPX_API int ddpx_bn_bwd_sums(const void* gout, const void* y, const float* a, c
   if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part);
+                     (const unsigned short*)y, a, b, mean, rstd, N, H, W, C, pool, relu, part, nullptr);
   launch_bwd_finalize(part, B, C, 1, sums, sums + C, dgamma, dbeta, out_bf16, accumulate,
                       SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
                       SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, s);
@@ -861,14 +871,10 @@ DDPX_API int ddpx_bias_act_bwd_sgd(const void* gout, const void* y, const float*
   if (C % 8 || C > 512 || (pool && (H % 2 || W % 2)) || (sb_p && !lr) || (!sb_p && !dbias)) return -1;
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
+                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part, (unsigned short*)dy);
   launch_bwd_finalize(part, B, C, N * H * W, c1, c2, nullptr, dbias, out_bf16, accumulate,
                       SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
                       SgdArgs{sb_p, sb_buf, (unsigned short*)sb_shadow, lr, mom, wd}, s);
-  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
-  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,
-                     (unsigned short*)dy);
   return (int)hipGetLastError();
 }
 
@@ -879,14 +885,10 @@ DDPX_API int ddpx_bias_act_bwd(const void* gout, const void* y, const float* bia
   if (C % 8 || C > 512 || (pool && (H % 2 || W % 2))) return -1;
   const int B = ddpx_bn_bwd_blocks(N, H, W, C);
   hipLaunchKernelGGL(bn::bwd_reduce_kernel, dim3(B), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part);
+                     (const unsigned short*)y, ones, bias, zeros, ones, N, H, W, C, pool, relu, part, (unsigned short*)dy);
   launch_bwd_finalize(part, B, C, N * H * W, c1, c2, nullptr, dbias, out_bf16, accumulate,
                       SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f},
                       SgdArgs{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f}, s);
-  const int n = (pool ? N * (H / 2) * (W / 2) : N * H * W) * (C / 8);
-  hipLaunchKernelGGL(bn::bwd_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const unsigned short*)gout,
-                     (const unsigned short*)y, ones, bias, zeros, ones, c1, c2, N, H, W, C, pool, relu, 0,
-                     (unsigned short*)dy);
   return (int)hipGetLastError();
 }
 
