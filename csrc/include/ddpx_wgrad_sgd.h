@@ -65,7 +65,10 @@ struct Cfg {
 // NMW: math waves, 4 (2 x 2 waves of 32 x 64) or 8 (2 x 4 waves of 32 x 32: two MFMA waves per SIMD, so one wave's
 // fragment reads, DMA issue and barrier wait run under the other's MFMAs — the 4-wave math side ran its K-steps at
 // 11 % MFMA busy with its waves waiting 62 % of their cycles, profiles/r6_pair).
-template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false, int NMW = 4>
+// CP (cache policy of the optimizer stream, measurement: DDPX_WSGD_CACHE): 0 = master / momentum non-temporal loads
+// and stores, shadow plain (default); 1 = everything plain (the 235 MB of toy-MLP master + momentum could stay in the
+// 256 MB Infinity Cache between steps); 2 = the shadow store non-temporal too.
+template <int STAGES, bool FP8, int NSW, bool NORD, int XTRA = 0, bool SB = false, int NMW = 4, int CP = 0>
 __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe::Params p0, pipe::Params p1, int nt1) {
   constexpr int ALD = Cfg<STAGES, XTRA, SB>::ALD, ACC_BYTES = Cfg<STAGES, XTRA, SB>::ACC_BYTES;
   constexpr int LDS_BYTES = Cfg<STAGES, XTRA, SB>::LDS_BYTES;
@@ -267,8 +270,13 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
     auto load_vec = [&](int j, int v, f32x4& pv, f32x4& mv) {
       int sel;
       const size_t off = vec_off(j, v, sel);
-      pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? P1 : P0) + off));
-      mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? M1 : M0) + off));
+      if constexpr (CP == 1) {
+        pv = *reinterpret_cast<const f32x4*>((sel ? P1 : P0) + off);
+        mv = *reinterpret_cast<const f32x4*>((sel ? M1 : M0) + off);
+      } else {
+        pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? P1 : P0) + off));
+        mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>((sel ? M1 : M0) + off));
+      }
     };
     auto grad_vec = [&](const float* T, int v) -> f32x4 {
       return *reinterpret_cast<const f32x4*>(T + (row0 + RSTEP * v) * ALD + col);
@@ -285,9 +293,16 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
         po[q] = fmaf(-lr, d, pv[q]);
         bo[q] = has_mom ? d : po[q];
       }
-      __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>((sel ? P1 : P0) + off));
-      __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>((sel ? M1 : M0) + off));
-      *reinterpret_cast<u32x2*>((sel ? S1 : S0) + off) = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      const u32x2 sh = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
+      if constexpr (CP == 1) {
+        *reinterpret_cast<f32x4*>((sel ? P1 : P0) + off) = po;
+        *reinterpret_cast<f32x4*>((sel ? M1 : M0) + off) = bo;
+      } else {
+        __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>((sel ? P1 : P0) + off));
+        __builtin_nontemporal_store(bo, reinterpret_cast<f32x4*>((sel ? M1 : M0) + off));
+      }
+      if constexpr (CP == 2) __builtin_nontemporal_store(sh, reinterpret_cast<u32x2*>((sel ? S1 : S0) + off));
+      else *reinterpret_cast<u32x2*>((sel ? S1 : S0) + off) = sh;
       if constexpr (FP8) {  // MX-FP8 weight copy for the next forward: 8 lanes = one 32-column block
         unsigned e8;
         const unsigned q = mx::e4m3_group8(po, &e8);
@@ -454,6 +469,15 @@ static inline int math_waves() {
   return v;
 }
 
+// Optimizer-stream cache policy (DDPX_WSGD_CACHE=0|1|2, see the kernel's CP; toy-MLP shapes only).
+static inline int cache_policy() {
+  static const int v = [] {
+    const char* e = getenv("DDPX_WSGD_CACHE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int STAGES, bool FP8>
 static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0, const pipe::Params& p1, int nt1,
                                int nsw) {
@@ -466,6 +490,11 @@ static inline void launch_dist(dim3 grid, hipStream_t s, const pipe::Params& p0,
         if (x == 4) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 4, false, 8>), grid, dim3(768), 0, s, p0, p1, nt1); return; }
       }
       if (x == 0) {
+        if constexpr (!FP8 && STAGES == 3) {
+          const int cp = cache_policy();
+          if (cp == 1) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 0, false, 8, 1>), grid, dim3(768), 0, s, p0, p1, nt1); return; }
+          if (cp == 2) { hipLaunchKernelGGL((wgrad_sgd_ws_kernel<3, false, 4, true, 0, false, 8, 2>), grid, dim3(768), 0, s, p0, p1, nt1); return; }
+        }
         hipLaunchKernelGGL((wgrad_sgd_ws_kernel<STAGES, FP8, 4, true, 0, false, 8>), grid, dim3(768), 0, s, p0, p1, nt1);
         return;
       }
