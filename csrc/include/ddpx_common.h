@@ -70,6 +70,10 @@ struct SgdArgs {
   // that support it (ddpx_mx.h): codes at the element offset, E8M0 scales at element offset / 32.
   unsigned char* q8 = nullptr;
   unsigned char* s8 = nullptr;
+  // the transposed MX-FP8 copy W^T [N][M] with 32-blocks along M (the data gradient's B operand): codes at
+  // n * M + m, scales at n * (M / 32) + m / 32 (ddpx_wgrad_sgd.h, 8 stream waves)
+  unsigned char* q8t = nullptr;
+  unsigned char* s8t = nullptr;
 };
 
 // Master and momentum are read-once / write-once streams: non-temporal, so the update leaves no

@@ -260,6 +260,16 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
     unsigned char* const Q1 = p1.sgd.q8;
     unsigned char* const E0 = p0.sgd.s8;
     unsigned char* const E1 = p1.sgd.s8;
+    // transposed MX copy (FP8, 8 stream waves): each updated vector is staged as fp32 in the gradient tile it
+    // replaced (the thread's own, already consumed slot), and once a 32-row block of the tile is complete (after
+    // the barrier that follows its last vector's update) every stream thread quantises 8 rows of one column:
+    // quad = 32 rows of a column = one MX block along M, its 4 lanes write 32 contiguous code bytes of W^T
+    unsigned char* const QT0 = p0.sgd.q8t;
+    unsigned char* const QT1 = p1.sgd.q8t;
+    unsigned char* const ET0 = p0.sgd.s8t;
+    unsigned char* const ET1 = p1.sgd.s8t;
+    const bool qt_on = FP8 && NSW == 8 && (QT0 != nullptr || QT1 != nullptr);  // (either GEMM may skip its copy)
+    unsigned qt_e0 = 0;  // block 0's E8M0 byte until block 1's: the column's two scales as one 2-byte store
     const int ldc0 = p0.ldc, ldc1 = p1.ldc;
     auto vec_off = [&](int j, int v, int& sel) -> size_t {
       int m0, n0;
@@ -282,7 +292,7 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
       return *reinterpret_cast<const f32x4*>(T + (row0 + RSTEP * v) * ALD + col);
     };
     // update vector v of tile j with gradient g, then refill the slot with the vector DIST ahead
-    auto update_vec_g = [&](int j, int v, const f32x4 g, f32x4& pv, f32x4& mv) {
+    auto update_vec_g = [&](int j, int v, const f32x4 g, f32x4& pv, f32x4& mv, float* stage) {
       int sel;
       const size_t off = vec_off(j, v, sel);
       f32x4 po, bo;
@@ -293,6 +303,7 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
         po[q] = fmaf(-lr, d, pv[q]);
         bo[q] = has_mom ? d : po[q];
       }
+      if (stage) *reinterpret_cast<f32x4*>(stage) = po;
       const u32x2 sh = (u32x2){pack_bf2(po[0], po[1]), pack_bf2(po[2], po[3])};
       if constexpr (CP == 1) {
         *reinterpret_cast<f32x4*>((sel ? P1 : P0) + off) = po;
@@ -321,7 +332,47 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
     };
     // update vector v of tile j from the gradient tile T
     auto update_vec = [&](int j, int v, const float* T, f32x4& pv, f32x4& mv) {
-      update_vec_g(j, v, grad_vec(T, v), pv, mv);
+      if constexpr (FP8 && NSW == 8) {
+        if (qt_on) {  // the updated vector back into its (consumed) gradient slot: the transposed copy's staging
+          float* slot = const_cast<float*>(T) + (row0 + RSTEP * v) * ALD + col;
+          const f32x4 g = *reinterpret_cast<const f32x4*>(slot);
+          update_vec_g(j, v, g, pv, mv, slot);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to the other waves after the next barrier
+          return;
+        }
+      }
+      update_vec_g(j, v, grad_vec(T, v), pv, mv, nullptr);
+    };
+    // quantise rows [32 b, 32 b + 32) of tile j (staged in T) into the transposed copy
+    auto quant_t = [&](int j, int b, const float* T) {
+      int m0, n0;
+      const int sel = tile_origin(j, m0, n0);
+      unsigned char* const qd = sel ? QT1 : QT0;
+      if (!qd) return;  // uniform: this GEMM writes no transposed copy
+      const int c = st >> 2, sub = st & 3;
+      float v[8];
+      float am = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v[r] = bf2f(f2bf(T[(32 * b + 8 * sub + r) * ALD + c]));  // the bf16 copy's value, as the quantiser sees it
+        am = fmaxf(am, fabsf(v[r]));
+      }
+      am = fmaxf(am, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, am), 0xB1, 0xF, 0xF, false)));
+      am = fmaxf(am, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, am), 0x4E, 0xF, 0xF, false)));
+      const int e = mx::block_exp(am, mx::kMaxE4M3);
+      const float inv = ldexpf(1.f, -e);
+      const unsigned lo = mx::quant4(v[0], v[1], v[2], v[3], inv, mx::kMaxE4M3, false);
+      const unsigned hi = mx::quant4(v[4], v[5], v[6], v[7], inv, mx::kMaxE4M3, false);
+      const int Mg = sel ? p1.M : p0.M;
+      *reinterpret_cast<u32x2*>(qd + (size_t)(n0 + c) * Mg + m0 + 32 * b + 8 * sub) = (u32x2){lo, hi};
+      if (sub == 0) {
+        if (b == 0) {
+          qt_e0 = (unsigned)(e + 127);
+        } else {
+          *reinterpret_cast<unsigned short*>((sel ? ET1 : ET0) + (size_t)(n0 + c) * (Mg / 32) + m0 / 32) =
+              (unsigned short)(qt_e0 | ((unsigned)(e + 127) << 8));
+        }
+      }
     };
     // iteration 0 (math fills the first tile): prefetch tile 0's first DIST vectors
 #pragma unroll
@@ -354,6 +405,12 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
           mark();
           __builtin_amdgcn_s_barrier();
         }
+        if constexpr (FP8 && NSW == 8) {  // SV = 4, TPI = 1: rows 0-31 are vectors 0-1, rows 32-63 vectors 2-3
+          if (qt_on && (t + u) % 2 == 1) {
+            quant_t(i - 1, (t + u) / 2, T);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+        }
       }
       if (r % TPI == TPI - 1) {  // end of iteration i: the buffer hand-off barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -375,7 +432,7 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
           __builtin_amdgcn_sched_barrier(0);
           const f32x4 g = gq;
           if (t + u + 1 < SV) gq = grad_vec(accb, t + u + 1);
-          update_vec_g(i - 1, t + u, g, rp[u], rm[u]);
+          update_vec_g(i - 1, t + u, g, rp[u], rm[u], nullptr);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int k = 1; k < KPU; ++k) {
@@ -406,7 +463,8 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
 // are nk + 1 per iteration), ldc % 4 == 0.
 static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
   return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K == 64 * VPT && (p.ldc & 3) == 0 && p.sgd.p &&
-         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && p.sgd.shadow && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3)));
+         p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && p.sgd.shadow && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3))) &&
+         (!p.sgd.q8t || (p.sgd.q8 && p.sgd.s8t && !((uintptr_t)p.sgd.q8t & 7) && !((uintptr_t)p.sgd.s8t & 1)));
 }
 
 // Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:
@@ -567,7 +625,10 @@ static inline hipError_t launch_pair(const pipe::Params& p0, const pipe::Params&
   const int grid = ntiles < num_cus ? ntiles : num_cus;
   if ((p0.sgd.q8 != nullptr) != (p1.sgd.q8 != nullptr)) return hipErrorInvalidValue;  // both or neither
   const bool fp8 = p0.sgd.q8 != nullptr;
-  const int nsw = stream_waves(ntiles, num_cus, fp8);
+  const bool qt = p0.sgd.q8t != nullptr || p1.sgd.q8t != nullptr;
+  if (qt && !fp8) return hipErrorInvalidValue;
+  // the transposed MX copy is emitted by the 8-stream-wave layout only
+  const int nsw = qt ? 8 : stream_waves(ntiles, num_cus, fp8);
   if (stages(ntiles, num_cus) == 4) {
     if (fp8) launch_dist<4, true>(dim3(grid), s, p0, p1, nt1, nsw);
     else launch_dist<4, false>(dim3(grid), s, p0, p1, nt1, nsw);

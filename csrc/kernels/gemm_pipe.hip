@@ -241,24 +241,28 @@ DDPX_API int ddpx_gemm_pipe(const void* A, const void* B, void* C, const float* 
 // Two fused weight-gradient + SGD GEMMs in ONE warp-specialised launch (dW_i = A_i^T-contig x B_i, M_i x N_i,
 // shared K = batch): the toy MLP's fc1 and fc0 updates, independent once fc1's data gradient has run.
 // Returns -20 when the pair is not eligible (the caller then launches them one by one).
-DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0, int lda0, int ldb0, int ldc0,
-                                 float* p0, float* buf0, void* sh0, void* q80, void* s80, const void* A1,
-                                 const void* B1, int M1, int N1, int lda1, int ldb1, int ldc1, float* p1, float* buf1,
-                                 void* sh1, void* q81, void* s81, int K, const float* lr, float mom, float wd,
-                                 hipStream_t stream) {
+// q8t_i / s8t_i (optional, with q8_i; each GEMM may skip its own): the transposed MX-FP8 copy of W_i (W_i^T [N_i][M_i],
+// 32-blocks along M_i: the data gradient's B operand), written by the stream waves too (8 stream waves).
+DDPX_API int ddpx_wgrad_sgd_pair_t(const void* A0, const void* B0, int M0, int N0, int lda0, int ldb0, int ldc0,
+                                   float* p0, float* buf0, void* sh0, void* q80, void* s80, void* q8t0, void* s8t0,
+                                   const void* A1, const void* B1, int M1, int N1, int lda1, int ldb1, int ldc1,
+                                   float* p1, float* buf1, void* sh1, void* q81, void* s81, void* q8t1, void* s8t1,
+                                   int K, const float* lr, float mom, float wd, hipStream_t stream) {
   // q8_i / s8_i (optional): MX-FP8 codes + E8M0 scales of the updated W_i, written by the stream waves
   auto make = [&](const void* A, const void* B, int M, int N, int lda, int ldb, int ldc, float* pp, float* buf,
-                  void* sh, void* q8, void* s8) {
+                  void* sh, void* q8, void* s8, void* q8t, void* s8t) {
     const size_t a_bytes = ((size_t)(K - 1) * lda + M) * 2, b_bytes = ((size_t)(K - 1) * ldb + N) * 2;
     return pipe::Params{(const unsigned short*)A, (const unsigned short*)B, pp, nullptr, nullptr, nullptr,
                         M, N, K, lda, ldb, ldc, 0, pipe::EPI_SGD, 0, 1.f, (unsigned)a_bytes, (unsigned)b_bytes,
-                        SgdArgs{pp, buf, (unsigned short*)sh, lr, mom, wd, (unsigned char*)q8, (unsigned char*)s8},
+                        SgdArgs{pp, buf, (unsigned short*)sh, lr, mom, wd, (unsigned char*)q8, (unsigned char*)s8,
+                                (unsigned char*)q8t, (unsigned char*)s8t},
                         pipe::make_geom(0, 0, 0, 0), 0, 0, 0, nullptr, 0u, nullptr, nullptr, 0, nullptr};
   };
   if (K <= 0 || lda0 % 8 || ldb0 % 8 || lda1 % 8 || ldb1 % 8 || M0 % 8 || N0 % 8 || M1 % 8 || N1 % 8) return -20;
   if (((uintptr_t)A0 | (uintptr_t)B0 | (uintptr_t)A1 | (uintptr_t)B1) & 15) return -20;
-  pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80);
-  const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81);
+  if ((q8t0 || q8t1) && (!q80 || !q81)) return -20;  // the transposed copies ride on the fp8 pair
+  pipe::Params q0 = make(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80, q8t0, s8t0);
+  const pipe::Params q1 = make(A1, B1, M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81, q8t1, s8t1);
   q0.stamp = g_stamp;  // diagnostics: per-role barrier arrival stamps (ddpx_wgrad_sgd.h kStampSlots) / xwg placement
   if ((size_t)q0.a_bytes != ((size_t)(K - 1) * lda0 + M0) * 2 || (size_t)q1.b_bytes != ((size_t)(K - 1) * ldb1 + N1) * 2)
     return -20;  // 32-bit buffer offsets
@@ -276,6 +280,16 @@ DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0,
                                                                   g_xwg_cap, stream) == hipSuccess)
     return 0;
   return (int)wsgd::launch_pair(q0, q1, cus, stream);
+}
+
+DDPX_API int ddpx_wgrad_sgd_pair(const void* A0, const void* B0, int M0, int N0, int lda0, int ldb0, int ldc0,
+                                 float* p0, float* buf0, void* sh0, void* q80, void* s80, const void* A1,
+                                 const void* B1, int M1, int N1, int lda1, int ldb1, int ldc1, float* p1, float* buf1,
+                                 void* sh1, void* q81, void* s81, int K, const float* lr, float mom, float wd,
+                                 hipStream_t stream) {
+  return ddpx_wgrad_sgd_pair_t(A0, B0, M0, N0, lda0, ldb0, ldc0, p0, buf0, sh0, q80, s80, nullptr, nullptr, A1, B1,
+                               M1, N1, lda1, ldb1, ldc1, p1, buf1, sh1, q81, s81, nullptr, nullptr, K, lr, mom, wd,
+                               stream);
 }
 
 // fc1's data gradient folded into the fc1 + fc0 weight-gradient + SGD launch (ddpx_wsgd_dgrad.h):

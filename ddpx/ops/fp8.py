@@ -39,10 +39,11 @@ class MX:
         return v * torch.exp2(e).repeat_interleave(32, dim=1)
 
 
-def quant(x: torch.Tensor, fmt: int = E4M3, rows: bool = True, cols: bool = False, out=None):
+def quant(x: torch.Tensor, fmt: int = E4M3, rows: bool = True, cols: bool = False, out=None, out_t=None):
     """MX-quantise bf16 ``x`` [R, C]: row blocks (for x as a K-contig operand, K = C) and/or the
     transposed operand xᵀ [C, R] with blocks along R.  Returns MX, or (MX, MX_T) if both.
-    ``out`` = (codes uint8 [R, C], scales uint8 [R, C / 32]) contiguous: write the row quantisation there."""
+    ``out`` = (codes uint8 [R, C], scales uint8 [R, C / 32]) contiguous: write the row quantisation there;
+    ``out_t`` = (codes uint8 [C, R], scales uint8 [C, R / 32]): the transposed one."""
     _req(x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1, "x must be 2-D bf16 (GPU)")
     R, C = x.shape
     _req(x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0, "x must be 16-B aligned with ld % 8 == 0")
@@ -58,8 +59,13 @@ def quant(x: torch.Tensor, fmt: int = E4M3, rows: bool = True, cols: bool = Fals
             s = torch.empty((R, C // 32), dtype=torch.uint8, device=x.device)
     if cols:
         _req(R % 32 == 0 and R % 16 == 0, "transposed quantisation needs R % 32 == 0")
-        qt = torch.empty((C, R), dtype=torch.uint8, device=x.device)
-        st = torch.empty((C, R // 32), dtype=torch.uint8, device=x.device)
+        if out_t is not None:
+            qt, st = out_t
+            _req(qt.dtype == torch.uint8 and qt.shape == (C, R) and qt.is_contiguous() and st.dtype == torch.uint8
+                 and st.shape == (C, R // 32) and st.is_contiguous(), "quant out_t: uint8 [C, R] + [C, R/32]")
+        else:
+            qt = torch.empty((C, R), dtype=torch.uint8, device=x.device)
+            st = torch.empty((C, R // 32), dtype=torch.uint8, device=x.device)
     rc = native.kernels().ddpx_mx8_quant(x.data_ptr(), R, C, x.stride(0), native.ptr(q), C, native.ptr(s),
                                          native.ptr(qt), R, native.ptr(st), int(fmt == E5M2), native.stream_handle())
     native.check(rc, f"ddpx_mx8_quant(R={R},C={C})")

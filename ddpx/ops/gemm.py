@@ -254,6 +254,11 @@ native.register_kernel_sig("ddpx_wgrad_sgd_pair", native.c_int, *([native.c_void
                            native.c_int, native.c_void_p, native.c_float, native.c_float, native.c_void_p)
 
 
+native.register_kernel_sig("ddpx_wgrad_sgd_pair_t", native.c_int, *([native.c_void_p, native.c_void_p] + [native.c_int] * 5
+                                                                    + [native.c_void_p] * 7) * 2,
+                           native.c_int, native.c_void_p, native.c_float, native.c_float, native.c_void_p)
+
+
 native.register_kernel_sig("ddpx_wsgd_set_xwg_scratch", None, native.c_void_p, native.c_void_p, native.c_int)
 _XWG = {}
 # DDPX_WSGD_XWG=1: the two-workgroup pair (measurement variant, measured slower: profiles/r6_pair/NOTES.md)
@@ -282,12 +287,14 @@ def xwg_poll_timeouts(dev) -> int:
     return int(cnt[2 * cap].item())
 
 
-def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
+def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None, mxt0=None, mxt1=None) -> bool:
     """Both fused weight-gradient + SGD updates (dW_i = dy_iᵀ x_i applied to sgd_i's parameter) in ONE
     warp-specialised launch.  False (nothing launched) when the pair is not eligible; the caller then
     issues them one by one with :func:`linear_wgrad`.  ``mx_i`` = (codes uint8 [M_i, N_i], E8M0 scales uint8
     [M_i, N_i / 32]): the stream waves also write the updated W_i as MX-FP8 e4m3 (the next forward's
-    operand, ``ddpx.ops.fp8``), bitwise what ``fp8.quant`` of the bf16 copy would give."""
+    operand, ``ddpx.ops.fp8``), bitwise what ``fp8.quant`` of the bf16 copy would give.  ``mxt_i`` (with
+    both ``mx``; either may be None) = (codes uint8 [N_i, M_i], scales uint8 [N_i, M_i / 32]): W_iᵀ with
+    blocks along M_i too (the data gradient's operand), bitwise ``fp8.quant(bf16 copy, rows=False, cols=True)``."""
     for t, n in ((dy0, "dy0"), (x0, "x0"), (dy1, "dy1"), (x1, "x1")):
         _check_bf16_2d(t, n)
     if dy0.shape[0] != dy1.shape[0] or x0.shape[0] != dy0.shape[0] or x1.shape[0] != dy1.shape[0]:
@@ -295,22 +302,31 @@ def wgrad_sgd_pair(dy0, x0, sgd0, dy1, x1, sgd1, mx0=None, mx1=None) -> bool:
     if sgd0[3] is not sgd1[3] or sgd0[4] != sgd1[4] or sgd0[5] != sgd1[5]:
         return False  # lr tensor, momentum, weight decay must be shared
     K = dy0.shape[0]
+    transposed = mxt0 is not None or mxt1 is not None
+    if transposed and (mx0 is None or mx1 is None):
+        return False
     args = []
-    for dy, x, sg, mx in ((dy0, x0, sgd0, mx0), (dy1, x1, sgd1, mx1)):
+    for dy, x, sg, mx, mxt in ((dy0, x0, sgd0, mx0, mxt0), (dy1, x1, sgd1, mx1, mxt1)):
         M, N = dy.shape[1], x.shape[1]
         _req(sg[0].numel() == M * N, "sgd target size mismatch")
         if mx is not None:
             _req(mx[0].dtype == torch.uint8 and mx[0].numel() == M * N and mx[0].is_contiguous()
                  and mx[1].dtype == torch.uint8 and mx[1].numel() == M * N // 32 and N % 32 == 0,
                  "fp8 copy must be uint8 [M, N] codes + [M, N/32] scales")
+        if mxt is not None:
+            _req(mxt[0].dtype == torch.uint8 and tuple(mxt[0].shape) == (N, M) and mxt[0].is_contiguous()
+                 and mxt[1].dtype == torch.uint8 and tuple(mxt[1].shape) == (N, M // 32) and mxt[1].is_contiguous()
+                 and M % 64 == 0, "transposed fp8 copy must be uint8 [N, M] codes + [N, M/32] scales, M % 64 == 0")
         args += [dy.data_ptr(), x.data_ptr(), M, N, dy.stride(0), x.stride(0), N, sg[0].data_ptr(),
                  native.ptr(sg[1]), native.ptr(sg[2]), native.ptr(mx[0] if mx else None),
                  native.ptr(mx[1] if mx else None)]
+        if transposed:
+            args += [native.ptr(mxt[0] if mxt else None), native.ptr(mxt[1] if mxt else None)]
     lr = sg[3]
     if _XWG_ON:
         _xwg_scratch(dy0.device)
-    rc = native.kernels().ddpx_wgrad_sgd_pair(*args, K, lr.data_ptr(), float(sgd0[4]), float(sgd0[5]),
-                                              native.stream_handle())
+    fn = native.kernels().ddpx_wgrad_sgd_pair_t if transposed else native.kernels().ddpx_wgrad_sgd_pair
+    rc = fn(*args, K, lr.data_ptr(), float(sgd0[4]), float(sgd0[5]), native.stream_handle())
     if rc == -20:
         return False
     native.check(rc, "ddpx_wgrad_sgd_pair")

@@ -39,12 +39,13 @@ _FP8_WGRAD = os.environ.get("DDPX_FP8_WGRAD", "0") == "1"
 _FP8_DGRAD = os.environ.get("DDPX_FP8_DGRAD", "0") == "1"
 
 
-def _dgrad_mx8(dpre, w_bf16, h, bias_grad=None, bias_acc=False, bias_sgd=None):
+def _dgrad_mx8(dpre, wq, h, bias_grad=None, bias_acc=False, bias_sgd=None):
     """dX = (dpre W) * (h > 0) on MX-FP8, plus the bias gradient of the layer below (stored / accumulated into
-    ``bias_grad`` or applied through ``bias_sgd``), as G.linear_dgrad's epilogue does on the bf16 pipe."""
+    ``bias_grad`` or applied through ``bias_sgd``), as G.linear_dgrad's epilogue does on the bf16 pipe.
+    ``wq``: Wᵀ [in][out] as MX-FP8 with blocks along out (FlatParams.mx8t_weight: the copy the previous step's
+    wgrad+SGD pair wrote, or the bf16 copy quantised now)."""
     from . import fp8 as F8
     from .elementwise import colsum_bf16, sgd_flat_
-    wq = F8.quant(w_bf16, F8.E4M3, rows=False, cols=True)  # W^T [in][out], blocks along out
     dq = F8.quant(dpre, F8.E4M3)                            # dpre [batch][out], blocks along out
     dx = F8.gemm(dq, wq, epi=G.EPI_RELUMASK_BF16, aux=h)
     if bias_sgd is not None:
@@ -158,6 +159,8 @@ def _backward(model, hs, dl, grad_out, saved8=None):
     bprev = ps[L - 1][1]
     fused = flat.fused_spec(wl) is not None
     fp8_dgrad = _FP8_DGRAD and bool(getattr(model, "fp8", False)) and hs[L].is_cuda
+    if fp8_dgrad and flat.shadow8t is None and not torch.cuda.is_current_stream_capturing():
+        flat.enable_fp8_transposed()
     dpre = torch.empty_like(hs[L])
     if fused:
         # optimizer fused into backward: each kernel that produces a gradient applies the SGD
@@ -177,7 +180,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                 bp = ps[l - 1][1]
                 flat.normalize_pingpong()  # (the unfused update writes the main bf16 copy)
                 if fp8_dgrad:
-                    dnext = _dgrad_mx8(dpre, flat.shadow_of(w), hs[l], bias_sgd=flat.fused_spec(bp))
+                    dnext = _dgrad_mx8(dpre, flat.mx8t_weight(w), hs[l], bias_sgd=flat.fused_spec(bp))
                 else:
                     dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_sgd=flat.fused_spec(bp))
                 flat.mark_updated(bp)
@@ -191,11 +194,14 @@ def _backward(model, hs, dl, grad_out, saved8=None):
                 mx1, mx0 = (flat.mx8_views(w1), flat.mx8_views(w)) if emit else (None, None)
                 if mx1 is None or mx0 is None:  # both copies or neither (a store without 128-aligned offsets)
                     mx1 = mx0 = None
-                paired = G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0, mx1, mx0)
+                # fp8 data gradients: W1's transposed copy for the next step's fc1 dgrad (fc0 has none)
+                mxt1 = flat.mx8t_views(w1) if (fp8_dgrad and mx1 is not None) else None
+                paired = G.wgrad_sgd_pair(d1, h1, s1, dpre, hs[0], s0, mx1, mx0, mxt1, None)
                 if not paired:
                     G.linear_wgrad(d1, h1, None, sgd=s1)
                     _wgrad(saved8, 0, dpre, hs[0], None, sgd=s0)
-                flat.mark_updated(w1, fp8_written=paired and mx1 is not None)
+                flat.mark_updated(w1, fp8_written=paired and mx1 is not None,
+                                  fp8t_written=paired and mxt1 is not None)
                 flat.mark_updated(w, fp8_written=paired and mx0 is not None)
                 dpre = dnext
                 continue
@@ -232,7 +238,7 @@ def _backward(model, hs, dl, grad_out, saved8=None):
             dbl, accl = flat.grad_target(bp)
             # ReLU backward + bias gradient of layer l-1 fused into the dgrad epilogue
             if fp8_dgrad:
-                dnext = _dgrad_mx8(dpre, flat.shadow_of(w), hs[l], bias_grad=dbl, bias_acc=accl)
+                dnext = _dgrad_mx8(dpre, flat.mx8t_weight(w), hs[l], bias_grad=dbl, bias_acc=accl)
             else:
                 dnext = G.linear_dgrad(dpre, flat.shadow_of(w), relu_mask_of=hs[l], bias_grad=dbl,
                                        bias_grad_accumulate=accl)

@@ -114,6 +114,11 @@ class FlatParams:
         self.shadow8 = None
         self.scale8 = None
         self.fp8_fresh = [False] * len(self.params)
+        # optional transposed MX-FP8 copy (enable_fp8_transposed): parameter [M, N] stored as its transpose [N, M]
+        # with 32-blocks along M (the data gradient's operand), written by the fused wgrad+SGD pair
+        self.shadow8t = None
+        self.scale8t = None
+        self.fp8t_fresh = [False] * len(self.params)
         # which optimizer kernels write the fp8 copy next to the bf16 one (DDPX_FP8_COPY): "pair" (default) the
         # fused wgrad+SGD stream (+53-126 us on the wide MLP's pair vs 175 us for quantising both weights
         # separately, profiles/r3_fp8), "1" also the flat SGD (DDP path; not measured faster), "0" none (every
@@ -220,6 +225,37 @@ class FlatParams:
         return (self.shadow8[o:o + n].view(p.shape),
                 self.scale8[o // 32:(o + n) // 32].view(p.shape[0], p.shape[1] // 32))
 
+    def enable_fp8_transposed(self):
+        """Keep the transposed MX-FP8 copy too (fp8 data gradients); stale until an optimizer writes it."""
+        if self.shadow8t is None:
+            self.shadow8t = torch.zeros(self.total, dtype=torch.uint8, device=self.device)
+            self.scale8t = torch.zeros(self.total // 32, dtype=torch.uint8, device=self.device)
+        self.fp8t_fresh = [False] * len(self.params)
+
+    def mx8t_views(self, p):
+        """(codes [cols, rows], scales [cols, rows / 32]) views of p's transposed fp8 copy, or None."""
+        if self.shadow8t is None or p.dim() != 2 or p.shape[0] % 64:
+            return None
+        i = self.index[id(p)]
+        o, n = self.offsets[i], self.numels[i]
+        if o % 128:
+            return None
+        return (self.shadow8t[o:o + n].view(p.shape[1], p.shape[0]),
+                self.scale8t[o // 32:(o + n) // 32].view(p.shape[1], p.shape[0] // 32))
+
+    def mx8t_weight(self, p):
+        """pᵀ as an MX-FP8 operand with blocks along p's rows: the optimizer-written copy when current, else the
+        bf16 copy quantised transposed now (into the store when it keeps one)."""
+        from ..ops import fp8 as F8
+        v = self.mx8t_views(p)
+        if v is None:
+            return F8.quant(self.shadow_of(p), F8.E4M3, rows=False, cols=True)
+        i = self.index[id(p)]
+        if not self.fp8t_fresh[i]:
+            F8.quant(self.shadow_of(p), F8.E4M3, rows=False, cols=True, out_t=v)
+            self.fp8t_fresh[i] = True
+        return F8.MX(v[0], v[1], F8.E4M3)
+
     def mx8_weight(self, p):
         """p's MX-FP8 operand (ddpx.ops.fp8.MX): the optimizer-written copy when current, else the bf16 copy
         quantised now (into the store when it keeps one, so later readers of this step reuse it)."""
@@ -241,6 +277,7 @@ class FlatParams:
                 self.version[i] += 1
                 if self.shadow8 is not None:
                     self.fp8_fresh[i] = bool(written and o >= start and o + n <= end)
+                self.fp8t_fresh[i] = False  # (no flat optimizer writes the transposed copy)
 
     def mx8_range(self, start, end):
         """(codes, scales) slices of the fp8 copy for a flat update of [start, end), or None."""
@@ -255,6 +292,7 @@ class FlatParams:
         For host bookkeeping that ran without its device work, e.g. a HIP-graph capture that aborted after the
         forward had recorded a weight re-layout or quantisation (and marked it current) that never executed."""
         self.fp8_fresh = [False] * len(self.params)
+        self.fp8t_fresh = [False] * len(self.params)
         # every parameter moves past any version a consumer may hold
         self.version = [max(self.version, default=0) + 1] * len(self.params)
 
@@ -324,6 +362,9 @@ class FlatParams:
         if self.shadow8 is not None:
             self.shadow8 = torch.zeros(total, dtype=torch.uint8, device=dev)
             self.scale8 = torch.zeros(total // 32, dtype=torch.uint8, device=dev)
+        if self.shadow8t is not None:
+            self.shadow8t = torch.zeros(total, dtype=torch.uint8, device=dev)
+            self.scale8t = torch.zeros(total // 32, dtype=torch.uint8, device=dev)
         self.state_tensors = states
         self.refresh_shadow()
         self.written = [False] * len(self.params)
@@ -385,12 +426,13 @@ class FlatParams:
     def version_of(self, p) -> int:
         return self.version[self.index[id(p)]]
 
-    def mark_updated(self, p, fp8_written: bool = False):
+    def mark_updated(self, p, fp8_written: bool = False, fp8t_written: bool = False):
         i = self.index[id(p)]
         self.updated[i] = True
         self.written[i] = True
         self.version[i] += 1
         self.fp8_fresh[i] = bool(fp8_written and self.shadow8 is not None)
+        self.fp8t_fresh[i] = bool(fp8t_written and self.shadow8t is not None)
 
     def grad_done(self, p, chunk=None):
         i = self.index[id(p)]

@@ -253,3 +253,85 @@ def test_mlp_fp8_dgrad_step_tracks_bf16(gpu, fused, monkeypatch):
         du, dr = (p - p0).float().flatten(), (q - p0).float().flatten()
         cos = torch.nn.functional.cosine_similarity(du, dr, dim=0).item()
         assert cos > 0.97, (n, cos)
+
+
+@pytest.mark.parametrize("both", [True, False])
+def test_wgrad_sgd_pair_emits_transposed_mx8_copy(gpu, both):
+    """The pair's stream waves also write Wᵀ as MX-FP8 with 32-blocks along W's rows (the fp8 data gradient's
+    operand, 8 stream waves): equal to the quantiser's transposed output for the bf16 copy, and master / momentum /
+    bf16 / row copy unchanged by the extra output (against a launch without it).  ``both=False``: only the first
+    GEMM asks for it (the MLP's fc0 has no data gradient)."""
+    from ddpx.ops import fp8 as F8
+    from ddpx.ops import gemm as G
+    torch.manual_seed(17)
+    K = 512
+    shapes = [(256, 512), (128, 384)]
+    dys = [((torch.rand(K, m, device=gpu) * 2 - 1) * 0.1).to(torch.bfloat16) for m, _ in shapes]
+    xs = [((torch.rand(K, n, device=gpu) * 2 - 1)).to(torch.bfloat16) for _, n in shapes]
+    lr = torch.full((), 0.05, device=gpu)
+    init = [(torch.randn(m * n, device=gpu) * 0.02, torch.randn(m * n, device=gpu) * 0.01) for m, n in shapes]
+
+    def state():
+        return [(p.clone(), b.clone(), torch.empty(p.numel(), dtype=torch.bfloat16, device=gpu)) for p, b in init]
+
+    def mx_rows():
+        return [(torch.empty(m, n, dtype=torch.uint8, device=gpu), torch.empty(m, n // 32, dtype=torch.uint8,
+                                                                               device=gpu)) for m, n in shapes]
+    sa, sb = state(), state()
+    ra, rb = mx_rows(), mx_rows()
+    mxt = [(torch.full((n, m), 0xAB, dtype=torch.uint8, device=gpu),
+            torch.full((n, m // 32), 0xAB, dtype=torch.uint8, device=gpu)) for m, n in shapes]
+    spec = lambda st: [(p, b, s, lr, 0.9, 5e-4) for p, b, s in st]  # noqa: E731
+    a, b = spec(sa), spec(sb)
+    assert G.wgrad_sgd_pair(dys[0], xs[0], a[0], dys[1], xs[1], a[1], ra[0], ra[1], mxt[0], mxt[1] if both else None)
+    assert G.wgrad_sgd_pair(dys[0], xs[0], b[0], dys[1], xs[1], b[1], rb[0], rb[1])
+    torch.cuda.synchronize()
+    for i, ((m, n), (pa, ba, sha), (pb, bb, shb)) in enumerate(zip(shapes, sa, sb)):
+        assert torch.equal(pa, pb) and torch.equal(ba, bb) and torch.equal(sha, shb)
+        assert torch.equal(ra[i][0], rb[i][0]) and torch.equal(ra[i][1], rb[i][1])
+        if i == 1 and not both:
+            assert bool((mxt[1][0] == 0xAB).all()) and bool((mxt[1][1] == 0xAB).all())  # untouched
+            continue
+        ref = F8.quant(sha.view(m, n), F8.E4M3, rows=False, cols=True)
+        assert torch.equal(mxt[i][0], ref.q), i
+        assert torch.equal(mxt[i][1], ref.s), i
+
+
+def test_mlp_fp8_dgrad_reads_pair_written_transposed_copy(gpu, monkeypatch):
+    """DDPX_FP8_DGRAD=1 with the fused optimizer: after the first step the fc1 data gradient's transposed MX operand
+    is the one the previous step's wgrad+SGD pair wrote (no per-step transposed quantisation), and it equals the
+    quantiser's output for the bf16 copy."""
+    import ddpx
+    from ddpx.models import MLP
+    from ddpx.ops import fp8 as F8
+    from ddpx.ops import mlp as mlp_ops
+    from ddpx.optim.sgd import SGD
+    monkeypatch.setattr(mlp_ops, "_FP8_DGRAD", True)
+    torch.manual_seed(6)
+    m = MLP(hidden=512)
+    m.fp8 = True
+    ddpx.prepare_model(m, gpu)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4, capturable=True, fused_backward=True)
+    x = torch.rand(512, 3072, device=gpu).to(torch.bfloat16)
+    t = torch.randint(0, 10, (512,), device=gpu)
+    flat = m.fc0.weight._ddpx_flat
+    orig = F8.quant
+    calls = []
+    for step in range(3):
+        opt.zero_grad()
+        F8.quant = lambda *a, **k: (calls.append(k.get("out_t") is not None), orig(*a, **k))[1]
+        try:
+            loss, _ = m.forward_loss(x, t)
+            loss.backward()
+        finally:
+            F8.quant = orig
+        opt.step()
+        assert sum(calls) == (1 if step == 0 else 0), (step, calls)
+        calls.clear()
+        w1 = m.linears()[1].weight
+        assert flat.fp8t_fresh[flat.index[id(w1)]]
+        q, s = flat.mx8t_views(w1)
+        ref = F8.quant(flat.shadow_of(w1), F8.E4M3, rows=False, cols=True)
+        torch.cuda.synchronize()
+        assert torch.equal(q, ref.q) and torch.equal(s, ref.s), step
+    assert torch.isfinite(loss).item()
