@@ -365,11 +365,12 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
       const unsigned hi = mx::quant4(v[4], v[5], v[6], v[7], inv, mx::kMaxE4M3, false);
       const int Mg = sel ? p1.M : p0.M;
       *reinterpret_cast<u32x2*>(qd + (size_t)(n0 + c) * Mg + m0 + 32 * b + 8 * sub) = (u32x2){lo, hi};
-      if (sub == 0) {
+      unsigned char* const ed = sel ? ET1 : ET0;  // (null: codes only — measurement, benchmarks/pair_fp8t.py)
+      if (sub == 0 && ed) {
         if (b == 0) {
           qt_e0 = (unsigned)(e + 127);
         } else {
-          *reinterpret_cast<unsigned short*>((sel ? ET1 : ET0) + (size_t)(n0 + c) * (Mg / 32) + m0 / 32) =
+          *reinterpret_cast<unsigned short*>(ed + (size_t)(n0 + c) * (Mg / 32) + m0 / 32) =
               (unsigned short)(qt_e0 | ((unsigned)(e + 127) << 8));
         }
       }
@@ -464,7 +465,7 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
 static inline bool eligible(const pipe::Params& p, bool ak, bool bk) {
   return !ak && !bk && p.M % BM == 0 && p.N % BN == 0 && p.K == 64 * VPT && (p.ldc & 3) == 0 && p.sgd.p &&
          p.sgd.lr && (p.sgd.mom == 0.f || p.sgd.buf) && p.sgd.shadow && (!p.sgd.q8 || (p.sgd.s8 && (p.ldc & 127) == 0 && !((uintptr_t)p.sgd.q8 & 3) && !((uintptr_t)p.sgd.s8 & 3))) &&
-         (!p.sgd.q8t || (p.sgd.q8 && p.sgd.s8t && !((uintptr_t)p.sgd.q8t & 7) && !((uintptr_t)p.sgd.s8t & 1)));
+         (!p.sgd.q8t || (p.sgd.q8 && !((uintptr_t)p.sgd.q8t & 7) && !((uintptr_t)p.sgd.s8t & 1)));
 }
 
 // Ring depth: DDPX_WSGD_STAGES=3|4 forces it; by default 4 stages once every CU owns >= 64 tiles (wide MLP:
