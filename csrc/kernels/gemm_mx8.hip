@@ -332,7 +332,18 @@ DDPX_API int ddpx_gemm_mx8(const void* A, const void* sa, const void* B, const v
   mp.sa_bytes = (unsigned)((size_t)M * (K / 32));
   mp.sb_bytes = (unsigned)((size_t)N * (K / 32));
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  if (fa) hipLaunchKernelGGL((mx8::gemm_mx8_kernel<3, 1>), dim3(tiles), dim3(256), 0, stream, mp);
-  else hipLaunchKernelGGL((mx8::gemm_mx8_kernel<3, 0>), dim3(tiles), dim3(256), 0, stream, mp);
+  // ring depth (DDPX_MX8_STAGES=2|3): 2 stages = 66 KiB, two workgroups per CU (default: wide-MLP products 7-24 %
+  // faster than one 3-stage workgroup of 99 KiB per CU, profiles/r6_fp8/fp8_table_s{2,3}.json)
+  static const int stages = [] {
+    const char* e = getenv("DDPX_MX8_STAGES");
+    return e && e[0] == '3' ? 3 : 2;
+  }();
+  if (stages == 2) {
+    if (fa) hipLaunchKernelGGL((mx8::gemm_mx8_kernel<2, 1>), dim3(tiles), dim3(256), 0, stream, mp);
+    else hipLaunchKernelGGL((mx8::gemm_mx8_kernel<2, 0>), dim3(tiles), dim3(256), 0, stream, mp);
+  } else {
+    if (fa) hipLaunchKernelGGL((mx8::gemm_mx8_kernel<3, 1>), dim3(tiles), dim3(256), 0, stream, mp);
+    else hipLaunchKernelGGL((mx8::gemm_mx8_kernel<3, 0>), dim3(tiles), dim3(256), 0, stream, mp);
+  }
   return (int)hipGetLastError();
 }

@@ -49,7 +49,10 @@ namespace pipe {
 static int pick(int M, int N, int K, bool ak, bool bk) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   if (!ak && !bk) return tiles(64, 128) >= 512 ? 5 : 7;      // wgrad-shaped (reduction over batch)
-  if (tiles(128, 128) >= 512 && K >= 2048) return 0;         // wide layers: 128x128 halves L2 traffic
+  // wide layers: 128x128 halves L2 traffic; two 2-stage workgroups per CU beat one 4-stage one on every wide-MLP
+  // product (profiles/r6_gemm/sweep_wide.json, us: fc0 fwd 52.4 vs 82.5, fc1 fwd 298.3 vs 344.7, fc1 dgrad 308.0 vs
+  // 406.4; hipBLASLt 62.1 / 260.7 / 352.0)
+  if (tiles(128, 128) >= 512 && K >= 2048) return 21;
   return 12;  // M=512-row forward / dgrad: 64x64, BK=128 (one barrier per 128 of K), 2 WG/CU
 }
 

@@ -78,6 +78,36 @@ def test_linear_fwd_dgrad_wgrad(gpu):
     assert _rel(db, 2 * dx2.float().sum(0)) < 1e-5
 
 
+def test_linear_wide_default_tile(gpu):
+    """The wide-layer default tile (pick -> 128x128, 2 stages, 4 waves, two workgroups per CU; profiles/r6_gemm
+    sweep_wide.json): forward with bias + ReLU, ReLU-masked data gradient with the in-launch bias-gradient column sums,
+    and the fused bias SGD, against fp32 references."""
+    from ddpx.ops import gemm as G
+    from ddpx.ops.elementwise import sgd_flat_
+    torch.manual_seed(3)
+    M, K, N = 512, 2048, 16384
+    x = _rand_bf16(M, N, dev=gpu)
+    w = _rand_bf16(K, N, dev=gpu) * 0.1
+    b = torch.randn(K, device=gpu)
+    y = G.linear_fwd(x, w.to(torch.bfloat16), b, relu=True)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    assert _rel(y, ref) < 5e-3
+    dy = _rand_bf16(M, K, dev=gpu)
+    db = torch.empty(N, device=gpu)
+    dx = G.linear_dgrad(dy, w.to(torch.bfloat16), relu_mask_of=x, bias_grad=db)
+    refdx = (dy.float() @ w.float()) * (x.float() > 0)
+    assert _rel(dx, refdx) < 5e-3
+    assert _rel(db, dx.float().sum(0)) < 1e-5
+    p0 = torch.randn(N, device=gpu)
+    buf0 = torch.randn(N, device=gpu) * 0.1
+    lr = torch.full((), 0.05, device=gpu)
+    pa, ba = p0.clone(), buf0.clone()
+    G.linear_dgrad(dy, w.to(torch.bfloat16), relu_mask_of=x, bias_sgd=(pa, ba, None, lr, 0.9, 5e-4))
+    pb, bb = p0.clone(), buf0.clone()
+    sgd_flat_(pb, bb, db, None, lr, 0.9, 5e-4)
+    assert torch.allclose(pa, pb, rtol=1e-6, atol=1e-6) and torch.allclose(ba, bb, rtol=1e-6, atol=1e-6)
+
+
 def test_head_fwd_bwd(gpu):
     from ddpx.ops.head import head_backward, head_forward
     torch.manual_seed(2)
