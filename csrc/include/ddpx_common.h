@@ -76,6 +76,20 @@ struct SgdArgs {
   unsigned char* s8t = nullptr;
 };
 
+// sgd_apply with the parameter and momentum already loaded (pv, mv: prefetched by the caller well before the
+// gradient is known, so the update costs no load round trip at the end of a reduction).  Same fma sequence.
+__device__ __forceinline__ float sgd_apply_pre(const SgdArgs& s, size_t i, float g, float lr, float pv, float mv) {
+  float d = fmaf(s.wd, pv, g);
+  if (s.mom != 0.f) {
+    d = fmaf(s.mom, mv, d);
+    __builtin_nontemporal_store(d, s.buf + i);
+  }
+  const float p = fmaf(-lr, d, pv);
+  __builtin_nontemporal_store(p, s.p + i);
+  if (s.shadow) s.shadow[i] = f2bf(p);
+  return p;
+}
+
 // Master and momentum are read-once / write-once streams: non-temporal, so the update leaves no
 // dirty L2 / MALL lines for the next forward's GEMMs to write back (profiles/r1_sgdnt).
 // Returns the updated parameter (for epilogues that also write it in a derived layout).

@@ -248,6 +248,25 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
 #pragma unroll
   for (int c = 0; c < C; ++c) hb[c] = 0.f;
   const bool head_bias = blockIdx.x == 0 && cg == 0;  // one thread per row sums dlogits for the head bias
+  // fused SGD: the threads that finish a column's dW / previous-layer bias (tid < 16 (C + 1)) and the head bias
+  // (block 0, tid < C) load their master / momentum now, under the main loop, not after the reduction
+  float pre_p = 0.f, pre_m = 0.f, preh_p = 0.f, preh_m = 0.f;
+  {
+    const int col = tid % kHeadCols, c = tid / kHeadCols;
+    if (tid < kHeadCols * (C + 1)) {
+      const SgdArgs& sg = c < C ? sW : sP;
+      const size_t idx = c < C ? (size_t)c * K + k0 + col : (size_t)(k0 + col);
+      if (sg.p) {
+        pre_p = __builtin_nontemporal_load(sg.p + idx);
+        if (sg.mom != 0.f) pre_m = __builtin_nontemporal_load(sg.buf + idx);
+      }
+    }
+    if (blockIdx.x == 0 && tid < C && sB.p) {
+      preh_p = __builtin_nontemporal_load(sB.p + tid);
+      if (sB.mom != 0.f) preh_m = __builtin_nontemporal_load(sB.buf + tid);
+    }
+  }
+  const float lr = sW.p ? *sW.lr : 0.f;
   for (int mb = r0; mb < M; mb += RL * RPT) {
     float2 dn[RPT][C / 2];
     u32x4 hn[RPT];
@@ -325,10 +344,9 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
     }
   }
   __syncthreads();
-  const float lr = sW.p ? *sW.lr : 0.f;
-  auto put = [&](const SgdArgs& sg, void* base, size_t idx, float v) {
+  auto put = [&](const SgdArgs& sg, void* base, size_t idx, float v, float pv, float mv) {
     if (sg.p) {  // fused optimizer: update the parameter instead of storing its gradient
-      sgd_apply(sg, idx, v, lr);
+      sgd_apply_pre(sg, idx, v, lr, pv, mv);
     } else if (out_bf16) {
       unsigned short* o = reinterpret_cast<unsigned short*>(base) + idx;
       *o = f2bf(accumulate ? v + bf2f(*o) : v);
@@ -344,16 +362,16 @@ head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_
     for (int ww = 0; ww < NWV; ++ww) s += lds[(ww * kHeadCols + col) * (C + 1) + c];
     const int kk = k0 + col;
     if (c < C) {
-      if (dW || sW.p) put(sW, dW, (size_t)c * K + kk, s);
+      if (dW || sW.p) put(sW, dW, (size_t)c * K + kk, s, pre_p, pre_m);
     } else if (dbprev || sP.p) {
-      put(sP, dbprev, kk, s);
+      put(sP, dbprev, kk, s, pre_p, pre_m);
     }
   }
   if (blockIdx.x == 0 && tid < C && (db || sB.p)) {  // head bias: db[c] = go * sum_m dlogits[m][c]
     float sh = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NWV; ++ww) sh += redh[ww * C + tid];
-    put(sB, db, tid, sh);
+    put(sB, db, tid, sh, preh_p, preh_m);
   }
 }
 
