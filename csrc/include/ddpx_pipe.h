@@ -1099,6 +1099,13 @@ gemm_pipe_kernel(Params p) {
   if (tid >= BN || n0 + tid >= p.N) return;
   const __amdgpu_buffer_rsrc_t rcs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.colsum, 0, (unsigned)((size_t)tiles_m * p.N * 4), 0x00020000);
+  // fused bias SGD: master / momentum / lr loads go out with the partials' (one round trip, not two)
+  float pv = 0.f, mv = 0.f, lrv = 0.f;
+  if (p.sgd.p) {
+    pv = __builtin_nontemporal_load(p.sgd.p + n0 + tid);
+    if (p.sgd.mom != 0.f) mv = __builtin_nontemporal_load(p.sgd.buf + n0 + tid);
+    lrv = *p.sgd.lr;
+  }
   float tot = 0.f;
   for (int t0 = 0; t0 < tiles_m; t0 += 8) {
     float v[8];
@@ -1111,7 +1118,7 @@ gemm_pipe_kernel(Params p) {
   }
   const int n = n0 + tid;
   if (p.sgd.p) {
-    sgd_apply(p.sgd, n, tot, *p.sgd.lr);
+    sgd_apply_pre(p.sgd, n, tot, lrv, pv, mv);
   } else if (p.cs_flags & 1) {
     unsigned short* o = reinterpret_cast<unsigned short*>(p.cs_out) + n;
     *o = f2bf((p.cs_flags & 2) ? tot + bf2f(*o) : tot);

@@ -86,6 +86,14 @@ head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __re
   const int row = m0 + (lane & 15);
   const int cls = lane & 15;
   const int ko = 8 * (lane >> 4);
+  // the LR-table advance at the very end reads counter -> table: both loaded now (by every workgroup: the last one
+  // to arrive is not known yet), so the kernel's tail carries no dependent load round trips for it
+  int lr_k = 0;
+  float lr_next = 0.f;
+  if (lr_counter && loss_mean) {
+    lr_k = *lr_counter;
+    lr_next = lr_table[lr_k < lr_n ? lr_k : lr_n - 1];
+  }
   const bool rok = row < M, cok = cls < C;
   const unsigned short* hp = H + (size_t)(rok ? row : 0) * ldh;
   const unsigned short* wp = W + (size_t)(cok ? cls : 0) * K;
@@ -176,9 +184,8 @@ head_fwd_kernel(const unsigned short* __restrict__ H, const unsigned short* __re
       // the training step's device LR schedule (SGD.device_lr_step): lr = table[step], step += 1.  Every
       // reader of the step counter (the batch gather) ran in an earlier kernel and every reader of lr (the
       // optimizer) runs in a later one, so this single thread saves the step its own 1-thread launch.
-      const int k = *lr_counter;
-      *lr_out = lr_table[k < lr_n ? k : lr_n - 1];
-      *lr_counter = k + 1;
+      *lr_out = lr_next;
+      *lr_counter = lr_k + 1;
     }
   }
 }
