@@ -318,11 +318,12 @@ __global__ void __launch_bounds__(64 * NMW + 64 * NSW) wgrad_sgd_ws_kernel(pipe:
         unsigned e8;
         const unsigned q = mx::e4m3_group8(po, &e8);
         *reinterpret_cast<unsigned*>((sel ? Q1 : Q0) + off) = q;
-        // the row's 4 block scales (lanes 0/8/16/24 of each half-wave) as ONE dword store by the half-wave's
-        // first lane: byte stores scattered over the tile's rows cost more than the codes themselves
-        const unsigned e1 = __shfl_down(e8, 8, 64), e2 = __shfl_down(e8, 16, 64), e3 = __shfl_down(e8, 24, 64);
-        if ((lane & 31) == 0)
-          *reinterpret_cast<unsigned*>((sel ? E1 : E0) + (off >> 5)) = e8 | (e1 << 8) | (e2 << 16) | (e3 << 24);
+        // the row's 4 block scales (lanes 0/8/16/24 of each half-wave) as two 2-byte stores by lanes 0 and 16 of
+        // each half-wave, the neighbouring block's byte fetched by DPP row_ror:8 (plain VALU, no LDS permute on
+        // the stream's per-update path); byte stores scattered over the tile's rows cost more than the codes
+        const unsigned e1 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)e8, 0x128, 0xF, 0xF, false);
+        if ((lane & 15) == 0)
+          *reinterpret_cast<unsigned short*>((sel ? E1 : E0) + (off >> 5)) = (unsigned short)(e8 | (e1 << 8));
       }
       // refill: vector v + DIST of tile j, or vector v + DIST - VPT of tile j + 1, or (past the last tile)
       // vector v of tile j again — a harmless reload that keeps the per-update operation count fixed
