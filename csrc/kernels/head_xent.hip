@@ -218,17 +218,19 @@ __device__ __forceinline__ float half_wave_sum(float v) {
 // then the 8 waves in order through LDS — a fixed order, so the result is bitwise reproducible.
 // Outputs are stored (fp32 / bf16, written or accumulated) or, with SgdArgs.p set, applied as an SGD
 // update: each workgroup reads only its own columns of W, all before it updates them.
-template <int C>
-__global__ void __launch_bounds__(512)
+// NT threads, RPT rows per thread in flight: 256 x 4 (round 6) halves the per-block cross-lane reduction work of
+// 512 x 2 (the 88 column sums' DPP butterflies dominated once the loads were in flight; wide MLP K = 16384: 1024
+// blocks).
+template <int C, int NT = 256, int RPT = 4>
+__global__ void __launch_bounds__(NT)
 head_bwd_kernel(const float* __restrict__ dlogits, const float* __restrict__ go_ptr,
                 const unsigned short* __restrict__ H, const unsigned short* __restrict__ W, int M, int K, int ldh,
                 unsigned short* __restrict__ dH, int relu_mask, float hscale, void* __restrict__ dW,
                 void* __restrict__ db, void* __restrict__ dbprev, int out_bf16, int accumulate, SgdArgs sW,
                 SgdArgs sB, SgdArgs sP) {
-  constexpr int NT = 512, NWV = NT / 64;
+  constexpr int NWV = NT / 64;
   constexpr int TPR = kHeadCols / 8;  // threads per row
-  constexpr int RL = NT / TPR;        // rows per pass (256)
-  constexpr int RPT = 2;              // passes whose loads are in flight together
+  constexpr int RL = NT / TPR;        // rows per pass (NT / 2)
   static_assert(C % 2 == 0, "dlogits rows are read as float2");
   __shared__ float lds[NWV * kHeadCols * (C + 1) + NWV * C];
   float* redh = lds + NWV * kHeadCols * (C + 1);
@@ -449,7 +451,7 @@ DDPX_API int ddpx_head_bwd(const float* dlogits, const float* go, const void* H,
   if (M <= 0) return 0;
   if (C != 10) return -1;
   if (K % kHeadCols || ldh % 8) return -2;
-  hipLaunchKernelGGL(head_bwd_kernel<10>, dim3(K / kHeadCols), dim3(512), 0, s, dlogits, go,
+  hipLaunchKernelGGL((head_bwd_kernel<10, 256, 4>), dim3(K / kHeadCols), dim3(256), 0, s, dlogits, go,
                      (const unsigned short*)H, (const unsigned short*)W, M, K, ldh, (unsigned short*)dH, relu_mask,
                      hscale, dW, db, dbprev, out_bf16, accumulate,
                      SgdArgs{sw_p, sw_buf, (unsigned short*)sw_sh, lr, mom, wd},
