@@ -211,8 +211,9 @@ def setup_dist(args):
         sys.exit(2)
     cpu = args.device == "cpu"
     if not cpu:
-        if args.comm == "host":
-            local = local % torch.cuda.device_count()  # ranks may share a device
+        ndev = torch.cuda.device_count()
+        if args.comm == "host" or (ndev and local >= ndev):
+            local = local % ndev  # ranks may share a device (host-staged comm, or the tests' one-GPU rehearsals)
         torch.cuda.set_device(local)
     # a hung collective is reported per rank after this long (RcclComm watchdog, eager steps and graph replays)
     os.environ.setdefault("DDPX_COMM_TIMEOUT", "300")
@@ -322,8 +323,34 @@ def make_comm(args, device, world):
     if args.comm == "host":
         return HostStagedComm()
     set_rccl_protocol(args.rccl_proto)
-    return RcclComm(device, channels=args.rccl_channels,
-                    sim_world=args.sim_world if (args.ddp_single and args.sim_world) else None)
+    sim = args.sim_world if (args.ddp_single and args.sim_world) else None
+    if world <= 1:
+        return RcclComm(device, channels=args.rccl_channels, sim_world=sim)
+    # N > 1: the native RCCL communicator is created on every rank, and every rank learns (over the gloo group)
+    # whether all of them got one.  If any rank failed, all fall back to the gloo-staged communicator, which is slow
+    # but correct and still yields the job's line (recorded as config.comm "host" + comm_fallback), instead of a
+    # job that dies, or ranks that disagree on the collective they run.
+    import torch.distributed as dist
+    from ddpx.parallel.calibrate import _all_ok
+    from ddpx.utils.faults import maybe_inject
+    comm, err = None, None
+    try:
+        maybe_inject("rccl", "", dist.get_rank())  # tests: a communicator that cannot be created (every rank)
+        comm = RcclComm(device, channels=args.rccl_channels, sim_world=sim)
+    except Exception as e:  # noqa: BLE001 - any failure of the native communicator
+        err = f"{type(e).__name__}: {e}"[:400]
+    if _all_ok(err is None):
+        return comm
+    if comm is not None:
+        try:
+            comm.close(abort=True)
+        except Exception:  # noqa: BLE001
+            pass
+    args.comm = "host"
+    args.comm_fallback = err or "RCCL communicator failed on another rank"
+    print(f"[bench] native RCCL communicator unavailable ({args.comm_fallback}); gloo-staged fallback",
+          file=sys.stderr, flush=True)
+    return HostStagedComm()
 
 
 def build_ddpx(args, device, world, comm=None):
@@ -943,6 +970,7 @@ def main(argv=None):
                    "kernels": (args.kernels if args.impl == "ddpx" else None),
                    "launcher": os.environ.get(LAUNCHER_ENV, "torchrun/external" if world > 1 else "none"),
                    "comm": (args.comm if ddpx_ddp else None),
+                   "comm_fallback": getattr(args, "comm_fallback", None),
                    "rccl": ({"channels": args.rccl_channels, "proto": os.environ.get("NCCL_PROTO")}
                             if (ddpx_ddp and args.comm == "rccl") else None),
                    "sim_world": (args.sim_world if (args.ddp_single and args.sim_world) else None),

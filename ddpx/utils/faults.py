@@ -6,7 +6,9 @@ hook.  ``DDPX_BENCH_INJECT`` is a comma-separated list of ``site[:match][@rankR]
 
 * ``stock`` — the stock recipe raises after building its model (every rank, or rank R);
 * ``calib:zero1`` — every calibration candidate whose name contains ``zero1`` raises in its first training
-  step (every rank, or rank R).
+  step (every rank, or rank R);
+* ``rccl`` — the native RCCL communicator of an N > 1 job cannot be created (every rank: the agreed gloo-staged
+  fallback; a single rank would leave the others inside RCCL's collective init).
 
 Unset (the default) it does nothing.
 """

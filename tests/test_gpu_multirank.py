@@ -178,6 +178,24 @@ def test_bench_self_launched_two_ranks_default_config(gpu):
     assert c["sharded_optimizer"] is False and c["replicas_consistent"] is True
 
 
+def test_bench_two_ranks_rccl_init_failure_falls_back(gpu):
+    """An N > 1 job whose native RCCL communicator cannot be created (injected on every rank) agrees on the
+    gloo-staged communicator and still prints its one JSON line, recording the fallback."""
+    import json
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DDPX_BENCH_INJECT="rccl")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+           "--hidden", "1024", "--stock_ref", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    c = json.loads(lines[0])["config"]
+    assert c["comm"] == "host" and "InjectedFault" in (c["comm_fallback"] or ""), c
+    assert c["replicas_consistent"] is True
+
+
 def _syncbn_worker(rank, ws, port, mode, errq):
     """Native VGG with SyncBatchNorm on 2 ranks (half batch each) == one process on the full batch.
     mode "dup": both ranks hold the same half (SyncBN == local BN);  "nosync": plain BN, reference = the
