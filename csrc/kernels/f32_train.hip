@@ -1178,7 +1178,10 @@ __global__ void __launch_bounds__(256) bn_bwd_sums4_kernel(const float* __restri
                                                             const float* __restrict__ a, const float* __restrict__ b,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int N, int H, int W, int C,
-                                                            int pool, int R, float* __restrict__ part) {
+                                                            int pool, int R, float* __restrict__ part,
+                                                            float* __restrict__ dyw) {
+  // dyw (bias + activation only: a = 1, mean = 0, rstd = 1, c1 = c2 = 0): dy = gz needs no sums, so this pass writes
+  // it too and bn_bwd_apply4_kernel's second read of g and y goes away (DeepNN fp32's pooled blocks)
   __shared__ f32x4 red[2][256];
   const int tid = threadIdx.x, C4 = C / 4, cq = tid % C4, gi = tid / C4, G = 256 / C4;
   const int c = 4 * cq;
@@ -1199,6 +1202,15 @@ __global__ void __launch_bounds__(256) bn_bwd_sums4_kernel(const float* __restri
         s1[e] += w.gz[q][e];
         s2[e] = fmaf(w.gz[q][e], w.xh[q][e], s2[e]);
       }
+    if (dyw) {
+      const int nq = pool ? 4 : 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q >= nq) break;
+        const size_t pp = pix0 + (size_t)(q >> 1) * W + (q & 1);
+        *reinterpret_cast<f32x4*>(dyw + pp * C + c) = (f32x4){w.gz[q][0], w.gz[q][1], w.gz[q][2], w.gz[q][3]};
+      }
+    }
   }
   red[0][tid] = s1;
   red[1][tid] = s2;
@@ -1719,13 +1731,28 @@ DDPX_API int ddpx_f32_bn_bwd_sums(const float* g, const float* y, const float* a
   if (pool && (H % 2 || W % 2)) return -1;
   if (bn_vec_ok(C, W, pool, R)) {
     hipLaunchKernelGGL(bn_bwd_sums4_kernel, dim3(nblk((long)N * H * W, R)), dim3(256), 0, s, g, y, a, b, mean, rstd,
-                       N, H, W, C, pool, R, part);
+                       N, H, W, C, pool, R, part, (float*)nullptr);
     return (int)hipGetLastError();
   }
   if (C > 512 || (256 % C && C % 256)) return -1;
   hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nblk((long)N * H * W, R)), dim3(bn_threads(C)), 0, s, g, y, a, b, mean,
                      rstd, N, H, W, C, pool, R, part);
   return (int)hipGetLastError();
+}
+
+// Bias + activation backward (a = 1, b = 0, mean = 0, rstd = 1): the sums pass also writes dy = gz.  Returns 1
+// when it did (the caller skips ddpx_f32_bn_bwd_apply), 0 when only the sums were written (no 4-channel path).
+DDPX_API int ddpx_f32_bias_act_bwd_sums(const float* g, const float* y, const float* one, const float* zero, int N,
+                                        int H, int W, int C, int pool, int R, float* part, float* dy, hipStream_t s) {
+  if (pool && (H % 2 || W % 2)) return -1;
+  if (bn_vec_ok(C, W, pool, R)) {
+    hipLaunchKernelGGL(bn_bwd_sums4_kernel, dim3(nblk((long)N * H * W, R)), dim3(256), 0, s, g, y, one, zero, zero,
+                       one, N, H, W, C, pool, R, part, dy);
+    const int e = (int)hipGetLastError();
+    return e ? -e : 1;
+  }
+  const int e = ddpx_f32_bn_bwd_sums(g, y, one, zero, zero, one, N, H, W, C, pool, R, part, s);
+  return e ? (e < 0 ? e : -e) : 0;
 }
 
 DDPX_API int ddpx_f32_bn_bwd_finalize(const float* part, int T, int P, int C, float* c1, float* c2, float* dgamma,

@@ -30,6 +30,7 @@ for _sig in (
         ("ddpx_f32_bn_finalize", _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _I, _P, _P, _P, _P, _P, _P),
         ("ddpx_f32_bn_apply", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_bn_bwd_sums", _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P),
+        ("ddpx_f32_bias_act_bwd_sums", _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_bn_bwd_finalize", _I, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P),
         ("ddpx_f32_bn_bwd_apply", _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P),
         ("ddpx_f32_avgpool", _I, _P, _I, _I, _I, _P, _I, _P),
@@ -679,14 +680,19 @@ def bias_act_backward(g, y, N, H, W, C, pool, plan, dbias, accumulate=False):
     T = (P + R - 1) // R
     one, zero = plan.ones[:C], plan.zeros[:C]
     part = torch.empty((T, 2, C), dtype=torch.float32, device=y.device)
-    _call("ddpx_f32_bn_bwd_sums", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
-          one.data_ptr(), N, H, W, C, int(pool), R, part.data_ptr())
+    dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
+    # the sums pass writes dy = gz too where the 4-channel path applies (no sums needed for it: no normalisation)
+    wrote = native.kernels().ddpx_f32_bias_act_bwd_sums(g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(),
+                                                        N, H, W, C, int(pool), R, part.data_ptr(), dy.data_ptr(),
+                                                        native.stream_handle())
+    if wrote < 0:
+        native.check(wrote, "ddpx_f32_bias_act_bwd_sums")
     c1, c2 = plan.scratch[:C], plan.scratch[C:2 * C]
     _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), None, dbias.data_ptr(),
           int(accumulate), native.ptr(_fin_ws(T, C, y.device)))
-    dy = torch.empty((P, C), dtype=torch.float32, device=y.device)
-    _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
-          one.data_ptr(), zero.data_ptr(), zero.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
+    if wrote != 1:
+        _call("ddpx_f32_bn_bwd_apply", g.data_ptr(), y.data_ptr(), one.data_ptr(), zero.data_ptr(), zero.data_ptr(),
+              one.data_ptr(), zero.data_ptr(), zero.data_ptr(), N, H, W, C, int(pool), dy.data_ptr())
     return dy
 
 
