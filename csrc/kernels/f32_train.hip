@@ -92,7 +92,7 @@ struct Stage {
   }
 };
 
-enum Flags { F_RELU = 1, F_ACCUM = 2, F_SPLIT = 4 };
+enum Flags { F_RELU = 1, F_ACCUM = 2, F_SPLIT = 4, F_VEC = 8 };  // F_VEC: LDS-DMA core's 16-B store epilogue
 
 // C[m][n] (+)= sum_k A(m,k) B(k,n)  [+ bias[n]] [relu] [* (mask[m][n] > 0)]; F_SPLIT: the K range of
 // blockIdx's split z goes to the raw slab C + z * split_stride.
@@ -475,6 +475,64 @@ gemm_f32_dma_kernel(const Operand A, const Operand B, int M, int N, int K, int k
     }
     return;
   }
+  if (flags & F_VEC) {
+    // Output tile staged through the idle LDS ring in row parts, then stored as 16-B row vectors (a 128-wide tile
+    // row is 512 contiguous bytes).  The fragment-order stores below write 4-B lanes in 64-B row pieces: DeepNN's
+    // first conv (K = 36, 256 MB of output) ran 171 us, store-bound, on them (profiles/r6_deepnn).  Same values,
+    // same epilogue order (bias, accumulate, ReLU, mask) — bitwise the scalar form.
+    constexpr int TLD = BN + 4;
+    constexpr int EH = (BM * TLD * 4 <= STAGES * SLOT) ? 1 : 2;
+    constexpr int BMH = BM / EH;
+    static_assert(BMH * TLD * 4 <= STAGES * SLOT, "epilogue staging does not fit the ring");
+    constexpr int Q = BN / 4, RSTEP = NT / Q, NV = BMH / RSTEP;
+    float* T = reinterpret_cast<float*>(smem);
+    const int cq = tid % Q, r0 = tid / Q;
+    const int col = n0 + 4 * cq;
+    const bool epi = !(flags & F_SPLIT);
+    f32x4 bv = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (epi && bias && col < N) bv = *reinterpret_cast<const f32x4*>(bias + col);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < EH; ++h) {
+      __syncthreads();  // the ring / the statistics scratch (h = 0), the previous part's reads (h = 1) are done
+      if (wm == h || EH == 1) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = (EH == 1 ? wm * (BM / 2) : 0) + i * 16 + lr * 4 + e;
+              T[r * TLD + wn * (BN / 2) + j * 16 + lc] = acc[i][j][e];
+            }
+      }
+      __syncthreads();
+      const int mh = m0 + h * BMH;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int r = r0 + i * RSTEP;
+        const int row = mh + r;
+        if (row >= M || col >= N) continue;
+        const size_t o = (size_t)row * ldc + col;
+        f32x4 v = *reinterpret_cast<const f32x4*>(T + r * TLD + 4 * cq);
+        if (epi) {
+          const f32x4 prev = (flags & F_ACCUM) ? *reinterpret_cast<const f32x4*>(out + o) : bv;
+          const f32x4 mk = mask ? *reinterpret_cast<const f32x4*>(mask + o) : (f32x4){1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float x = v[q];
+            if (bias) x += bv[q];
+            if (flags & F_ACCUM) x += prev[q];
+            if (flags & F_RELU) x = fmaxf(x, 0.f);
+            if (!(mk[q] > 0.f)) x = 0.f;
+            v[q] = x;
+          }
+        }
+        *reinterpret_cast<f32x4*>(out + o) = v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -521,6 +579,15 @@ static bool f32_dma() {
   return g_f32_staging == 1;
 }
 constexpr int kF32Stages = 4;
+// Output stores of the LDS-DMA core: 16-B row vectors staged through LDS (default) or the fragment-order 4-B
+// stores (DDPX_F32_EPI=scalar; A/B).  Bitwise the same results.
+static bool f32_vec_epi() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_F32_EPI");
+    return !(e && e[0] == 's');
+  }();
+  return v;
+}
 // Summation block of the LDS-DMA core's blocked mode, in 16-k K-steps (DDPX_F32_BLOCK=1|2|4, default 4): a fresh
 // block accumulator per 64 k, added to the running sum.  Measured on MI355X (profiles/r4_f32): the rounding
 // error of a length-K dot product is smallest near blocks of sqrt(K) (~64 at VGG's K = 2304-4608: conv7 / conv4
@@ -548,6 +615,9 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
   const bool conv = AM == IM2COL_KC || BMD == IM2COL_OC;
   const bool plain = mode == 1 || (mode == 0 && !conv);
   if (f32_dma() && a_bytes && b_bytes) {
+    const auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (f32_vec_epi() && N % 4 == 0 && ldc % 4 == 0 && split_stride % 4 == 0 && al16(C) && al16(bias) && al16(mask))
+      flags |= F_VEC;
     if (plain)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
                          N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
