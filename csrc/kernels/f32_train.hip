@@ -569,6 +569,15 @@ static int f32_sum_mode() {  // 0 auto, 1 plain, 2 blocked
   return v;
 }
 
+// 3-slot ring for im2col GEMMs with K <= 48 (DDPX_F32_SMALLK=0 disables; A/B).  Same summation: bitwise equal.
+static bool f32_small_k_ring() {
+  static const bool v = [] {
+    const char* e = getenv("DDPX_F32_SMALLK");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // Operand staging: DDPX_F32_STAGING=dma (LDS-DMA ring, default) | reg (register-staged, double-buffered LDS).
 static int g_f32_staging = -1;  // -1: from the environment; ddpx_f32_set_staging() overrides (tests, A/B)
 static bool f32_dma() {
@@ -618,6 +627,15 @@ static void launch(const Operand& A, const Operand& B, int M, int N, int K, int 
     const auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (f32_vec_epi() && N % 4 == 0 && ldc % 4 == 0 && split_stride % 4 == 0 && al16(C) && al16(bias) && al16(mask))
       flags |= F_VEC;
+    if constexpr (AM == IM2COL_KC) {
+      // the image's first convolution (K = 36: 3 K-steps): a 3-slot ring holds the whole K range, and the smaller
+      // LDS footprint (48 KB at 128x128, not 64) fits 3 workgroups per CU instead of 2
+      if (!plain && kchunk <= 3 * BK && f32_block() == 4 && f32_small_k_ring()) {
+        hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, false, 3, 4>), dim3(nwg), dim3(NT), 0, s, A, B, M, N,
+                           K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
+        return;
+      }
+    }
     if (plain)
       hipLaunchKernelGGL((gemm_f32_dma_kernel<BM, BN, AM, BMD, true, kF32Stages>), dim3(nwg), dim3(NT), 0, s, A, B, M,
                          N, K, kchunk, C, ldc, split_stride, bias, mask, flags, tm, tn, a_bytes, b_bytes, stats, sgd);
@@ -1669,7 +1687,12 @@ DDPX_API int ddpx_f32_gemm(int amode, const float* a, int lda, int bmode, const 
   if (splits > 1) flags |= F_SPLIT;
   Operand A{a, lda, M, lc, lh, lw, sgn}, B{b, ldb, N, lc, lh, lw, sgn};
   const unsigned ab = operand_bytes(amode, lda, M, K, gc, M), bb = operand_bytes(bmode, ldb, N, K, gc, K);
-  if (tile < 0) tile = auto_tile(M, N, splits);
+  if (tile < 0) {
+    tile = auto_tile(M, N, splits);
+    // first convolution (K <= 48, 3-slot ring): 128x64 tiles, 105 vs 128 us at 3 -> 128 channels, batch 512
+    // (benchmarks/f32_first_conv_probe.py, profiles/r6_f32epi)
+    if (amode == IM2COL_KC && K <= 3 * BK && splits == 1 && tile == 0) tile = 1;
+  }
   const int key = amode * 4 + bmode;
   switch (key) {
     case DENSE_KC * 4 + DENSE_KC:
