@@ -708,6 +708,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   const float* p = part + (size_t)co * 9 * Cp + rs * Cp + ci;
   float acc = 0.f;
   int z = 0;
+  // 32 slabs' loads in flight: the first conv (3 input channels: 14 workgroups, 512 slabs) was latency-bound at
+  // 8 (28 us in the DeepNN fp32 step); same adds in the same order
+  for (; z + 32 <= S; z += 32) {
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = p[(size_t)(z + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) acc += v[u];
+  }
   for (; z + 8 <= S; z += 8) {
     float v[8];
 #pragma unroll
