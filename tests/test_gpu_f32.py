@@ -660,6 +660,28 @@ def test_wino_wgrad_matches_fp64(gpu, shape):
     assert err < max(2 * e_direct, 2e-6), (err, e_direct)
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_wgrad_32_channels_padded_winograd(gpu, accumulate):
+    """conv_wgrad of a 32-output-channel layer (DeepNN's 64 -> 32 at 16x16) runs the Winograd weight gradient over
+    dy zero-padded to 64 channels: fp64 agreement, only the first 32 rows written, accumulate adds."""
+    from ddpx.ops import f32
+    torch.manual_seed(7)
+    N, H, Ci, Co = 4, 16, 64, 32
+    assert not f32.wino_wgrad_applies(H, H, Ci, Co) and f32.wino_wgrad_applies(H, H, Ci, 64)
+    x = torch.randn(N, Ci, H, H, device=gpu)
+    w = torch.randn(Co, Ci, 3, 3, device=gpu) / (Ci * 9) ** 0.5
+    dy = torch.randn(N, H, H, Co, device=gpu)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    wr = w.double().requires_grad_(True)
+    F.conv2d(x.double(), wr, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+    buf = torch.full((Co * Ci * 9 + 64,), 0.25, device=gpu)  # guard words after the gradient
+    out = buf[:Co * Ci * 9].view(Co, Ci, 3, 3)
+    f32.conv_wgrad(dy.reshape(-1, Co), xn, Co, Ci, out, accumulate=accumulate)
+    got = out - 0.25 if accumulate else out
+    assert _err_vs_fp64(got, wr.grad)["rel_l2"] < 1e-5
+    assert torch.all(buf[Co * Ci * 9:] == 0.25)
+
+
 def test_vgg_fp32_runs_winograd_layers(gpu):
     """The fp32 VGG plan puts every layer with >= 64 input channels on Winograd (forward + data gradient)."""
     import ddpx
