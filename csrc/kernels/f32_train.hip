@@ -1586,6 +1586,38 @@ __global__ void __launch_bounds__(256) head_dgrad4_kernel(const float* __restric
 }
 
 // out[n] (+)= sum_m x[m][n]: workgroups of 64 columns x 16 row groups, fixed-order LDS reduction
+// part[t][0][c] = sum of x[r][c] over chunk t's R rows, part[t][1][c] = 0 (the [T][2][C] layout
+// ddpx_f32_bn_bwd_finalize merges in fixed order): the bias gradient of a conv + ReLU block whose data gradient
+// was masked by the producing GEMM.  C / 4 lanes per row (16-B loads), 256 / (C / 4) rows in parallel, their
+// partial sums combined in row-lane order (deterministic).
+__global__ void __launch_bounds__(256) colsum_part_kernel(const float* __restrict__ x, int P, int C, int R,
+                                                          float* __restrict__ part) {
+  __shared__ f32x4 red[256];
+  const int Q = C / 4, RP = 256 / Q;
+  const int q = threadIdx.x % Q, rl = threadIdx.x / Q;
+  const int r0 = blockIdx.x * R, r1 = min(P, r0 + R);
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (rl < RP) {
+    int r = r0 + rl;
+    for (; r + 3 * RP < r1; r += 4 * RP) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(x + (size_t)(r + u * RP) * C + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    for (; r < r1; r += RP) acc += *reinterpret_cast<const f32x4*>(x + (size_t)r * C + 4 * q);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < Q) {
+    f32x4 t = red[threadIdx.x];
+    for (int j = 1; j < RP; ++j) t += red[j * Q + threadIdx.x];
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * 2 * C + 4 * threadIdx.x) = t;
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * 2 * C + C + 4 * threadIdx.x) = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ x, int M, int N,
                                                        float* __restrict__ out, int accumulate) {
   __shared__ float red[16][64];
@@ -1925,6 +1957,12 @@ DDPX_API int ddpx_f32_head_bwd(const float* dl, const float* go, const float* h,
   else if (dh)
     hipLaunchKernelGGL(head_dgrad_kernel, dim3(nblk((long)M * K)), dim3(256), 0, s, dl, go, w, h, M, K, NC,
                        relu_mask, dh_scale, dh);
+  return (int)hipGetLastError();
+}
+
+DDPX_API int ddpx_f32_colsum_part(const float* x, int P, int C, int R, float* part, hipStream_t s) {
+  if (C % 4 || C > 1024 || R < 1 || ((uintptr_t)x & 15) || ((uintptr_t)part & 15)) return -1;
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((P + R - 1) / R), dim3(256), 0, s, x, P, C, R, part);
   return (int)hipGetLastError();
 }
 

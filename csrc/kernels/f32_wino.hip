@@ -141,7 +141,7 @@ template <int STAGES, int WAVES_PER_SIMD, bool ASMRD = true>
 __global__ void __launch_bounds__(NT, WAVES_PER_SIMD)  // 2: <= 256 VGPR + AGPR (128 are accumulators); 3: <= 168
 wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                 float* __restrict__ stats, const float* __restrict__ bias, int relu, int N, int H, int W, int C, int K,
-                int tiles_p, unsigned x_bytes, unsigned u_bytes) {
+                int tiles_p, unsigned x_bytes, unsigned u_bytes, const float* __restrict__ mask) {
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -297,7 +297,13 @@ wino_f32_kernel(const float* __restrict__ x, const float* __restrict__ U, float*
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const size_t pix = ((size_t)n * H + 2 * th + i) * W + 2 * tw + jj;
-        *reinterpret_cast<float2*>(y + pix * K + k0 + 2 * tl) = make_float2(out[e][0][i * 2 + jj], out[e][1][i * 2 + jj]);
+        float2 v = make_float2(out[e][0][i * 2 + jj], out[e][1][i * 2 + jj]);
+        if (mask) {  // data gradient through the ReLU below: zero where that layer's output mask[pix] <= 0
+          const float2 mk = *reinterpret_cast<const float2*>(mask + pix * K + k0 + 2 * tl);
+          if (!(mk.x > 0.f)) v.x = 0.f;
+          if (!(mk.y > 0.f)) v.y = 0.f;
+        }
+        *reinterpret_cast<float2*>(y + pix * K + k0 + 2 * tl) = v;
       }
   }
   if (!stats) return;
@@ -653,8 +659,9 @@ DDPX_API int ddpx_f32_wino_wprep(const float* w, int Co, int Ci, int Cp, float* 
 
 // y [N*H*W][K] = conv3x3(x [N][H][W][C]) with U [16][C][K] [+ bias[K]] [relu]; stats (nullable): [tiles_p][2][K]
 // chunk statistics of 256-pixel chunks.  Returns the statistics chunk rows (256) or a negative error.
-DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float* stats, const float* bias, int relu,
-                                int N, int H, int W, int C, int K, hipStream_t s) {
+// mask (nullable, [N*H*W][K]): y is zeroed where mask <= 0 (the data gradient of a conv + ReLU block below)
+DDPX_API int ddpx_f32_wino_conv_mask(const float* x, const float* U, float* y, float* stats, const float* bias,
+                                     int relu, const float* mask, int N, int H, int W, int C, int K, hipStream_t s) {
   if (!ddpx_f32_wino_ok(H, W, C, K)) return -2;
   const size_t xb = (size_t)N * H * W * C * 4, ub = (size_t)16 * C * K * 4;
   if (xb >= 0x80000000ull || ub >= 0x80000000ull) return -3;  // 32-bit buffer offsets, top bit = out of bounds
@@ -670,15 +677,20 @@ DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float*
   }();
   if (stages == 2)
     hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
-                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
+                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub, mask);
   else if (stages == 1)
     hipLaunchKernelGGL((wino::wino_f32_kernel<2, 3, false>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias,
-                       relu, N, H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
+                       relu, N, H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub, mask);
   else
     hipLaunchKernelGGL((wino::wino_f32_kernel<3, 2>), dim3(nwg), dim3(wino::NT), 0, s, x, U, y, stats, bias, relu, N,
-                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub);
+                       H, W, C, K, tiles_p, (unsigned)xb, (unsigned)ub, mask);
   const int e = (int)hipGetLastError();
   return e ? -e : 4 * wino::TP;
+}
+
+DDPX_API int ddpx_f32_wino_conv(const float* x, const float* U, float* y, float* stats, const float* bias, int relu,
+                                int N, int H, int W, int C, int K, hipStream_t s) {
+  return ddpx_f32_wino_conv_mask(x, U, y, stats, bias, relu, nullptr, N, H, W, C, K, s);
 }
 
 // Winograd weight gradient applies: 3x3 / s1 / p1, H and W even, Cp % 32 == 0, Co % 64 == 0.

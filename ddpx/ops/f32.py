@@ -45,6 +45,8 @@ for _sig in (
         ("ddpx_f32_wgrad_sgd", _I, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P),
         ("ddpx_f32_splitk_epi", _I, _P, _I, _I, _I, _P, _P, _P, _I, _P),
         ("ddpx_f32_wino_ok", _I, _I, _I, _I, _I),
+        ("ddpx_f32_wino_conv_mask", _I, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P),
+        ("ddpx_f32_colsum_part", _I, _P, _I, _I, _I, _P, _P),
         ("ddpx_f32_wino_wprep", _I, _P, _I, _I, _I, _P, _P, _P),
         ("ddpx_f32_wino_conv", _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P),
         ("ddpx_f32_wino_wgrad_ok", _I, _I, _I, _I, _I),
@@ -302,16 +304,21 @@ def wino_wprep(w, uf, ud):
     _call("ddpx_f32_wino_wprep", w.data_ptr(), Co, Ci, Cp, native.ptr(uf), native.ptr(ud))
 
 
-def wino_conv(x, u, K, stats=False, bias=None, relu=False):
+def wino_conv(x, u, K, stats=False, bias=None, relu=False, mask=None):
     """y [N*H*W, K] = [relu](conv3x3(x [N,H,W,C]) [+ bias]) through F(2,3) with u [16][C][K]; with ``stats``:
-    (y, (part, T, 256)), the BatchNorm chunk statistics of every 256-pixel output chunk from the epilogue."""
+    (y, (part, T, 256)), the BatchNorm chunk statistics of every 256-pixel output chunk from the epilogue.
+    ``mask`` [N*H*W, K] (a data gradient through the ReLU of the block below): y = 0 where mask <= 0."""
     N, H, W, C = x.shape
     _f32(x, "x")
+    if mask is not None:
+        _f32(mask, "mask")
+        _req(mask.numel() == N * H * W * K, "wino_conv: bad mask")
     y = torch.empty((N * H * W, K), dtype=torch.float32, device=x.device)
     T = (N * (H // 2) * (W // 2) + 63) // 64
     st = torch.empty((T, 2, K), dtype=torch.float32, device=x.device) if stats else None
-    r = native.kernels().ddpx_f32_wino_conv(x.data_ptr(), u.data_ptr(), y.data_ptr(), native.ptr(st),
-                                             native.ptr(bias), int(relu), N, H, W, C, K, native.stream_handle())
+    r = native.kernels().ddpx_f32_wino_conv_mask(x.data_ptr(), u.data_ptr(), y.data_ptr(), native.ptr(st),
+                                                  native.ptr(bias), int(relu), native.ptr(mask), N, H, W, C, K,
+                                                  native.stream_handle())
     native.check(r if r < 0 else 0, "ddpx_f32_wino_conv")
     return (y, (st, T, r)) if stats else y
 
@@ -710,6 +717,24 @@ def bias_act_backward(g, y, N, H, W, C, pool, plan, dbias, accumulate=False):
     return dy
 
 
+# DDPX_F32_DGRAD_MASK=1: the Winograd data gradient into a non-pooled conv + ReLU block applies that block's ReLU
+# mask in its epilogue, and the block only sums the bias gradient (colsum_bias) instead of the one-pass
+# bias_act_backward (default 0).  Measured even (profiles/r6_f32epi): the first conv's backward pass drops
+# 156 -> 49 us, but the mask read in the 128 -> 64 layer's dgrad epilogue adds 126 us (377 -> 503).
+_DGRAD_MASK = _os.environ.get("DDPX_F32_DGRAD_MASK", "0") != "0"
+
+
+def colsum_bias(dy, P, C, plan, dbias, accumulate=False):
+    """dbias (+)= sum over the P rows of dy [P, C] (fixed-order chunk sums merged by bn_bwd_finalize)."""
+    R = bn_chunk_rows(P, C)
+    T = (P + R - 1) // R
+    part = torch.empty((T, 2, C), dtype=torch.float32, device=dy.device)
+    _call("ddpx_f32_colsum_part", dy.data_ptr(), P, C, R, part.data_ptr())
+    c1, c2 = plan.scratch[:C], plan.scratch[C:2 * C]
+    _call("ddpx_f32_bn_bwd_finalize", part.data_ptr(), T, P, C, c1.data_ptr(), c2.data_ptr(), None, dbias.data_ptr(),
+          int(accumulate), native.ptr(_fin_ws(T, C, dy.device)))
+
+
 def _deepnn_forward(model, x, targets, training):
     plan = _deepnn_plan(model)
     saved = []
@@ -764,6 +789,7 @@ def _deepnn_backward(model, saved, last, dl, grad_out):
     _grad_write(flat, l0.bias, lambda o, ac: colsum(dd0, o, ac))
     _grad_write(flat, l0.weight, lambda o, ac: linear_wgrad(dd0, feat, o, ac))
     g = nchw_unflatten(linear_dgrad(dd0, l0.weight), *xshape)
+    g_masked = False  # g already through the block's ReLU (the producing dgrad's epilogue applied the mask)
     for bi in range(len(plan.blocks) - 1, -1, -1):
         conv, pool = plan.blocks[bi]
         x, y, (N, H, W, C, Co), _, wino = saved[bi]
@@ -771,14 +797,22 @@ def _deepnn_backward(model, saved, last, dl, grad_out):
 
         def bias_grad(o, ac):
             nonlocal dy
-            dy = bias_act_backward(g, y, N, H, W, Co, pool, plan, o, ac)
+            if g_masked:
+                dy = g.reshape(N * H * W, Co)
+                colsum_bias(dy, N * H * W, Co, plan, o, ac)
+            else:
+                dy = bias_act_backward(g, y, N, H, W, Co, pool, plan, o, ac)
         _grad_write(flat, conv.bias, bias_grad)
         _grad_write(flat, conv.weight, lambda o, ac: conv_wgrad(dy, x, Co, conv.weight.shape[1], o, ac))
         if bi > 0:
             if wino and plan.ud[bi] is not None:  # made by this step's forward (Winograd data gradient planned)
-                g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C).view(N, H, W, C)
+                below_pool = plan.blocks[bi - 1][1]
+                mask = saved[bi - 1][1] if _DGRAD_MASK and not below_pool else None
+                g = wino_conv(dy.view(N, H, W, Co), plan.ud[bi], C, mask=mask).view(N, H, W, C)
+                g_masked = mask is not None
             else:
                 g = conv_dgrad(dy, plan.wd[bi], N, H, W, C, Co)
+                g_masked = False
 
 
 class _DeepNNLossF32(torch.autograd.Function):

@@ -682,6 +682,30 @@ def test_conv_wgrad_32_channels_padded_winograd(gpu, accumulate):
     assert torch.all(buf[Co * Ci * 9:] == 0.25)
 
 
+def test_wino_conv_relu_mask_and_colsum_bias(gpu):
+    """The Winograd data gradient with the ReLU mask of the block below in its epilogue equals the unmasked one
+    times (mask > 0) bitwise; colsum_bias matches the fp64 column sums and accumulates."""
+    from ddpx.ops import f32
+    from ddpx.models import DeepNN
+    torch.manual_seed(8)
+    N, H, C, K = 8, 16, 64, 128
+    x = torch.randn(N, H, H, C, device=gpu)
+    w = torch.randn(K, C, 3, 3, device=gpu) / (C * 9) ** 0.5
+    u = torch.empty(16 * C * K, device=gpu)
+    f32.wino_wprep(w, u, None)
+    mask = torch.relu(torch.randn(N * H * H, K, device=gpu))
+    raw = f32.wino_conv(x, u, K)
+    got = f32.wino_conv(x, u, K, mask=mask)
+    assert torch.equal(got, torch.where(mask > 0, raw, torch.zeros_like(raw)))
+    plan = f32._deepnn_plan(DeepNN().to(gpu))
+    db = torch.full((K,), 0.5, device=gpu)
+    f32.colsum_bias(got, N * H * H, K, plan, db, accumulate=True)
+    ref = got.double().sum(0)
+    assert _rel((db - 0.5).cpu(), ref.cpu()) < 1e-6
+    f32.colsum_bias(got, N * H * H, K, plan, db)
+    assert _rel(db.cpu(), ref.cpu()) < 1e-6
+
+
 def test_vgg_fp32_runs_winograd_layers(gpu):
     """The fp32 VGG plan puts every layer with >= 64 input channels on Winograd (forward + data gradient)."""
     import ddpx
